@@ -1,0 +1,411 @@
+"""bench.py -- encode throughput of the MI355X hot path (BASELINE.json metric:
+"encode MPixels/s (and MB/s out) at 1/2/4/8 GPUs; bit-exact vs CPU").
+
+Default workload (c3, BASELINE.json configs[2], the north star's roofline config): per GPU one
+16384x16384 8-bit gray image (synthetic, device-resident) -> 8 bitplanes -> med residual ->
+per-row runs -> Golomb stream AND EG stream for every plane. MPix = binary pixels =
+rows*cols*planes. N GPUs = N independent images (weak scaling, no data-path collective).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
+
+Multi-GPU: launched by torch.distributed.run, one rank per GPU (RCCL = backend "nccl").
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "binary-image-compression_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "encode MPixels/s (and MB/s out) at 1/2/4/8 GPUs; bit-exact vs CPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--rows", type=int, default=0, help="override image rows (c3/c2/c5)")
+    ap.add_argument("--cols", type=int, default=0, help="override image cols")
+    ap.add_argument("--cpu-rows", type=int, default=4096, help="rows per plane in the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    import torch
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def load_pmc(workload, kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def rand_words(t, shape, dev, g):
+    """uniform 64-bit words (Bernoulli(0.5) pixels) as int64, generated on the device."""
+    n = int(np.prod(shape))
+    return t.randint(0, 256, (n * 8,), dtype=t.uint8, device=dev, generator=g).view(t.int64).view(*shape)
+
+
+# ------------------------------------------------------------------------------------------
+class C3:
+    """gray image -> 8 bitplanes -> med -> Golomb + EG (per GPU)."""
+
+    def __init__(self, ctx, args, rank):
+        import pybic
+        t = ctx.torch
+        self.ctx, self.pybic = ctx, pybic
+        self.rows = args.rows or 16384
+        self.cols = args.cols or 16384
+        self.nplanes = 8
+        g = t.Generator(device=ctx.dev)
+        g.manual_seed(0x5EED0000 + rank)
+        # two gray buffers, alternated per step, so the Infinity Cache cannot serve re-runs
+        self.gray = [t.randint(0, 256, (self.rows, self.cols), dtype=t.uint8, device=ctx.dev, generator=g)
+                     for _ in range(2)]
+        self.wpr = (self.cols + 63) // 64
+        self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr)
+        self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
+        self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
+        self.out_g = ctx.empty_i64(self.nplanes, self.slot_g)
+        self.out_e = ctx.empty_i64(self.nplanes, self.slot_e)
+        self.bits_g = ctx.empty_i64(self.nplanes)
+        self.bits_e = ctx.empty_i64(self.nplanes)
+        ctx.reserve(self.nplanes, self.rows, self.cols)
+        self.k = 0
+        self.pixels = self.rows * self.cols * self.nplanes
+        self.workload = (f"c3: {self.rows}x{self.cols} 8-bit gray -> 8 bitplanes -> med -> per-row runs "
+                         f"-> Golomb + EG streams per plane")
+
+    def step(self):
+        c, p = self.ctx, self.pybic
+        c.bitplanes_u8(self.gray[self.k & 1], nplanes=8, out=self.planes)
+        c.encode_planes(self.planes, self.cols, True, p.CODER_GOLOMB, self.slot_g, self.out_g, self.bits_g)
+        c.encode_planes(self.planes, self.cols, True, p.CODER_EG, self.slot_e, self.out_e, self.bits_e)
+        self.k += 1
+
+    def out_bytes(self):
+        b = self.pybic.as_u64(self.bits_g).astype(np.int64).sum() + self.pybic.as_u64(self.bits_e).astype(np.int64).sum()
+        return int(b) / 8.0
+
+    def kernel_bytes(self):
+        """algorithmic bytes per launch."""
+        plane_b = self.nplanes * self.rows * self.wpr * 8
+        g = int(self.pybic.as_u64(self.bits_g).astype(np.int64).sum()) // 8
+        e = int(self.pybic.as_u64(self.bits_e).astype(np.int64).sum()) // 8
+        return {"bitplanes_u8": self.rows * self.cols + plane_b, "med_count": plane_b, "golomb_bits": plane_b,
+                "golomb_emit": plane_b + g, "eg_emit": plane_b + e}
+
+    def host_planes(self, rows):
+        return self.pybic.as_u64(self.planes[:, :rows])
+
+    def check(self, oracle):
+        """plane 0 of the last step: Golomb and EG streams == the oracle's."""
+        P = self.pybic.as_u64(self.planes[0])
+        ok = True
+        for coder, out, bits in ((0, self.out_g, self.bits_g), (1, self.out_e, self.bits_e)):
+            eb, est, _ = oracle.encode_plane(P, self.cols, 1, coder)
+            nb = int(self.pybic.as_u64(bits)[0])
+            ok &= (nb == eb) and self.pybic.stream_bytes(out[0], nb) == est.tobytes()
+        return ok
+
+
+class C2(C3):
+    """one 4096x4096 bitplane, Golomb on the raw plane (no predictor)."""
+
+    def __init__(self, ctx, args, rank):
+        import pybic
+        t = ctx.torch
+        self.ctx, self.pybic = ctx, pybic
+        self.rows = args.rows or 4096
+        self.cols = args.cols or 4096
+        self.nplanes = 1
+        self.wpr = (self.cols + 63) // 64
+        g = t.Generator(device=ctx.dev)
+        g.manual_seed(0x5EED0000 + rank)
+        self.planes_in = [rand_words(t, (1, self.rows, self.wpr), ctx.dev, g) for _ in range(2)]
+        self.planes = self.planes_in[0]
+        self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
+        self.out_g = ctx.empty_i64(1, self.slot_g)
+        self.bits_g = ctx.empty_i64(1)
+        self.out_e, self.bits_e = None, ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
+        ctx.reserve(1, self.rows, self.cols)
+        self.k = 0
+        self.pixels = self.rows * self.cols
+        self.workload = f"c2: one {self.rows}x{self.cols} bitplane, Golomb-only (raw runs, no predictor)"
+
+    def step(self):
+        self.planes = self.planes_in[self.k & 1]
+        self.ctx.encode_planes(self.planes, self.cols, False, self.pybic.CODER_GOLOMB, self.slot_g, self.out_g,
+                               self.bits_g)
+        self.k += 1
+
+    def kernel_bytes(self):
+        plane_b = self.rows * self.wpr * 8
+        g = int(self.pybic.as_u64(self.bits_g)[0]) // 8
+        return {"med_count": plane_b, "golomb_bits": plane_b, "golomb_emit": plane_b + g}
+
+    def check(self, oracle):
+        P = self.pybic.as_u64(self.planes[0])
+        eb, est, _ = oracle.encode_plane(P, self.cols, 0, 0)
+        nb = int(self.pybic.as_u64(self.bits_g)[0])
+        return nb == eb and self.pybic.stream_bytes(self.out_g[0], nb) == est.tobytes()
+
+
+class C4(C3):
+    """64 independent 4096x4096 frames sharded over the ranks (strong scaling), med + Golomb,
+    streams packed per rank and gathered to rank 0 over RCCL."""
+
+    def __init__(self, ctx, args, rank, world):
+        import pybic
+        t = ctx.torch
+        self.ctx, self.pybic, self.rank, self.world = ctx, pybic, rank, world
+        self.rows = args.rows or 4096
+        self.cols = args.cols or 4096
+        total = 64
+        lo, hi = rank * total // world, (rank + 1) * total // world
+        self.nplanes = hi - lo
+        self.wpr = (self.cols + 63) // 64
+        g = t.Generator(device=ctx.dev)
+        g.manual_seed(0x5EED0000 + rank)
+        self.planes = rand_words(t, (self.nplanes, self.rows, self.wpr), ctx.dev, g)
+        self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
+        self.out_g = ctx.empty_i64(self.nplanes, self.slot_g)
+        self.bits_g = ctx.empty_i64(self.nplanes)
+        self.bits_e = ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
+        self.packed = ctx.empty_i64(self.nplanes * self.slot_g)
+        self.word_off = ctx.empty_i64(self.nplanes + 1)
+        self.gathered = None
+        ctx.reserve(self.nplanes, self.rows, self.cols)
+        self.k = 0
+        self.pixels = self.rows * self.cols * self.nplanes
+        self.workload = (f"c4: 64 frames {self.rows}x{self.cols} sharded over ranks, med -> Golomb, "
+                         f"per-rank packed streams gathered to rank 0 (RCCL)")
+
+    def step(self):
+        from pybic.parallel import gather_streams
+        c, p = self.ctx, self.pybic
+        c.encode_planes(self.planes, self.cols, True, p.CODER_GOLOMB, self.slot_g, self.out_g, self.bits_g)
+        self.packed, self.word_off = c.pack_streams(self.out_g, self.bits_g)
+        if self.world > 1:
+            self.gathered = gather_streams(self.packed, self.word_off[-1:], self.world, self.rank)
+        self.k += 1
+
+    def kernel_bytes(self):
+        plane_b = self.nplanes * self.rows * self.wpr * 8
+        g = int(self.pybic.as_u64(self.bits_g).astype(np.int64).sum()) // 8
+        return {"med_count": plane_b, "golomb_bits": plane_b, "golomb_emit": plane_b + g}
+
+    def check(self, oracle):
+        P = self.pybic.as_u64(self.planes[0])
+        eb, est, _ = oracle.encode_plane(P, self.cols, 1, 0)
+        nb = int(self.pybic.as_u64(self.bits_g)[0])
+        return nb == eb and self.pybic.stream_bytes(self.out_g[0], nb) == est.tobytes()
+
+
+class C5(C3):
+    """8192x8192 plane, 32x32 tiles (compress7 R = 0 path): weights, mode, Golomb over tiles."""
+
+    def __init__(self, ctx, args, rank):
+        import pybic
+        t = ctx.torch
+        self.ctx, self.pybic = ctx, pybic
+        self.rows = args.rows or 8192
+        self.cols = args.cols or 8192
+        self.W = 32
+        self.nplanes = 1
+        self.wpr = (self.cols + 63) // 64
+        g = t.Generator(device=ctx.dev)
+        g.manual_seed(0x5EED0000 + rank)
+        self.planes = rand_words(t, (1, self.rows, self.wpr), ctx.dev, g)
+        self.lt = pybic.lentab(self.W)
+        self.res = None
+        self.k = 0
+        self.pixels = self.rows * self.cols
+        self.bits_e = ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
+        self.workload = f"c5: {self.rows}x{self.cols} plane, 32x32 tiles, per-tile med/mode + Golomb over weights"
+
+    def step(self):
+        self.res = self.ctx.patch_encode(self.planes[0], self.cols, self.W, self.lt, want_resid=True)
+        self.k += 1
+
+    def out_bytes(self):
+        return int(self.pybic.as_u64(self.res["stats"])[0]) / 8.0
+
+    def kernel_bytes(self):
+        return {"tiles": 2 * self.rows * self.wpr * 8}
+
+    def check(self, oracle):
+        P = self.pybic.as_u64(self.planes[0])
+        exp = oracle.patch_encode(P, self.cols, self.W, self.lt, want_stream=True)
+        st = self.pybic.as_u64(self.res["stats"])
+        return int(st[0]) == exp["bits"] and int(st[2]) == exp["L"]
+
+
+# ------------------------------------------------------------------------------------------
+def cpu_baseline(wl, args):
+    """The reference's own bit-serial med + GolombCoder + EGCoder (oracle/_ref, kind
+    "reference") -- or the oracle restatement ("port") where _ref was not built -- on a bounded
+    sample of the same workload, OpenMP over independent planes, on this host's cores."""
+    from oracle_lib import Oracle, Ref, have_ref
+    rows = min(args.cpu_rows, wl.rows)
+    planes = np.ascontiguousarray(wl.host_planes(rows)) if hasattr(wl, "host_planes") else None
+    if planes is None:
+        return None
+    nplanes = planes.shape[0]
+    threads = max(1, min(nplanes, int(os.environ.get("OMP_NUM_THREADS", "8") or 8)))
+    do_eg = 1 if isinstance(wl, C3) and type(wl) is C3 else 0
+    predict = 0 if isinstance(wl, C2) else 1
+    if have_ref():
+        dt, gb, eb, used = Ref().baseline(planes, rows, wl.cols, predict=predict, do_eg=do_eg, threads=threads)
+        kind = "reference"
+    else:
+        import ctypes as C
+        o = Oracle()
+        used_c = C.c_int(0)
+        t0 = time.perf_counter()
+        o.lib.bo_baseline_planes(planes.ctypes.data_as(C.POINTER(C.c_uint64)), nplanes, rows, wl.cols,
+                                 planes.shape[-1], predict, do_eg, C.byref(used_c))
+        dt, used, kind = time.perf_counter() - t0, used_c.value, "port"
+    px = nplanes * rows * wl.cols
+    return {"value": px / dt / 1e6, "unit": "MPix/s", "cores": int(min(used, nplanes)), "kind": kind,
+            "sample": f"{nplanes} planes x {rows} rows x {wl.cols} cols (first {rows} rows of the bench input), "
+                      f"{'med+Golomb+EG' if do_eg else ('med+Golomb' if predict else 'Golomb')}, "
+                      f"OpenMP over planes, {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    world, rank, local = dist_setup(args)
+    import pybic
+    ctx = pybic.Context(local)
+    if args.workload == "c3":
+        wl = C3(ctx, args, rank)
+    elif args.workload == "c2":
+        wl = C2(ctx, args, rank)
+    elif args.workload == "c4":
+        wl = C4(ctx, args, rank, world)
+    else:
+        wl = C5(ctx, args, rank)
+    dev = ctx.dev
+    for _ in range(args.warmup):
+        wl.step()
+    ctx.sync()
+    barrier(world)
+    ctx.prof_enable(True)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    ctx.sync()
+    prof = ctx.prof_collect()
+    ctx.prof_enable(False)
+    dt_max = max_over_ranks(dt, world, dev)
+    pixels_all = sum_over_ranks(float(wl.pixels), world, dev) * args.steps
+    out_all = sum_over_ranks(wl.out_bytes(), world, dev) * args.steps
+    value = pixels_all / dt_max / 1e6
+    # dominant kernel and its roofline (algorithmic bytes / measured average launch time)
+    kb = wl.kernel_bytes()
+    timed = {k: v for k, v in prof.items() if k in kb}
+    dom = max(timed, key=lambda k: timed[k][1]) if timed else None
+    roof = None
+    per_kernel = {k: {"launches": n, "avg_us": 1e3 * ms / max(n, 1)} for k, (n, ms) in prof.items()}
+    if dom:
+        n, ms = timed[dom]
+        avg_s = ms / 1e3 / n
+        ach = kb[dom] / avg_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc(args.workload, dom), "kernel": dom,
+                "algorithmic_bytes_per_launch": kb[dom], "avg_launch_us": round(avg_s * 1e6, 2)}
+    pred_pass = None
+    if "med_count" in timed:
+        n, ms = timed["med_count"]
+        avg_s = ms / 1e3 / n
+        pred_pass = {"kernel": "med_count", "achieved": round(kb["med_count"] / avg_s / 1e9, 1),
+                     "frac": round(kb["med_count"] / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "avg_launch_us": round(avg_s * 1e6, 2), "traffic": load_pmc(args.workload, "med_count")}
+    ok = None
+    cpu = None
+    if rank == 0 and not args.no_check:
+        from oracle_lib import Oracle
+        ok = bool(wl.check(Oracle()))
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(wl, args)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong" if args.workload == "c4" else "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (seeded uniform bytes / Bernoulli(0.5) words, device-resident)",
+            "config": {"workload": wl.workload, "rows": wl.rows, "cols": wl.cols, "planes_per_gpu": wl.nplanes,
+                       "parallelism": f"dp{world} (independent images per GPU)" if args.workload != "c4"
+                       else f"dp{world} (64 frames sharded)"},
+            "mb_per_s_out": round(out_all / dt_max / 1e6, 1),
+            "gray_mpix_per_s": round(value / 8, 1) if args.workload == "c3" else None,
+            "roofline": roof, "predictor_pass": pred_pass, "kernels": per_kernel,
+            "bit_exact_check": ok, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    ctx.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

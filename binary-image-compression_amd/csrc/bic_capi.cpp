@@ -1,0 +1,394 @@
+// bic_capi.cpp -- the C ABI of include/bic.h: argument validation (the reference's asserts
+// become BIC_EINVAL), the per-device context (stream, scratch arena, deferred-error flags)
+// and the launch sequences. Compiled with hipcc for gfx950; no CPU fallback exists: without a
+// gfx950 device every entry point fails with BIC_ENODEV.
+#include "bic.h"
+#include "bic_internal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+struct bic_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t cur = nullptr;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  uint32_t* flags = nullptr;      // device [2]: overflow, domain
+  uint64_t* lentab = nullptr;     // device copy of the tile length table
+  size_t lentab_cap = 0;          // entries
+  uint64_t* staging = nullptr;    // pinned host staging for lentab
+  size_t staging_cap = 0;         // entries
+  // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
+  bool prof_on = false;
+  struct Rec { const char* name; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+};
+
+namespace {
+
+#define BIC_HIP(x)                                  \
+  do {                                              \
+    if ((x) != hipSuccess) return BIC_EDEVICE;      \
+  } while (0)
+
+hipEvent_t take_event(bic_ctx* ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Runs one launch, bracketed by events when profiling is on.
+template <typename F>
+void timed(bic_ctx* ctx, const char* name, F&& launch) {
+  if (!ctx->prof_on) {
+    launch();
+    return;
+  }
+  hipEvent_t a = take_event(ctx), b = take_event(ctx);
+  (void)hipEventRecord(a, ctx->cur);
+  launch();
+  (void)hipEventRecord(b, ctx->cur);
+  ctx->recs.push_back({name, a, b});
+}
+
+int bind(bic_ctx* ctx) {
+  if (!ctx) return BIC_EINVAL;
+  BIC_HIP(hipSetDevice(ctx->device));
+  return BIC_OK;
+}
+
+int ensure_scratch(bic_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return BIC_OK;
+  BIC_HIP(hipStreamSynchronize(ctx->cur));  // earlier calls may still use the old arena
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  ctx->scratch = nullptr;
+  ctx->scratch_bytes = 0;
+  const size_t want = bytes + bytes / 4 + 4096;
+  if (hipMalloc(&ctx->scratch, want) != hipSuccess) {
+    ctx->scratch = nullptr;
+    return BIC_ENOMEM;
+  }
+  ctx->scratch_bytes = want;
+  return BIC_OK;
+}
+
+bool geom_ok(size_t rows, size_t cols, size_t wpr) {
+  if (cols == 0 || rows > 0x7fffffffu || cols > 0x7ffffffeu) return false;
+  if (wpr < (cols + 63) / 64 || wpr > 0xffffffffu) return false;
+  // the reference's 32-bit coder state (Golomb.h:21-24) is only defined while the sample
+  // count and accumulated error stay below 2^31: both are bounded by rows*(cols+1).
+  return (unsigned long long)rows * (cols + 1) < 0x80000000ull;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* bic_strerror(int code) {
+  switch (code) {
+    case BIC_OK: return "ok";
+    case BIC_EINVAL: return "invalid argument";
+    case BIC_ENOMEM: return "device allocation failed";
+    case BIC_EDEVICE: return "HIP runtime error";
+    case BIC_ENOSPC: return "output slot too small";
+    case BIC_ENODEV: return "no gfx950 device";
+    default: return "unknown error";
+  }
+}
+
+int bic_device_count(int* n) {
+  if (!n) return BIC_EINVAL;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return BIC_OK;
+}
+
+int bic_ctx_create(int device, bic_ctx** out) {
+  if (!out) return BIC_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return BIC_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return BIC_EDEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return BIC_ENODEV;  // built for gfx950 only
+  BIC_HIP(hipSetDevice(device));
+  bic_ctx* ctx = new (std::nothrow) bic_ctx();
+  if (!ctx) return BIC_ENOMEM;
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return BIC_EDEVICE;
+  }
+  ctx->cur = ctx->own;
+  if (hipMalloc(&ctx->flags, 2 * sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(ctx->flags, 0, 2 * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+    return BIC_ENOMEM;
+  }
+  *out = ctx;
+  return BIC_OK;
+}
+
+int bic_ctx_destroy(bic_ctx* ctx) {
+  if (!ctx) return BIC_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->cur);
+  for (auto& r : ctx->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (auto e : ctx->pool) (void)hipEventDestroy(e);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->flags) (void)hipFree(ctx->flags);
+  if (ctx->lentab) (void)hipFree(ctx->lentab);
+  if (ctx->staging) (void)hipHostFree(ctx->staging);
+  if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+  return BIC_OK;
+}
+
+int bic_ctx_set_stream(bic_ctx* ctx, void* hip_stream) {
+  if (!ctx) return BIC_EINVAL;
+  ctx->cur = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own;
+  return BIC_OK;
+}
+
+void* bic_ctx_get_stream(bic_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->cur) : nullptr; }
+
+int bic_sync(bic_ctx* ctx) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  BIC_HIP(hipStreamSynchronize(ctx->cur));
+  BIC_HIP(hipGetLastError());
+  uint32_t f[2] = {0, 0};
+  BIC_HIP(hipMemcpy(f, ctx->flags, sizeof(f), hipMemcpyDeviceToHost));
+  if (f[0] || f[1]) BIC_HIP(hipMemset(ctx->flags, 0, sizeof(f)));
+  if (f[1]) return BIC_EINVAL;
+  if (f[0]) return BIC_ENOSPC;
+  return BIC_OK;
+}
+
+int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (nplanes < 1 || !geom_ok(rows, cols, (cols + 63) / 64)) return BIC_EINVAL;
+  const bic::Geom g = bic::make_geom(rows, cols, (cols + 63) / 64, nplanes);
+  return ensure_scratch(ctx, bic::chunk_scratch_bytes(g));
+}
+
+int bic_bitplanes_u8(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols,
+                     int nplanes, uint64_t* planes, size_t wpr) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!gray || !planes || nplanes < 1 || nplanes > 8 || pitch < cols) return BIC_EINVAL;
+  if (!geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (rows == 0) return BIC_OK;
+  timed(ctx, "bitplanes_u8", [&] {
+    bic::launch_bitplanes_u8(ctx->cur, gray, pitch, (uint32_t)rows, (uint32_t)cols, nplanes, planes,
+                             (uint32_t)wpr);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_med_residual(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                     size_t wpr, int predict, uint64_t* resid, uint64_t* weight_out) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!planes || nplanes < 1 || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (weight_out) BIC_HIP(hipMemsetAsync(weight_out, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+  if (rows == 0) return BIC_OK;
+  const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
+  if ((rc = ensure_scratch(ctx, bic::chunk_scratch_bytes(g)))) return rc;
+  const bic::ChunkScratch cs = bic::carve_chunk_scratch(ctx->scratch, g);
+  timed(ctx, "med_count", [&] { bic::launch_count(ctx->cur, g, planes, predict ? 1 : 0, cs, resid, weight_out); });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+size_t bic_encode_slot_words(size_t rows, size_t cols, int coder) {
+  const unsigned long long base = (unsigned long long)rows * (cols + 1);
+  if (coder == BIC_CODER_EG) return (size_t)((base + 1 + 63) / 64);
+  return (size_t)((2 * base + 63) / 64 + 64);
+}
+
+int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                      size_t wpr, int predict, int coder, uint64_t* out, size_t slot_words,
+                      uint64_t* plane_bits) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!planes || !out || !plane_bits || nplanes < 1 || slot_words == 0) return BIC_EINVAL;
+  if (coder != BIC_CODER_GOLOMB && coder != BIC_CODER_EG) return BIC_EINVAL;
+  if (!geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (rows == 0) {
+    BIC_HIP(hipMemsetAsync(plane_bits, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+    return BIC_OK;
+  }
+  const int pr = predict ? 1 : 0;
+  const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
+  if ((rc = ensure_scratch(ctx, bic::chunk_scratch_bytes(g)))) return rc;
+  const bic::ChunkScratch cs = bic::carve_chunk_scratch(ctx->scratch, g);
+  timed(ctx, "med_count", [&] { bic::launch_count(ctx->cur, g, planes, pr, cs, nullptr, nullptr); });
+  timed(ctx, "scan_rows", [&] { bic::launch_scan_rows(ctx->cur, g, cs); });
+  if (coder == BIC_CODER_GOLOMB) {
+    timed(ctx, "golomb_bits", [&] { bic::launch_golomb_bits(ctx->cur, g, planes, pr, cs); });
+    timed(ctx, "golomb_offsets", [&] {
+      bic::launch_golomb_offsets(ctx->cur, g, cs, out, slot_words, plane_bits, ctx->flags);
+    });
+    timed(ctx, "golomb_emit", [&] { bic::launch_golomb_emit(ctx->cur, g, planes, pr, cs, out, slot_words); });
+  } else {
+    timed(ctx, "eg_emit", [&] {
+      bic::launch_eg_emit(ctx->cur, g, planes, pr, cs, out, slot_words, plane_bits, ctx->flags);
+    });
+  }
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_golomb_encode_samples(bic_ctx* ctx, const uint32_t* samples, size_t n, uint64_t n0,
+                              uint64_t a0, unsigned bit0, uint64_t* out, size_t cap_words,
+                              uint64_t* bits_out) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if ((!samples && n) || !out || !bits_out || bit0 >= 64 || cap_words == 0) return BIC_EINVAL;
+  if (n0 + n >= 0x80000000ull || a0 >= 0x80000000ull) return BIC_EINVAL;
+  if ((rc = ensure_scratch(ctx, bic::sample_scratch_bytes(n)))) return rc;
+  const bic::SampleScratch ss = bic::carve_sample_scratch(ctx->scratch, n);
+  timed(ctx, "golomb_samples", [&] {
+    bic::launch_golomb_samples(ctx->cur, samples, n, n0, a0, bit0, out, cap_words, bits_out, ss, ctx->flags);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
+                     unsigned W, const uint64_t* lentab, uint32_t* weights, uint32_t* w_nonpred,
+                     uint32_t* w_pred, uint8_t* modes, uint64_t* resid, uint64_t* stream,
+                     size_t cap_words, uint64_t* stats) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!plane || !lentab || !stream || !stats || cap_words == 0) return BIC_EINVAL;
+  if (W < 1 || W > 64 || rows % W || cols % W || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  const size_t M = (size_t)W * W;
+  const size_t ntiles = (rows / W) * (cols / W);
+  if (ntiles >= 0x80000000ull || (unsigned long long)ntiles * M >= 0x80000000ull) return BIC_EINVAL;
+  // length table -> device (pinned staging; the previous copy must be done before reuse)
+  if (ctx->staging_cap < M + 1) {
+    BIC_HIP(hipStreamSynchronize(ctx->cur));
+    if (ctx->staging) (void)hipHostFree(ctx->staging);
+    if (ctx->lentab) (void)hipFree(ctx->lentab);
+    ctx->staging = nullptr;
+    ctx->lentab = nullptr;
+    ctx->staging_cap = ctx->lentab_cap = 0;
+    if (hipHostMalloc(&ctx->staging, (M + 1) * sizeof(uint64_t)) != hipSuccess) return BIC_ENOMEM;
+    if (hipMalloc(&ctx->lentab, (M + 1) * sizeof(uint64_t)) != hipSuccess) return BIC_ENOMEM;
+    ctx->staging_cap = ctx->lentab_cap = M + 1;
+  } else {
+    BIC_HIP(hipStreamSynchronize(ctx->cur));
+  }
+  std::memcpy(ctx->staging, lentab, (M + 1) * sizeof(uint64_t));
+  BIC_HIP(hipMemcpyAsync(ctx->lentab, ctx->staging, (M + 1) * sizeof(uint64_t),
+                         hipMemcpyHostToDevice, ctx->cur));
+  // per-tile chosen weights feed the sample coder: use the caller's array or scratch
+  const size_t wbytes = ((ntiles * sizeof(uint32_t)) + 255) & ~(size_t)255;
+  if ((rc = ensure_scratch(ctx, wbytes + bic::sample_scratch_bytes(ntiles)))) return rc;
+  uint32_t* wts = weights ? weights : reinterpret_cast<uint32_t*>(ctx->scratch);
+  const bic::SampleScratch ss =
+      bic::carve_sample_scratch(reinterpret_cast<char*>(ctx->scratch) + wbytes, ntiles);
+  BIC_HIP(hipMemsetAsync(stats, 0, 3 * sizeof(uint64_t), ctx->cur));
+  if (resid) BIC_HIP(hipMemsetAsync(resid, 0, rows * wpr * sizeof(uint64_t), ctx->cur));
+  timed(ctx, "tiles", [&] {
+    bic::launch_tiles(ctx->cur, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, W, ctx->lentab, wts,
+                      w_nonpred, w_pred, modes, resid, stats);
+  });
+  timed(ctx, "golomb_samples", [&] {
+    bic::launch_golomb_samples(ctx->cur, wts, ntiles, 0, 0, 0, stream, cap_words, stats, ss, ctx->flags);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_pack_streams(bic_ctx* ctx, const uint64_t* slots, int nplanes, size_t slot_words,
+                     const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!slots || !plane_bits || !dst || !word_off || nplanes < 1 || nplanes > 65535 || slot_words == 0)
+    return BIC_EINVAL;
+  timed(ctx, "pack", [&] { bic::launch_pack(ctx->cur, slots, nplanes, slot_words, plane_bits, dst, word_off); });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+// log2 C(n, r): the reference's enumL / enumerative_codelength (coding.cpp:19-22,
+// compress7_test.cpp:25-28) without GSL. Exact at r in {0, n} (0) and, for power-of-two n,
+// at r in {1, n-1} (log2 n -- where GSL's last-ulp rounding is unpinned, SURVEY.md §8 c);
+// long-double lgamma elsewhere.
+double bic_enum_codelength(unsigned n, unsigned r) {
+  if (r == 0 || r >= n) return 0.0;
+  const unsigned m = r * 2 > n ? n - r : r;
+  if (m == 1) {
+    if ((n & (n - 1)) == 0) {
+      unsigned e = 0;
+      while ((1u << e) < n) ++e;
+      return (double)e;
+    }
+    return (double)std::log2((long double)n);
+  }
+  const long double ln = std::lgamma((long double)n + 1.0L) - std::lgamma((long double)m + 1.0L) -
+                         std::lgamma((long double)(n - m) + 1.0L);
+  return (double)(ln * 1.442695040888963407359924681001892137L);
+}
+
+int bic_tile_lentab(unsigned W, uint64_t* lentab) {
+  if (W < 1 || W > 64 || !lentab) return BIC_EINVAL;
+  const unsigned M = W * W;
+  for (unsigned w = 0; w <= M; ++w)  // compress7_test.cpp:220-221: (idx_t)(1 + 1 + enumL(M, w))
+    lentab[w] = (uint64_t)(2.0 + bic_enum_codelength(M, w));
+  return BIC_OK;
+}
+
+int bic_prof_enable(bic_ctx* ctx, int on) {
+  if (!ctx) return BIC_EINVAL;
+  ctx->prof_on = on != 0;
+  return BIC_OK;
+}
+
+int bic_prof_collect(bic_ctx* ctx, char* buf, size_t cap) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!buf || cap == 0) return BIC_EINVAL;
+  BIC_HIP(hipStreamSynchronize(ctx->cur));
+  std::map<std::string, std::pair<unsigned long, double>> agg;
+  for (auto& r : ctx->recs) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = -1.f;
+    auto& e = agg[r.name];
+    e.first += 1;
+    e.second += ms;
+    ctx->pool.push_back(r.a);
+    ctx->pool.push_back(r.b);
+  }
+  ctx->recs.clear();
+  std::string outs;
+  for (auto& kv : agg) {
+    char line[160];
+    std::snprintf(line, sizeof line, "%s %lu %.6f\n", kv.first.c_str(), kv.second.first, kv.second.second);
+    outs += line;
+  }
+  std::snprintf(buf, cap, "%s", outs.c_str());
+  return outs.size() < cap ? BIC_OK : BIC_ENOSPC;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// bic_internal.h -- shared between the HIP kernels (bic_kernels.hip) and the C ABI
+// (bic_capi.cpp). Not installed; the public surface is include/bic.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace bic {
+
+// Geometry of one batch of planes as the chunk kernels see it. A "chunk" is the unit
+// one wavefront processes: up to 64*WPL consecutive words of ONE row (lane l handles
+// words c0 + 64*t + l for t < WPL, so every load instruction is 512 contiguous bytes).
+struct Geom {
+  uint32_t rows, cols, wpr;
+  uint32_t used;  // ceil(cols/64): words that hold pixels
+  uint32_t wpl;   // words per lane (1, 2 or 4)
+  uint32_t wpc;   // words per chunk = 64*wpl
+  uint32_t cpr;   // chunks per row = ceil(used/wpc)
+  uint32_t nplanes;
+  uint64_t trail;             // valid-bit mask of word used-1 (binmat.cpp:146-147)
+  uint64_t plane_words;       // rows*wpr
+  uint64_t chunks_per_plane;  // rows*cpr
+  uint64_t nchunks;           // nplanes*chunks_per_plane
+  uint64_t words_used;        // rows*used per plane (word_bits stride)
+};
+
+Geom make_geom(size_t rows, size_t cols, size_t wpr, int nplanes);
+
+// Per-call device scratch carved from the context arena.
+struct ChunkScratch {
+  uint32_t* ones;      // [nchunks]
+  int32_t* last;       // [nchunks] last 1-column in the chunk, -1 if none
+  int32_t* first;      // [nchunks] first 1-column in the chunk, INT32_MAX if none
+  uint32_t* nbase;     // [nchunks] global sample index of the chunk's first 1
+  int32_t* jprev;      // [nchunks] column of the last 1 before the chunk in its row, -1
+  uint64_t* bits;      // [nchunks] Golomb bits of the chunk
+  uint64_t* boff;      // [nchunks] absolute bit offset of the chunk in `out`
+  uint32_t* word_bits; // [nplanes*rows*used]
+  uint64_t* plane_F;   // [nplanes] raster index of the plane's first residual 1 (~0 if none)
+  uint64_t* plane_ones;// [nplanes]
+};
+size_t chunk_scratch_bytes(const Geom& g);
+ChunkScratch carve_chunk_scratch(void* base, const Geom& g);
+
+// Launchers (all asynchronous on `s`). flags[0] = overflow, flags[1] = domain error.
+void launch_bitplanes_u8(hipStream_t s, const uint8_t* gray, size_t pitch, uint32_t rows,
+                         uint32_t cols, int nplanes, uint64_t* planes, uint32_t wpr);
+void launch_count(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                  const ChunkScratch& cs, uint64_t* resid, uint64_t* weight_out);
+void launch_scan_rows(hipStream_t s, const Geom& g, const ChunkScratch& cs);
+void launch_golomb_bits(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                        const ChunkScratch& cs);
+void launch_golomb_offsets(hipStream_t s, const Geom& g, const ChunkScratch& cs, uint64_t* out,
+                           uint64_t slot_words, uint64_t* plane_bits, uint32_t* flags);
+void launch_golomb_emit(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                        const ChunkScratch& cs, uint64_t* out, uint64_t slot_words);
+void launch_eg_emit(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                    const ChunkScratch& cs, uint64_t* out, uint64_t slot_words,
+                    uint64_t* plane_bits, uint32_t* flags);
+
+// Sample coder (GolombCoder::codeSample over an array).
+struct SampleScratch {
+  uint64_t* blk_sum;   // [nblk]
+  uint64_t* blk_A;     // [nblk]
+  uint64_t* blk_bits;  // [nblk]
+  uint64_t* blk_off;   // [nblk]
+};
+size_t sample_scratch_bytes(size_t n);
+SampleScratch carve_sample_scratch(void* base, size_t n);
+void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uint64_t n0,
+                           uint64_t a0, unsigned bit0, uint64_t* out, size_t cap_words,
+                           uint64_t* bits_out, const SampleScratch& ss, uint32_t* flags);
+
+// Tiles (compress7 R = 0 path).
+void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols,
+                  uint32_t wpr, uint32_t W, const uint64_t* lentab_dev, uint32_t* weights,
+                  uint32_t* w_nonpred, uint32_t* w_pred, uint8_t* modes, uint64_t* resid,
+                  uint64_t* stats);
+
+void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
+                 const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
+
+}  // namespace bic

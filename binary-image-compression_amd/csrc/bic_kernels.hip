@@ -1,0 +1,1074 @@
+// bic_kernels.hip -- hand-written gfx950 (CDNA4) kernels for the hot path of
+// nacho-pancho/binary-image-compression. Integer/bitwise only: no MFMA. Every kernel
+// is HBM- or VALU-bound; loads are laid out so one wave instruction moves 512
+// contiguous bytes, and chunk kernels remap blockIdx so neighbouring rows (which
+// re-read each other as the "row above") stay on one XCD's L2.
+//
+// Reference semantics restated here (file:line under /root/reference/src):
+//   med (pred.cpp:3-15)         word form: R = P ^ U ^ (P>>1|Pl<<63) ^ (U>>1|Ul<<63),
+//                               R(0,0) = 0, pad bits 0
+//   GolombCoder (GolombCoder.cpp:13-34, Golomb.h:14-19)
+//                               k_0 = 1; after n samples with sum A: k = min{k : n<<k >= A}
+//   EGCoder as written (eg.cpp:20-37)  len+1 bits per run, +1 on the first non-EOL run
+//   bitplanes (bitplane_tool.cpp:24-30)
+//   tile path (compress7_test.cpp:184-275 with R = 0)
+#include "bic_internal.h"
+
+#include <climits>
+
+namespace bic {
+
+#define BIC_MSB 0x8000000000000000ull
+constexpr int kBlock = 256;   // 4 waves
+constexpr int kWaves = kBlock / 64;
+constexpr int kLdsWords = 1024;  // u32 staging words per wave in the emitter (32768 bits)
+
+// ------------------------------------------------------------------------------------
+// wave / block primitives (wave64)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((unsigned)(v & 0xffffffffu), src);
+  const uint32_t hi = __shfl((unsigned)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+  const uint32_t lo = __shfl_up((unsigned)(v & 0xffffffffu), d);
+  const uint32_t hi = __shfl_up((unsigned)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_incl_sum_u64(uint64_t x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = shfl_up_u64(x, d);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_incl_max(int x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (l >= d) x = max(x, y);
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += shfl_u64(x, lane_id() ^ d);
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  return x;
+}
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = max(x, __shfl_xor(x, d));
+  return x;
+}
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d));
+  return x;
+}
+
+// Exclusive block scan for blockDim.x <= 1024 (<= 16 waves). tmp: >= 17 entries of LDS.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T x, T* tmp, T& total) {
+  const int l = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T inc;
+  if constexpr (sizeof(T) == 8) inc = wave_incl_sum_u64(x);
+  else inc = wave_incl_sum_u32(x);
+  if (l == 63) tmp[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    const T v = l < nw ? tmp[l] : T(0);
+    T vi;
+    if constexpr (sizeof(T) == 8) vi = wave_incl_sum_u64(v);
+    else vi = wave_incl_sum_u32(v);
+    if (l < nw) tmp[l] = vi - v;
+    if (l == nw - 1) tmp[16] = vi;
+  }
+  __syncthreads();
+  const T res = tmp[w] + inc - x;
+  total = tmp[16];
+  __syncthreads();
+  return res;
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// blocks that share an XCD (b % 8 equal) get a contiguous range of logical ids, so the
+// chunks of consecutive rows -- which re-read each other as the row above -- share an L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
+  if (nb < 16) return b;
+  const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// GolombCoder.cpp:33 for n >= 1 samples with accumulated error A (A < 2^31):
+// the smallest k >= 0 with (n << k) >= A, found from the two leading-one positions.
+__device__ __forceinline__ uint32_t golomb_k(uint32_t n, uint32_t A) {
+  if (A <= n) return 0;
+  uint32_t k = (uint32_t)(__clz((int)n) - __clz((int)A));
+  return k + ((n << k) < A ? 1u : 0u);
+}
+__device__ __forceinline__ uint32_t golomb_k_state(uint32_t n, uint32_t A) {
+  return n == 0 ? 1u : golomb_k(n, A);  // Golomb.h:18 -- a fresh coder starts at k = 1
+}
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// ------------------------------------------------------------------------------------
+// residual word of a chunk step (med in word form), shared by every chunk kernel
+// ------------------------------------------------------------------------------------
+struct RowCtx {
+  const uint64_t* cur;  // row i
+  const uint64_t* up;   // row i-1 (nullptr for i = 0)
+  uint64_t pcarry, ucarry;  // left neighbours of lane 0 for the next step
+};
+
+__device__ __forceinline__ RowCtx row_ctx(const uint64_t* planes, const Geom& g, uint32_t plane,
+                                          uint32_t row, uint32_t c0) {
+  RowCtx rc;
+  rc.cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
+  rc.up = row ? rc.cur - g.wpr : nullptr;
+  rc.pcarry = c0 ? rc.cur[c0 - 1] : 0;
+  rc.ucarry = (c0 && rc.up) ? rc.up[c0 - 1] : 0;
+  return rc;
+}
+
+template <bool PREDICT>
+__device__ __forceinline__ uint64_t resid_word(RowCtx& rc, const Geom& g, uint32_t row, uint32_t w) {
+  const bool valid = w < g.used;
+  const uint64_t p = valid ? rc.cur[w] : 0;
+  uint64_t r;
+  if constexpr (PREDICT) {
+    const uint64_t u = (valid && rc.up) ? rc.up[w] : 0;
+    uint64_t pl = shfl_up_u64(p, 1), ul = shfl_up_u64(u, 1);
+    if (lane_id() == 0) { pl = rc.pcarry; ul = rc.ucarry; }
+    rc.pcarry = shfl_u64(p, 63);
+    rc.ucarry = shfl_u64(u, 63);
+    r = p ^ u ^ ((p >> 1) | (pl << 63)) ^ ((u >> 1) | (ul << 63));
+    if (row == 0 && w == 0) r &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+  } else {
+    r = p;
+  }
+  if (w == g.used - 1) r &= g.trail;
+  return valid ? r : 0;
+}
+
+struct ChunkId {
+  uint32_t plane, row, c;
+  uint64_t id;
+  bool ok;
+};
+__device__ __forceinline__ ChunkId chunk_id(const Geom& g) {
+  ChunkId ci;
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  ci.id = (uint64_t)b * kWaves + (threadIdx.x >> 6);
+  ci.ok = ci.id < g.nchunks;
+  const uint64_t id = ci.ok ? ci.id : 0;
+  ci.plane = (uint32_t)(id / g.chunks_per_plane);
+  const uint64_t r = id % g.chunks_per_plane;
+  ci.row = (uint32_t)(r / g.cpr);
+  ci.c = (uint32_t)(r % g.cpr);
+  return ci;
+}
+
+// ------------------------------------------------------------------------------------
+// K1: bitplanes (bitplane_tool.cpp:24-30). 4 lanes build one 64-pixel word: each lane
+// loads 16 pixels (one 16-byte load), an 8x8 bit transpose turns 8 pixels into one byte
+// per plane (MSB = leftmost pixel), and the 4 x 16-bit pieces meet in LDS.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t transpose8x8(uint64_t x) {
+  uint64_t t;
+  t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+  x = x ^ t ^ (t << 7);
+  t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+  x = x ^ t ^ (t << 14);
+  t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+  x = x ^ t ^ (t << 28);
+  return x;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void k_bitplanes_u8(const uint8_t* __restrict__ gray, size_t pitch,
+                                                         uint32_t rows, uint32_t cols, uint32_t used,
+                                                         int nplanes, uint64_t* __restrict__ planes,
+                                                         uint32_t wpr) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][8][16][4];
+  const uint64_t total = (uint64_t)rows * used * 4;
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, grp = lane >> 2, sub = lane & 3;
+  uint64_t tl = 0, th = 0;
+  if (tid < total) {
+    const uint64_t widx = tid >> 2;
+    const uint32_t row = (uint32_t)(widx / used), w = (uint32_t)(widx % used);
+    const uint32_t j0 = w * 64 + sub * 16;
+    const uint8_t* src = gray + (uint64_t)row * pitch + j0;
+    uint64_t lo = 0, hi = 0;
+    if (VEC && j0 + 16 <= cols) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src);
+      lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    } else {
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const uint64_t px = (j0 + x < cols) ? (uint64_t)src[x] : 0;
+        if (x < 8) lo |= px << (8 * x);
+        else hi |= px << (8 * (x - 8));
+      }
+    }
+    tl = transpose8x8(bswap64(lo));
+    th = transpose8x8(bswap64(hi));
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    lds[wave][b][grp][3 - sub] = (uint16_t)((((tl >> (8 * b)) & 0xff) << 8) | ((th >> (8 * b)) & 0xff));
+  __syncthreads();
+  const int b = lane >> 3;
+  const uint64_t plane_words = (uint64_t)rows * wpr;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int g2 = (lane & 7) * 2 + h;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBlock + wave * 64 + g2 * 4;
+    if (b < nplanes && t0 < total) {
+      const uint64_t wi = t0 >> 2;
+      const uint32_t row = (uint32_t)(wi / used), w = (uint32_t)(wi % used);
+      planes[b * plane_words + (uint64_t)row * wpr + w] =
+          *reinterpret_cast<const uint64_t*>(&lds[wave][b][g2][0]);
+    }
+  }
+}
+
+void launch_bitplanes_u8(hipStream_t s, const uint8_t* gray, size_t pitch, uint32_t rows,
+                         uint32_t cols, int nplanes, uint64_t* planes, uint32_t wpr) {
+  const uint32_t used = (cols + 63) / 64;
+  const uint64_t total = (uint64_t)rows * used * 4;
+  const uint32_t grid = (uint32_t)((total + kBlock - 1) / kBlock);
+  const bool vec = (pitch % 16 == 0) && (((uintptr_t)gray) % 16 == 0);
+  if (vec)
+    k_bitplanes_u8<true><<<grid, kBlock, 0, s>>>(gray, pitch, rows, cols, used, nplanes, planes, wpr);
+  else
+    k_bitplanes_u8<false><<<grid, kBlock, 0, s>>>(gray, pitch, rows, cols, used, nplanes, planes, wpr);
+}
+
+// ------------------------------------------------------------------------------------
+// K2: count pass -- med residual per chunk: popcount, first/last 1-column, optional
+// residual store and per-plane weight (binmat.cpp:57-67).
+// ------------------------------------------------------------------------------------
+template <int WPL, bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_count(Geom g, const uint64_t* __restrict__ planes,
+                                                  ChunkScratch cs, uint64_t* __restrict__ resid,
+                                                  unsigned long long* __restrict__ weight_out) {
+  const ChunkId ci = chunk_id(g);
+  if (!ci.ok) return;  // whole wave uniform
+  const uint32_t c0 = ci.c * g.wpc;
+  RowCtx rc = row_ctx(planes, g, ci.plane, ci.row, c0);
+  const int lane = lane_id();
+  uint32_t ones = 0;
+  int last = -1, first = INT_MAX;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = c0 + t * 64 + lane;
+    const uint64_t r = resid_word<PREDICT>(rc, g, ci.row, w);
+    if (resid && w < g.wpr)
+      resid[(uint64_t)ci.plane * g.plane_words + (uint64_t)ci.row * g.wpr + w] = r;
+    ones += (uint32_t)__popcll(r);
+    if (r) {
+      last = (int)(w * 64 + 63 - __builtin_ctzll(r));
+      if (first == INT_MAX) first = (int)(w * 64 + __builtin_clzll(r));
+    }
+  }
+  ones = wave_sum_u32(ones);
+  last = wave_max(last);
+  first = wave_min(first);
+  if (lane == 0) {
+    cs.ones[ci.id] = ones;
+    cs.last[ci.id] = last;
+    cs.first[ci.id] = first;
+    if (weight_out && ones) atomicAdd(&weight_out[ci.plane], (unsigned long long)ones);
+  }
+}
+
+template <int WPL>
+static void launch_count_t(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                           const ChunkScratch& cs, uint64_t* resid, uint64_t* weight_out) {
+  const uint32_t grid = (uint32_t)((g.nchunks + kWaves - 1) / kWaves);
+  auto* wo = reinterpret_cast<unsigned long long*>(weight_out);
+  if (predict) k_count<WPL, true><<<grid, kBlock, 0, s>>>(g, planes, cs, resid, wo);
+  else k_count<WPL, false><<<grid, kBlock, 0, s>>>(g, planes, cs, resid, wo);
+}
+
+void launch_count(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                  const ChunkScratch& cs, uint64_t* resid, uint64_t* weight_out) {
+  if (g.wpl == 1) launch_count_t<1>(s, g, planes, predict, cs, resid, weight_out);
+  else if (g.wpl == 2) launch_count_t<2>(s, g, planes, predict, cs, resid, weight_out);
+  else launch_count_t<4>(s, g, planes, predict, cs, resid, weight_out);
+}
+
+// ------------------------------------------------------------------------------------
+// K3: per-plane row scan -- sample index of each chunk's first 1 (ones before it + one
+// EOL sample per earlier row), the last 1 before each chunk in its row, the plane's
+// first residual 1 (for EG) and its ones total. One 1024-thread workgroup per plane,
+// one thread per row.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_scan_rows(Geom g, ChunkScratch cs) {
+  __shared__ uint32_t tmp[17];
+  __shared__ unsigned long long fmin;
+  const uint32_t plane = blockIdx.x;
+  const uint64_t cbase = (uint64_t)plane * g.chunks_per_plane;
+  if (threadIdx.x == 0) fmin = ~0ull;
+  uint32_t carry = 0;
+  for (uint32_t r0 = 0; r0 < g.rows; r0 += blockDim.x) {
+    const uint32_t row = r0 + threadIdx.x;
+    uint32_t row_ones = 0;
+    if (row < g.rows)
+      for (uint32_t c = 0; c < g.cpr; ++c) row_ones += cs.ones[cbase + (uint64_t)row * g.cpr + c];
+    uint32_t tot;
+    const uint32_t before = block_excl_scan<uint32_t>(row_ones, tmp, tot) + carry;
+    if (row < g.rows) {
+      uint32_t n = before + row;  // ones before the row + one EOL sample per earlier row
+      int jp = -1;
+      bool seen = false;
+      for (uint32_t c = 0; c < g.cpr; ++c) {
+        const uint64_t id = cbase + (uint64_t)row * g.cpr + c;
+        cs.nbase[id] = n;
+        cs.jprev[id] = jp;
+        const uint32_t o = cs.ones[id];
+        n += o;
+        if (o) {
+          if (!seen) {
+            atomicMin(&fmin, (unsigned long long)row * g.cols + (uint64_t)cs.first[id]);
+            seen = true;
+          }
+          jp = cs.last[id];
+        }
+      }
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cs.plane_F[plane] = fmin;
+    cs.plane_ones[plane] = carry;
+  }
+}
+
+void launch_scan_rows(hipStream_t s, const Geom& g, const ChunkScratch& cs) {
+  k_scan_rows<<<g.nplanes, 1024, 0, s>>>(g, cs);
+}
+
+// ------------------------------------------------------------------------------------
+// Shared per-step bookkeeping of the Golomb kernels: for the lane's word, the sample
+// index of its first 1 and the column of the last 1 before it in the row.
+// ------------------------------------------------------------------------------------
+struct StepState {
+  uint32_t n_carry;
+  int jp_carry;
+};
+
+__device__ __forceinline__ void step_prefix(uint64_t r, uint32_t w, StepState& st, uint32_t& n_w,
+                                            int& jp_w) {
+  const uint32_t pc = (uint32_t)__popcll(r);
+  const uint32_t inc = wave_incl_sum_u32(pc);
+  n_w = st.n_carry + inc - pc;
+  st.n_carry += __shfl(inc, 63);
+  const int lastc = r ? (int)(w * 64 + 63 - __builtin_ctzll(r)) : -1;
+  const int mx = wave_incl_max(lastc);
+  int ex = __shfl_up(mx, 1);
+  if (lane_id() == 0) ex = -1;
+  jp_w = max(st.jp_carry, ex);
+  st.jp_carry = max(st.jp_carry, __shfl(mx, 63));
+}
+
+// ------------------------------------------------------------------------------------
+// K4: Golomb bit lengths per word (and per chunk).
+// ------------------------------------------------------------------------------------
+template <int WPL, bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_golomb_bits(Geom g, const uint64_t* __restrict__ planes,
+                                                        ChunkScratch cs) {
+  const ChunkId ci = chunk_id(g);
+  if (!ci.ok) return;
+  const uint32_t c0 = ci.c * g.wpc;
+  RowCtx rc = row_ctx(planes, g, ci.plane, ci.row, c0);
+  const int lane = lane_id();
+  StepState st{cs.nbase[ci.id], cs.jprev[ci.id]};
+  const uint32_t arow = ci.row * (g.cols + 1);  // A = row*(C+1) + jp + 1 - n
+  uint64_t total = 0;
+  uint32_t* wb = cs.word_bits + (uint64_t)ci.plane * g.words_used + (uint64_t)ci.row * g.used;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = c0 + t * 64 + lane;
+    uint64_t x = resid_word<PREDICT>(rc, g, ci.row, w);
+    uint32_t n;
+    int jp;
+    step_prefix(x, w, st, n, jp);
+    uint32_t bits = 0;
+    while (x) {
+      const int cz = __builtin_clzll(x);
+      x ^= BIC_MSB >> cz;
+      const int j = (int)(w * 64) + cz;
+      const uint32_t s = (uint32_t)(j - jp - 1);
+      const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
+      bits += k + (s >> k) + 1;
+      ++n;
+      jp = j;
+    }
+    if (w == g.used - 1) {  // EOL sample: the row's trailing zeros
+      const uint32_t s = (uint32_t)((int)g.cols - 1 - jp);
+      const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
+      bits += k + (s >> k) + 1;
+    }
+    if (w < g.used) wb[w] = bits;
+    total += bits;
+  }
+  total = wave_sum_u64(total);
+  if (lane == 0) cs.bits[ci.id] = total;
+}
+
+void launch_golomb_bits(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                        const ChunkScratch& cs) {
+  const uint32_t grid = (uint32_t)((g.nchunks + kWaves - 1) / kWaves);
+#define BIC_GB(W)                                                                     \
+  if (predict) k_golomb_bits<W, true><<<grid, kBlock, 0, s>>>(g, planes, cs);         \
+  else k_golomb_bits<W, false><<<grid, kBlock, 0, s>>>(g, planes, cs);
+  if (g.wpl == 1) { BIC_GB(1) }
+  else if (g.wpl == 2) { BIC_GB(2) }
+  else { BIC_GB(4) }
+#undef BIC_GB
+}
+
+// ------------------------------------------------------------------------------------
+// K5: chunk bit offsets per plane (exclusive scan), plane totals, overflow check, and
+// zeroing of every chunk's first/last output word (the only words two chunks share;
+// the emitter ORs into them and plain-stores everything in between).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_golomb_offsets(Geom g, ChunkScratch cs, uint64_t* out,
+                                                         uint64_t slot_words, uint64_t* plane_bits,
+                                                         uint32_t* flags) {
+  __shared__ uint64_t tmp[17];
+  const uint32_t plane = blockIdx.x;
+  const uint64_t cbase = (uint64_t)plane * g.chunks_per_plane;
+  const uint64_t slot0 = (uint64_t)plane * slot_words * 64;
+  const uint64_t cap = slot_words * 64;
+  uint64_t carry = 0;
+  for (uint64_t i0 = 0; i0 < g.chunks_per_plane; i0 += blockDim.x) {
+    const uint64_t i = i0 + threadIdx.x;
+    const uint64_t b = i < g.chunks_per_plane ? cs.bits[cbase + i] : 0;
+    uint64_t tot;
+    const uint64_t rel = block_excl_scan<uint64_t>(b, tmp, tot) + carry;
+    if (i < g.chunks_per_plane) {
+      cs.boff[cbase + i] = slot0 + rel;
+      if (b && rel + b <= cap) {
+        out[(slot0 + rel) / 64] = 0;
+        out[(slot0 + rel + b - 1) / 64] = 0;
+      }
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    plane_bits[plane] = carry;
+    if (carry > cap) atomicOr(&flags[0], 1u);
+  }
+}
+
+void launch_golomb_offsets(hipStream_t s, const Geom& g, const ChunkScratch& cs, uint64_t* out,
+                           uint64_t slot_words, uint64_t* plane_bits, uint32_t* flags) {
+  k_golomb_offsets<<<g.nplanes, 1024, 0, s>>>(g, cs, out, slot_words, plane_bits, flags);
+}
+
+// ------------------------------------------------------------------------------------
+// K6: Golomb emitter. Codeword = k-bit binary part (s mod 2^k, MSB-first), (s>>k) zeros,
+// '1' (GolombCoder.cpp:22-25). The output is zero except for the binary parts and the
+// terminators, so each lane ORs only those bits. A chunk whose output span fits the wave's
+// 4 KB LDS window assembles it there (u32 LDS ORs, one per touched word per lane) and
+// writes it out with coalesced stores; longer spans (very long zero runs) OR straight
+// into global memory.
+// ------------------------------------------------------------------------------------
+struct LdsSink {
+  uint32_t* buf;
+  uint32_t idx, cur;
+  __device__ __forceinline__ void flush() {
+    if (cur) atomicOr(&buf[idx], cur);
+    cur = 0;
+  }
+  __device__ __forceinline__ void orw(uint32_t i, uint32_t v) {
+    if (i != idx) { flush(); idx = i; }
+    cur |= v;
+  }
+  // nb <= 32 bits of v at local bit offset off (MSB-first)
+  __device__ __forceinline__ void put(uint32_t off, uint32_t v, uint32_t nb) {
+    const uint32_t i = off >> 5, sh = off & 31;
+    if (sh + nb <= 32) {
+      orw(i, v << (32 - sh - nb));
+    } else {
+      orw(i, v >> (sh + nb - 32));
+      orw(i + 1, v << (64 - sh - nb));
+    }
+  }
+  __device__ __forceinline__ void bit(uint32_t off) { orw(off >> 5, 0x80000000u >> (off & 31)); }
+};
+
+struct GlobalSink {
+  unsigned long long* buf;  // big-endian 64-bit words
+  uint64_t idx, cur;
+  __device__ __forceinline__ void flush() {
+    if (cur) atomicOr(&buf[idx], (unsigned long long)bswap64(cur));
+    cur = 0;
+  }
+  __device__ __forceinline__ void orw(uint64_t i, uint64_t v) {
+    if (i != idx) { flush(); idx = i; }
+    cur |= v;
+  }
+  __device__ __forceinline__ void put(uint64_t off, uint32_t v, uint32_t nb) {
+    const uint64_t i = off >> 6;
+    const uint32_t sh = (uint32_t)(off & 63);
+    if (sh + nb <= 64) {
+      orw(i, (uint64_t)v << (64 - sh - nb));
+    } else {
+      orw(i, (uint64_t)v >> (sh + nb - 64));
+      orw(i + 1, (uint64_t)v << (128 - sh - nb));
+    }
+  }
+  __device__ __forceinline__ void bit(uint64_t off) { orw(off >> 6, BIC_MSB >> (off & 63)); }
+};
+
+template <typename Sink, typename Off>
+__device__ __forceinline__ void emit_codeword(Sink& sk, Off off, uint32_t s, uint32_t k) {
+  if (k) {
+    const uint32_t bin = s & ((1u << k) - 1u);
+    if (bin) sk.put(off, bin, k);
+  }
+  sk.bit(off + k + (s >> k));
+}
+
+template <int WPL, bool PREDICT, bool STAGED>
+__device__ __forceinline__ void emit_chunk(const Geom& g, const uint64_t* planes, const ChunkScratch& cs,
+                                           const ChunkId& ci, uint64_t cb, uint32_t* lds,
+                                           unsigned long long* gout) {
+  const uint32_t c0 = ci.c * g.wpc;
+  RowCtx rc = row_ctx(planes, g, ci.plane, ci.row, c0);
+  const int lane = lane_id();
+  StepState st{cs.nbase[ci.id], cs.jprev[ci.id]};
+  const uint32_t arow = ci.row * (g.cols + 1);
+  const uint32_t* wb = cs.word_bits + (uint64_t)ci.plane * g.words_used + (uint64_t)ci.row * g.used;
+  const uint64_t gbase = (cb >> 6) << 6;  // bit index of LDS word 0
+  uint64_t off_carry = cb;
+  LdsSink ls{lds, 0, 0};
+  GlobalSink gs{gout, 0, 0};
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = c0 + t * 64 + lane;
+    uint64_t x = resid_word<PREDICT>(rc, g, ci.row, w);
+    uint32_t n;
+    int jp;
+    step_prefix(x, w, st, n, jp);
+    const uint32_t bits = w < g.used ? wb[w] : 0;
+    const uint32_t binc = wave_incl_sum_u32(bits);
+    uint64_t off = off_carry + binc - bits;
+    off_carry += __shfl(binc, 63);
+    const bool eol = (w == g.used - 1);
+    while (x || eol) {
+      int j;
+      uint32_t s;
+      if (x) {
+        const int cz = __builtin_clzll(x);
+        x ^= BIC_MSB >> cz;
+        j = (int)(w * 64) + cz;
+        s = (uint32_t)(j - jp - 1);
+      } else {
+        j = (int)g.cols;  // EOL: the row's trailing zeros
+        s = (uint32_t)((int)g.cols - 1 - jp);
+      }
+      const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
+      if constexpr (STAGED) emit_codeword(ls, (uint32_t)(off - gbase), s, k);
+      else emit_codeword(gs, off, s, k);
+      off += k + (s >> k) + 1;
+      ++n;
+      jp = j;
+      if (j == (int)g.cols) break;
+    }
+  }
+  if constexpr (STAGED) ls.flush();
+  else gs.flush();
+}
+
+template <int WPL, bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_golomb_emit(Geom g, const uint64_t* __restrict__ planes,
+                                                        ChunkScratch cs, uint64_t* __restrict__ out,
+                                                        uint64_t slot_words) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[kWaves * kLdsWords];
+  const ChunkId ci = chunk_id(g);
+  if (!ci.ok) return;
+  const int lane = lane_id();
+  uint32_t* lds = lds_all + (threadIdx.x >> 6) * kLdsWords;
+  const uint64_t L = cs.bits[ci.id];
+  const uint64_t cb = cs.boff[ci.id];
+  const uint64_t slot_end = ((uint64_t)ci.plane + 1) * slot_words * 64;
+  if (L == 0 || cb + L > slot_end) return;  // empty chunk, or the plane overflowed its slot
+  const uint64_t w_first = cb >> 6, w_last = (cb + L - 1) >> 6;
+  const uint64_t span_words = w_last - w_first + 1;  // 64-bit words
+  auto* gout = reinterpret_cast<unsigned long long*>(out);
+  if (span_words * 2 <= (uint64_t)kLdsWords) {
+    for (uint32_t i = lane; i < span_words * 2; i += 64) lds[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    emit_chunk<WPL, PREDICT, true>(g, planes, cs, ci, cb, lds, gout);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < span_words; i += 64) {
+      const uint64_t v = ((uint64_t)lds[2 * i] << 32) | lds[2 * i + 1];
+      const uint64_t be = bswap64(v);
+      if (i == 0 || i == span_words - 1) {
+        if (v) atomicOr(&gout[w_first + i], (unsigned long long)be);
+      } else {
+        out[w_first + i] = be;
+      }
+    }
+  } else {
+    for (uint64_t i = w_first + 1 + lane; i < w_last; i += 64) out[i] = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    emit_chunk<WPL, PREDICT, false>(g, planes, cs, ci, cb, lds, gout);
+  }
+}
+
+void launch_golomb_emit(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                        const ChunkScratch& cs, uint64_t* out, uint64_t slot_words) {
+  const uint32_t grid = (uint32_t)((g.nchunks + kWaves - 1) / kWaves);
+#define BIC_GE(W)                                                                               \
+  if (predict) k_golomb_emit<W, true><<<grid, kBlock, 0, s>>>(g, planes, cs, out, slot_words); \
+  else k_golomb_emit<W, false><<<grid, kBlock, 0, s>>>(g, planes, cs, out, slot_words);
+  if (g.wpl == 1) { BIC_GE(1) }
+  else if (g.wpl == 2) { BIC_GE(2) }
+  else { BIC_GE(4) }
+#undef BIC_GE
+}
+
+// ------------------------------------------------------------------------------------
+// K7: EG as written (eg.cpp:20-37 with incBlockSize disabled): blockSize stays 1, so a run
+// of len zeros costs len '1' bits, then '1' at EOL or '0' (+ one g=1 bit '0' on the plane's
+// first non-EOL run, after which g = 0). The stream is therefore, per row, the complement of
+// the residual row followed by '1', with a single '0' inserted after the plane's first
+// residual 1. One thread per output word; no atomics, no pre-zeroing.
+// ------------------------------------------------------------------------------------
+template <bool PREDICT>
+__device__ __forceinline__ uint64_t resid_word_at(const uint64_t* plane, const Geom& g, uint32_t i,
+                                                  uint32_t w) {
+  if (w >= g.used) return 0;
+  const uint64_t* cur = plane + (uint64_t)i * g.wpr;
+  uint64_t r = cur[w];
+  if constexpr (PREDICT) {
+    const uint64_t pl = w ? cur[w - 1] : 0;
+    uint64_t u = 0, ul = 0;
+    if (i) {
+      u = (cur - g.wpr)[w];
+      ul = w ? (cur - g.wpr)[w - 1] : 0;
+    }
+    r = r ^ u ^ ((r >> 1) | (pl << 63)) ^ ((u >> 1) | (ul << 63));
+    if (i == 0 && w == 0) r &= ~BIC_MSB;
+  }
+  if (w == g.used - 1) r &= g.trail;
+  return r;
+}
+
+// 64 bits of the complemented residual row i starting at column j (left-aligned).
+template <bool PREDICT>
+__device__ __forceinline__ uint64_t notresid_bits(const uint64_t* plane, const Geom& g, uint32_t i,
+                                                  uint32_t j) {
+  const uint32_t w = j >> 6, sh = j & 63;
+  uint64_t v = resid_word_at<PREDICT>(plane, g, i, w) << sh;
+  if (sh) v |= resid_word_at<PREDICT>(plane, g, i, w + 1) >> (64 - sh);
+  return ~v;
+}
+
+// 64 bits of the base stream S0 (rows of cols+1 bits: ~R row then '1') from bit a.
+template <bool PREDICT>
+__device__ __forceinline__ uint64_t eg_window(const uint64_t* plane, const Geom& g, uint64_t a) {
+  const uint64_t rowlen = (uint64_t)g.cols + 1;
+  uint64_t i = a / rowlen;
+  uint32_t j = (uint32_t)(a % rowlen);
+  uint64_t out = 0;
+  uint32_t filled = 0;
+  while (filled < 64 && i < g.rows) {
+    if (j < g.cols) {
+      const uint32_t take = min(64u - filled, g.cols - j);
+      uint64_t v = notresid_bits<PREDICT>(plane, g, (uint32_t)i, j);
+      if (take < 64) v &= ~(~0ull >> take);
+      out |= v >> filled;
+      filled += take;
+      j += take;
+    }
+    if (filled < 64 && j == g.cols) {
+      out |= BIC_MSB >> filled;
+      ++filled;
+      ++i;
+      j = 0;
+    }
+  }
+  return out;
+}
+
+template <bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_eg_emit(Geom g, const uint64_t* __restrict__ planes,
+                                                    ChunkScratch cs, uint64_t* __restrict__ out,
+                                                    uint64_t slot_words, uint64_t words_per_plane,
+                                                    uint64_t* plane_bits, uint32_t* flags) {
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t plane = (uint32_t)(tid / words_per_plane);
+  if (plane >= g.nplanes) return;
+  const uint64_t o = tid % words_per_plane;
+  const uint64_t F = cs.plane_F[plane];
+  const bool hasF = F != ~0ull;
+  const uint64_t bits = (uint64_t)g.rows * (g.cols + 1) + (hasF ? 1 : 0);
+  const uint64_t nw = (bits + 63) / 64;
+  if (o == 0) {
+    plane_bits[plane] = bits;
+    if (nw > slot_words) atomicOr(&flags[0], 1u);
+  }
+  if (nw > slot_words || o >= nw) return;
+  const uint64_t* P = planes + (uint64_t)plane * g.plane_words;
+  const uint64_t b0 = o * 64;
+  uint64_t v;
+  if (!hasF) {
+    v = eg_window<PREDICT>(P, g, b0);
+  } else {
+    const uint64_t f0 = (F / g.cols) * ((uint64_t)g.cols + 1) + F % g.cols;  // S0 index of F
+    if (b0 + 63 <= f0) {
+      v = eg_window<PREDICT>(P, g, b0);
+    } else if (b0 >= f0 + 1) {
+      v = eg_window<PREDICT>(P, g, b0 - 1);
+      if (b0 == f0 + 1) v &= ~BIC_MSB;  // the inserted '0'
+    } else {
+      const uint32_t q = (uint32_t)(f0 + 1 - b0);  // 1..63: position of the inserted '0'
+      const uint64_t X = eg_window<PREDICT>(P, g, b0);
+      const uint64_t Y = eg_window<PREDICT>(P, g, b0 - 1);
+      const uint64_t hi = ~(~0ull >> q);
+      const uint64_t lo = (q == 63) ? 0ull : (~0ull >> (q + 1));
+      v = (X & hi) | (Y & lo);
+    }
+  }
+  // pad bits after the stream end are zero
+  if (o == nw - 1 && (bits & 63)) v &= ~(~0ull >> (bits & 63));
+  out[(uint64_t)plane * slot_words + o] = bswap64(v);
+}
+
+void launch_eg_emit(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
+                    const ChunkScratch& cs, uint64_t* out, uint64_t slot_words,
+                    uint64_t* plane_bits, uint32_t* flags) {
+  const uint64_t wpp = ((uint64_t)g.rows * (g.cols + 1) + 1 + 63) / 64;
+  const uint64_t total = wpp * g.nplanes;
+  const uint32_t grid = (uint32_t)((total + kBlock - 1) / kBlock);
+  if (predict)
+    k_eg_emit<true><<<grid, kBlock, 0, s>>>(g, planes, cs, out, slot_words, wpp, plane_bits, flags);
+  else
+    k_eg_emit<false><<<grid, kBlock, 0, s>>>(g, planes, cs, out, slot_words, wpp, plane_bits, flags);
+}
+
+// ------------------------------------------------------------------------------------
+// Sample coder: GolombCoder::codeSample over an array (reduce -> scan -> lengths ->
+// scan -> emit). ITEMS consecutive samples per thread.
+// ------------------------------------------------------------------------------------
+constexpr int kItems = 8;
+constexpr uint32_t kSampPerBlk = kBlock * kItems;
+
+__global__ __launch_bounds__(kBlock) void k_samp_sum(const uint32_t* __restrict__ s, size_t n,
+                                                     uint64_t* blk_sum) {
+  __shared__ uint64_t tmp[17];
+  const uint64_t base = (uint64_t)blockIdx.x * kSampPerBlk + (uint64_t)threadIdx.x * kItems;
+  uint64_t a = 0;
+#pragma unroll
+  for (int i = 0; i < kItems; ++i)
+    if (base + i < n) a += s[base + i];
+  uint64_t tot;
+  block_excl_scan<uint64_t>(a, tmp, tot);
+  if (threadIdx.x == 0) blk_sum[blockIdx.x] = tot;
+}
+
+// single workgroup: exclusive scan of per-block values (+ init) -> dst, total -> *total_out
+__global__ __launch_bounds__(1024) void k_scan_blocks(const uint64_t* src, uint64_t* dst, uint32_t nblk,
+                                                      uint64_t init, uint64_t* total_out) {
+  __shared__ uint64_t tmp[17];
+  uint64_t carry = init;
+  for (uint32_t i0 = 0; i0 < nblk; i0 += blockDim.x) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint64_t v = i < nblk ? src[i] : 0;
+    uint64_t tot;
+    const uint64_t e = block_excl_scan<uint64_t>(v, tmp, tot);
+    if (i < nblk) dst[i] = carry + e;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && total_out) *total_out = carry - init;
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(kBlock) void k_samp_code(const uint32_t* __restrict__ s, size_t n, uint64_t n0,
+                                                      const uint64_t* blk_A, uint64_t* blk_bits,
+                                                      const uint64_t* blk_off, uint64_t* out,
+                                                      uint32_t* flags, const uint64_t* total_bits,
+                                                      unsigned bit0, size_t cap_words) {
+  __shared__ uint64_t tmp[17];
+  if constexpr (EMIT) {
+    if ((bit0 + *total_bits + 63) / 64 > cap_words) return;  // block-uniform
+  }
+  const uint64_t base = (uint64_t)blockIdx.x * kSampPerBlk + (uint64_t)threadIdx.x * kItems;
+  uint32_t v[kItems];
+  uint64_t a = 0;
+#pragma unroll
+  for (int i = 0; i < kItems; ++i) {
+    v[i] = base + i < n ? s[base + i] : 0;
+    a += v[i];
+  }
+  uint64_t tot;
+  uint64_t A = blk_A[blockIdx.x] + block_excl_scan<uint64_t>(a, tmp, tot);
+  // lengths
+  uint64_t bits = 0;
+  {
+    uint64_t AA = A;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      if (base + i < n) {
+        const uint64_t nn = n0 + base + i;
+        if (nn >= 0x80000000ull || AA >= 0x80000000ull) atomicOr(&flags[1], 1u);
+        const uint32_t k = golomb_k_state((uint32_t)nn, (uint32_t)AA);
+        bits += k + (v[i] >> k) + 1;
+        AA += v[i];
+      }
+    }
+  }
+  if constexpr (!EMIT) {
+    uint64_t bt;
+    block_excl_scan<uint64_t>(bits, tmp, bt);
+    if (threadIdx.x == 0) blk_bits[blockIdx.x] = bt;
+  } else {
+    uint64_t bt;
+    uint64_t off = blk_off[blockIdx.x] + block_excl_scan<uint64_t>(bits, tmp, bt);
+    GlobalSink gs{reinterpret_cast<unsigned long long*>(out), 0, 0};
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      if (base + i < n) {
+        const uint32_t k = golomb_k_state((uint32_t)(n0 + base + i), (uint32_t)A);
+        emit_codeword(gs, off, v[i], k);
+        off += k + (v[i] >> k) + 1;
+        A += v[i];
+      }
+    }
+    gs.flush();
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_samp_zero(uint64_t* out, const uint64_t* total_bits,
+                                                    unsigned bit0, size_t cap_words, uint32_t* flags) {
+  const uint64_t words = (bit0 + *total_bits + 63) / 64;
+  if (words > cap_words) {
+    if (threadIdx.x == 0) atomicOr(&flags[0], 1u);
+    return;
+  }
+  for (uint64_t i = threadIdx.x; i < words; i += blockDim.x) out[i] = 0;
+}
+
+size_t sample_scratch_bytes(size_t n) {
+  const size_t nblk = (n + kSampPerBlk - 1) / kSampPerBlk + 1;
+  return 4 * nblk * sizeof(uint64_t) + 256;
+}
+SampleScratch carve_sample_scratch(void* base, size_t n) {
+  const size_t nblk = (n + kSampPerBlk - 1) / kSampPerBlk + 1;
+  uint64_t* p = reinterpret_cast<uint64_t*>(base);
+  return SampleScratch{p, p + nblk, p + 2 * nblk, p + 3 * nblk};
+}
+
+void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uint64_t n0,
+                           uint64_t a0, unsigned bit0, uint64_t* out, size_t cap_words,
+                           uint64_t* bits_out, const SampleScratch& ss, uint32_t* flags) {
+  const uint32_t nblk = (uint32_t)((n + kSampPerBlk - 1) / kSampPerBlk);
+  if (nblk == 0) {
+    (void)hipMemsetAsync(bits_out, 0, 2 * sizeof(uint64_t), s);
+    return;
+  }
+  k_samp_sum<<<nblk, kBlock, 0, s>>>(samples, n, ss.blk_sum);
+  k_scan_blocks<<<1, 1024, 0, s>>>(ss.blk_sum, ss.blk_A, nblk, a0, bits_out + 1);
+  k_samp_code<false><<<nblk, kBlock, 0, s>>>(samples, n, n0, ss.blk_A, ss.blk_bits, nullptr, nullptr, flags,
+                                              nullptr, 0, 0);
+  k_scan_blocks<<<1, 1024, 0, s>>>(ss.blk_bits, ss.blk_off, nblk, bit0, bits_out);
+  k_samp_zero<<<1, 1024, 0, s>>>(out, bits_out, bit0, cap_words, flags);
+  k_samp_code<true><<<nblk, kBlock, 0, s>>>(samples, n, n0, ss.blk_A, nullptr, ss.blk_off, out, flags,
+                                             bits_out, bit0, cap_words);
+}
+
+// ------------------------------------------------------------------------------------
+// K8: W x W tiles (compress7_test.cpp:184-275, R = 0). One lane per tile row, floor(64/W)
+// tiles per wave; med inside the tile (out-of-tile neighbours 0, R(0,0) = 0).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_tiles(const uint64_t* __restrict__ plane, uint32_t rows,
+                                                  uint32_t cols, uint32_t wpr, uint32_t W, uint32_t nx,
+                                                  uint32_t ntiles, const uint64_t* __restrict__ lentab,
+                                                  uint32_t* weights, uint32_t* w_nonpred, uint32_t* w_pred,
+                                                  uint8_t* modes, unsigned long long* resid,
+                                                  unsigned long long* stats) {
+  __shared__ uint32_t pc_o[kBlock], pc_O[kBlock];
+  __shared__ uint8_t sel[kBlock];
+  __shared__ uint64_t red[2][kWaves];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t tpw = 64 / W;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave;
+  const uint32_t tloc = lane / W, r = lane % W;
+  const uint64_t tile = gw * tpw + tloc;
+  const bool active = tloc < tpw && tile < ntiles;
+  const uint64_t topW = W == 64 ? ~0ull : ~(~0ull >> W);
+  uint64_t x = 0;
+  uint32_t i = 0, j0 = 0;
+  if (active) {
+    const uint32_t ti = (uint32_t)(tile / nx), tj = (uint32_t)(tile % nx);
+    i = ti * W + r;
+    j0 = tj * W;
+    const uint64_t* row = plane + (uint64_t)i * wpr;
+    const uint32_t w = j0 >> 6, sh = j0 & 63;
+    x = row[w] << sh;
+    if (sh && sh + W > 64) x |= row[w + 1] >> (64 - sh);
+    x &= topW;
+  }
+  uint64_t up = shfl_up_u64(x, 1);
+  if (r == 0) up = 0;
+  uint64_t R = (x ^ (x >> 1) ^ up ^ (up >> 1)) & topW;
+  if (r == 0) R &= ~BIC_MSB;
+  pc_o[threadIdx.x] = (uint32_t)__popcll(x);
+  pc_O[threadIdx.x] = (uint32_t)__popcll(R);
+  __syncthreads();
+  uint64_t myL = 0, myW = 0;
+  if (active && r == 0) {
+    uint32_t wo = 0, wO = 0;
+    for (uint32_t q = 0; q < W; ++q) {
+      wo += pc_o[threadIdx.x + q];
+      wO += pc_O[threadIdx.x + q];
+    }
+    const bool pred = lentab[wo] > lentab[wO];  // compress7_test.cpp:248
+    const uint32_t wc = pred ? wO : wo;
+    if (weights) weights[tile] = wc;
+    if (w_nonpred) w_nonpred[tile] = wo;
+    if (w_pred) w_pred[tile] = wO;
+    if (modes) modes[tile] = pred ? 'O' : 'o';
+    sel[threadIdx.x] = pred;
+    myL = lentab[wc];
+    myW = wc;
+  }
+  __syncthreads();
+  if (resid && active) {
+    const uint64_t v = sel[threadIdx.x - r] ? R : x;
+    if (v) {
+      const uint32_t w = j0 >> 6, sh = j0 & 63;
+      unsigned long long* row = resid + (uint64_t)i * wpr;
+      atomicOr(&row[w], (unsigned long long)(v >> sh));
+      if (sh && sh + W > 64) atomicOr(&row[w + 1], (unsigned long long)(v << (64 - sh)));
+    }
+  }
+  myL = wave_sum_u64(myL);
+  myW = wave_sum_u64(myW);
+  if (lane == 0) { red[0][wave] = myL; red[1][wave] = myW; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t a = 0, b = 0;
+    for (int q = 0; q < kWaves; ++q) { a += red[0][q]; b += red[1][q]; }
+    if (a) atomicAdd(&stats[2], (unsigned long long)a);
+    (void)b;
+  }
+}
+
+void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
+                  uint32_t W, const uint64_t* lentab_dev, uint32_t* weights, uint32_t* w_nonpred,
+                  uint32_t* w_pred, uint8_t* modes, uint64_t* resid, uint64_t* stats) {
+  const uint32_t nx = cols / W, ny = rows / W;
+  const uint32_t ntiles = nx * ny;
+  const uint32_t tpw = 64 / W;
+  const uint64_t waves = (ntiles + tpw - 1) / tpw;
+  const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
+  k_tiles<<<grid, kBlock, 0, s>>>(plane, rows, cols, wpr, W, nx, ntiles, lentab_dev, weights, w_nonpred,
+                                  w_pred, modes, reinterpret_cast<unsigned long long*>(resid),
+                                  reinterpret_cast<unsigned long long*>(stats));
+}
+
+// ------------------------------------------------------------------------------------
+// stream packing: plane p's words go to dst + sum_{q<p} ceil(bits_q/64)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ slots, int nplanes,
+                                                 uint64_t slot_words, const uint64_t* __restrict__ plane_bits,
+                                                 uint64_t* __restrict__ dst, uint64_t* word_off) {
+  const int p = blockIdx.y;
+  uint64_t off = 0;
+  for (int q = 0; q < p; ++q) off += (plane_bits[q] + 63) / 64;
+  const uint64_t nw = (plane_bits[p] + 63) / 64;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    word_off[p] = off;
+    if (p == nplanes - 1) word_off[nplanes] = off + nw;
+  }
+  if (nw > slot_words) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * kBlock)
+    dst[off + i] = slots[(uint64_t)p * slot_words + i];
+}
+
+void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
+                 const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off) {
+  uint32_t gx = (uint32_t)((slot_words + kBlock - 1) / kBlock);
+  if (gx > 1024) gx = 1024;
+  if (gx == 0) gx = 1;
+  k_pack<<<dim3(gx, nplanes), kBlock, 0, s>>>(slots, nplanes, slot_words, plane_bits, dst, word_off);
+}
+
+// ------------------------------------------------------------------------------------
+Geom make_geom(size_t rows, size_t cols, size_t wpr, int nplanes) {
+  Geom g{};
+  g.rows = (uint32_t)rows;
+  g.cols = (uint32_t)cols;
+  g.wpr = (uint32_t)wpr;
+  g.used = (uint32_t)((cols + 63) / 64);
+  g.wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
+  g.wpc = 64 * g.wpl;
+  g.cpr = (g.used + g.wpc - 1) / g.wpc;
+  g.nplanes = (uint32_t)nplanes;
+  g.trail = ~0ull << (63 - (cols - 1) % 64);
+  g.plane_words = (uint64_t)rows * wpr;
+  g.chunks_per_plane = (uint64_t)rows * g.cpr;
+  g.nchunks = g.chunks_per_plane * (uint64_t)nplanes;
+  g.words_used = (uint64_t)rows * g.used;
+  return g;
+}
+
+static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t chunk_scratch_bytes(const Geom& g) {
+  const size_t n = g.nchunks;
+  return al(n * 4) * 5 + al(n * 8) * 2 + al(g.words_used * g.nplanes * 4) + al(g.nplanes * 8) * 2 + 256;
+}
+
+ChunkScratch carve_chunk_scratch(void* base, const Geom& g) {
+  char* p = reinterpret_cast<char*>(base);
+  const size_t n = g.nchunks;
+  ChunkScratch cs;
+  cs.ones = reinterpret_cast<uint32_t*>(p); p += al(n * 4);
+  cs.last = reinterpret_cast<int32_t*>(p); p += al(n * 4);
+  cs.first = reinterpret_cast<int32_t*>(p); p += al(n * 4);
+  cs.nbase = reinterpret_cast<uint32_t*>(p); p += al(n * 4);
+  cs.jprev = reinterpret_cast<int32_t*>(p); p += al(n * 4);
+  cs.bits = reinterpret_cast<uint64_t*>(p); p += al(n * 8);
+  cs.boff = reinterpret_cast<uint64_t*>(p); p += al(n * 8);
+  cs.word_bits = reinterpret_cast<uint32_t*>(p); p += al(g.words_used * g.nplanes * 4);
+  cs.plane_F = reinterpret_cast<uint64_t*>(p); p += al(g.nplanes * 8);
+  cs.plane_ones = reinterpret_cast<uint64_t*>(p);
+  return cs;
+}
+
+}  // namespace bic

@@ -1,0 +1,268 @@
+"""pybic -- thin ctypes binding of lib/libbic.so (include/bic.h) for tests, bench and tools.
+
+torch supplies device memory and the stream (plumbing only); every computation runs in the
+HIP kernels behind the C ABI. There is no fallback: if libbic.so or a gfx950 device is
+missing, construction of `Context` raises.
+
+uint64 planes/streams are carried in torch.int64 tensors (same bits); use `as_u64()` to view
+them as numpy uint64 on the host.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "lib", "libbic.so")
+
+BIC_OK, BIC_EINVAL, BIC_ENOMEM, BIC_EDEVICE, BIC_ENOSPC, BIC_ENODEV = range(6)
+CODER_GOLOMB, CODER_EG = 0, 1
+
+# every symbol include/bic.h declares (tests check the library exports all of them)
+EXPORTS = [
+    "bic_ctx_create", "bic_ctx_destroy", "bic_ctx_set_stream", "bic_ctx_get_stream", "bic_sync",
+    "bic_strerror", "bic_device_count", "bic_reserve", "bic_bitplanes_u8", "bic_med_residual",
+    "bic_encode_planes", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
+    "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
+]
+
+
+class BicError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        super().__init__(f"{what}: bic error {code} ({_strerror(code)})")
+
+
+_lib = None
+
+
+def _strerror(code):
+    try:
+        return load().bic_strerror(code).decode()
+    except Exception:  # pragma: no cover
+        return "?"
+
+
+def load(path=LIB_PATH):
+    """Load libbic.so (raises OSError if it is missing: build it with `make` in the package)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} not built; run make -C binary-image-compression_amd")
+    L = C.CDLL(path)
+    vp, sz, u64, i32, u32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_int, C.c_uint
+
+    def sig(name, res, args):
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+
+    sig("bic_ctx_create", i32, [i32, C.POINTER(vp)])
+    sig("bic_ctx_destroy", i32, [vp])
+    sig("bic_ctx_set_stream", i32, [vp, vp])
+    sig("bic_ctx_get_stream", vp, [vp])
+    sig("bic_sync", i32, [vp])
+    sig("bic_strerror", C.c_char_p, [i32])
+    sig("bic_device_count", i32, [C.POINTER(i32)])
+    sig("bic_reserve", i32, [vp, i32, sz, sz])
+    sig("bic_bitplanes_u8", i32, [vp, vp, sz, sz, sz, i32, vp, sz])
+    sig("bic_med_residual", i32, [vp, vp, i32, sz, sz, sz, i32, vp, vp])
+    sig("bic_encode_planes", i32, [vp, vp, i32, sz, sz, sz, i32, i32, vp, sz, vp])
+    sig("bic_encode_slot_words", sz, [sz, sz, i32])
+    sig("bic_golomb_encode_samples", i32, [vp, vp, sz, u64, u64, u32, vp, sz, vp])
+    sig("bic_patch_encode", i32, [vp, vp, sz, sz, sz, u32, vp, vp, vp, vp, vp, vp, vp, sz, vp])
+    sig("bic_pack_streams", i32, [vp, vp, i32, sz, vp, vp, vp])
+    sig("bic_prof_enable", i32, [vp, i32])
+    sig("bic_prof_collect", i32, [vp, C.c_char_p, sz])
+    sig("bic_enum_codelength", C.c_double, [u32, u32])
+    sig("bic_tile_lentab", i32, [u32, vp])
+    _lib = L
+    return L
+
+
+def as_u64(t):
+    """torch int64 tensor (any device) -> numpy uint64 copy."""
+    return t.detach().cpu().numpy().view(np.uint64)
+
+
+def stream_bytes(words_i64, nbits):
+    """First ceil(nbits/64) big-endian words of a stream slot as the MSB-first byte string."""
+    nw = (int(nbits) + 63) // 64
+    return as_u64(words_i64[:nw]).tobytes()
+
+
+def _p(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class Context:
+    """One device context (include/bic.h bic_ctx). Calls are enqueued on torch's current
+    stream of the device, so they order with torch allocations and copies."""
+
+    def __init__(self, device=0):
+        import torch
+
+        self.torch = torch
+        self.lib = load()
+        self.device = device
+        h = C.c_void_p()
+        rc = self.lib.bic_ctx_create(device, C.byref(h))
+        if rc != BIC_OK:
+            raise BicError(rc, f"bic_ctx_create({device})")
+        self.h = h
+        self.dev = torch.device("cuda", device)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.bic_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- plumbing ---------------------------------------------------------------------
+    def _bind_stream(self):
+        s = self.torch.cuda.current_stream(self.dev).cuda_stream
+        self.lib.bic_ctx_set_stream(self.h, C.c_void_p(s))
+
+    def _chk(self, rc, what):
+        if rc != BIC_OK:
+            raise BicError(rc, what)
+
+    def sync(self):
+        rc = self.lib.bic_sync(self.h)
+        self._chk(rc, "bic_sync")
+
+    def empty_i64(self, *shape):
+        return self.torch.empty(*shape, dtype=self.torch.int64, device=self.dev)
+
+    def to_dev(self, a):
+        """numpy array -> device tensor (uint64 carried as int64, uint32 as int32)."""
+        a = np.ascontiguousarray(a)
+        if a.dtype == np.uint64:
+            a = a.view(np.int64)
+        elif a.dtype == np.uint32:
+            a = a.view(np.int32)
+        return self.torch.from_numpy(a).to(self.dev)
+
+    def reserve(self, nplanes, rows, cols):
+        self._chk(self.lib.bic_reserve(self.h, nplanes, rows, cols), "bic_reserve")
+
+    def prof_enable(self, on=True):
+        self._chk(self.lib.bic_prof_enable(self.h, int(on)), "bic_prof_enable")
+
+    def prof_collect(self):
+        """-> {kernel name: (launches, total_ms)} since the last collect (syncs)."""
+        buf = C.create_string_buffer(1 << 16)
+        self._chk(self.lib.bic_prof_collect(self.h, buf, len(buf)), "bic_prof_collect")
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, n, ms = line.split()
+            out[name] = (int(n), float(ms))
+        return out
+
+    # -- ops --------------------------------------------------------------------------
+    def bitplanes_u8(self, gray, cols=None, nplanes=8, wpr=None, out=None):
+        """gray: uint8 device tensor [rows, pitch] -> int64 tensor [nplanes, rows, wpr]."""
+        rows, pitch = gray.shape
+        cols = pitch if cols is None else cols
+        wpr = wpr or (cols + 63) // 64
+        if out is None:
+            out = self.empty_i64(nplanes, rows, wpr)
+        self._bind_stream()
+        self._chk(self.lib.bic_bitplanes_u8(self.h, _p(gray), pitch, rows, cols, nplanes, _p(out), wpr),
+                  "bic_bitplanes_u8")
+        return out
+
+    def med_residual(self, planes, cols, predict=True, want_resid=True, want_weight=True):
+        planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
+        n, rows, wpr = planes.shape
+        resid = self.empty_i64(n, rows, wpr) if want_resid else None
+        w = self.torch.zeros(n, dtype=self.torch.int64, device=self.dev) if want_weight else None
+        self._bind_stream()
+        self._chk(self.lib.bic_med_residual(self.h, _p(planes), n, rows, cols, wpr, int(predict),
+                                            _p(resid), _p(w)), "bic_med_residual")
+        return resid, w
+
+    def slot_words(self, rows, cols, coder):
+        return int(self.lib.bic_encode_slot_words(rows, cols, coder))
+
+    def encode_planes(self, planes, cols, predict=True, coder=CODER_GOLOMB, slot_words=None,
+                      out=None, plane_bits=None):
+        """-> (out int64 [nplanes, slot_words], plane_bits int64 [nplanes]) (async)."""
+        planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
+        n, rows, wpr = planes.shape
+        slot_words = slot_words or self.slot_words(rows, cols, coder)
+        if out is None:
+            out = self.empty_i64(n, slot_words)
+        if plane_bits is None:
+            plane_bits = self.empty_i64(n)
+        self._bind_stream()
+        self._chk(self.lib.bic_encode_planes(self.h, _p(planes), n, rows, cols, wpr, int(predict), coder,
+                                             _p(out), slot_words, _p(plane_bits)), "bic_encode_planes")
+        return out, plane_bits
+
+    def golomb_encode_samples(self, samples, n0=0, a0=0, bit0=0, cap_words=None, out=None):
+        """samples: int32 device tensor (uint32 values) -> (stream int64 [cap], bits int64[2])."""
+        n = samples.numel()
+        cap_words = cap_words or max(1, (n * 40 + bit0 + 63) // 64 + 2)
+        if out is None:
+            out = self.empty_i64(cap_words)
+        bits = self.empty_i64(2)
+        self._bind_stream()
+        self._chk(self.lib.bic_golomb_encode_samples(self.h, _p(samples), n, n0, a0, bit0, _p(out),
+                                                     cap_words, _p(bits)), "bic_golomb_encode_samples")
+        return out, bits
+
+    def patch_encode(self, plane, cols, W, lentab, cap_words=None, want_resid=True):
+        """plane: int64 [rows, wpr]; lentab: numpy uint64 [W*W+1] (host)."""
+        rows, wpr = plane.shape
+        nt = (rows // W) * (cols // W)
+        t = self.torch
+        weights = t.empty(nt, dtype=t.int32, device=self.dev)
+        wo = t.empty(nt, dtype=t.int32, device=self.dev)
+        wO = t.empty(nt, dtype=t.int32, device=self.dev)
+        modes = t.empty(nt, dtype=t.uint8, device=self.dev)
+        resid = self.empty_i64(rows, wpr) if want_resid else None
+        cap_words = cap_words or max(1, (nt * 48 + 63) // 64 + 2)
+        stream = self.empty_i64(cap_words)
+        stats = self.empty_i64(3)
+        lt = np.ascontiguousarray(lentab, np.uint64)
+        self._bind_stream()
+        self._chk(self.lib.bic_patch_encode(self.h, _p(plane), rows, cols, wpr, W, lt.ctypes.data_as(C.c_void_p),
+                                            _p(weights), _p(wo), _p(wO), _p(modes), _p(resid), _p(stream),
+                                            cap_words, _p(stats)), "bic_patch_encode")
+        return dict(weights=weights, w_nonpred=wo, w_pred=wO, modes=modes, resid=resid, stream=stream,
+                    stats=stats)
+
+    def pack_streams(self, slots, plane_bits, dst_words=None):
+        n, slot_words = slots.shape
+        dst = self.empty_i64(dst_words or n * slot_words)
+        off = self.empty_i64(n + 1)
+        self._bind_stream()
+        self._chk(self.lib.bic_pack_streams(self.h, _p(slots), n, slot_words, _p(plane_bits), _p(dst), _p(off)),
+                  "bic_pack_streams")
+        return dst, off
+
+
+def enum_codelength(n, r):
+    """log2 C(n, r) (coding.h enumerative_codelength), host-side, from libbic.so."""
+    return float(load().bic_enum_codelength(n, r))
+
+
+def lentab(W):
+    """tile length table for bic_patch_encode: (uint64)(2 + log2 C(W*W, w)), w = 0..W*W."""
+    out = np.zeros(W * W + 1, np.uint64)
+    rc = load().bic_tile_lentab(W, out.ctypes.data_as(C.c_void_p))
+    if rc != BIC_OK:
+        raise BicError(rc, "bic_tile_lentab")
+    return out
+
+
+def device_count():
+    n = C.c_int(0)
+    load().bic_device_count(C.byref(n))
+    return n.value

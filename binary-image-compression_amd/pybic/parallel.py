@@ -1,0 +1,60 @@
+"""Multi-GPU plumbing over torch.distributed (backend "nccl" = RCCL over xGMI on ROCm; "gloo"
+for CPU tests). The encode itself never exchanges data: planes/frames are independent units
+(SURVEY.md §8 e). Two real exchange steps exist:
+
+* gather_streams: the final stream concatenation -- every rank's packed stream goes to rank 0
+  by direct point-to-point transfers (xGMI is point-to-point; a ring would be per-link bound).
+* shard_state / shard_offsets: one adaptive Golomb coder split across ranks (the C5 tile
+  sequence): each rank needs the coder state (samples, accumulated error) and the bit offset of
+  everything before it -- an all-gather of two u64 per rank each.
+"""
+import torch
+import torch.distributed as dist
+
+
+def _allgather_i64(vals, device):
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, t)
+    return [o.tolist() for o in outs]
+
+
+def gather_streams(packed, nwords, world=None, rank=None, dst=0):
+    """packed: int64 tensor whose first nwords entries are this rank's stream words; nwords:
+    int (or 1-element tensor). Returns (words, offsets) on `dst` -- all ranks' words back to
+    back in rank order and each rank's start -- and (None, None) elsewhere."""
+    world = world or dist.get_world_size()
+    rank = dist.get_rank() if rank is None else rank
+    n = int(nwords.reshape(-1)[0].item()) if torch.is_tensor(nwords) else int(nwords)
+    sizes = [s[0] for s in _allgather_i64([n], packed.device)]
+    if rank == dst:
+        offs = [0]
+        for s in sizes:
+            offs.append(offs[-1] + s)
+        out = torch.empty(offs[-1], dtype=packed.dtype, device=packed.device)
+        out[offs[rank]:offs[rank] + n].copy_(packed[:n])
+        ops = [dist.P2POp(dist.irecv, out[offs[r]:offs[r + 1]], r) for r in range(world) if r != dst and sizes[r]]
+        for req in (dist.batch_isend_irecv(ops) if ops else []):
+            req.wait()
+        return out, offs
+    if n:
+        for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed[:n].contiguous(), dst)]):
+            req.wait()
+    return None, None
+
+
+def shard_state(count, total, device):
+    """Exclusive prefix over ranks of (samples, accumulated error): the GolombCoder state a
+    rank's first sample sees (Golomb.h:21-24) when the sequence is split in rank order."""
+    rows = _allgather_i64([int(count), int(total)], device)
+    r = dist.get_rank()
+    n0 = sum(x[0] for x in rows[:r])
+    a0 = sum(x[1] for x in rows[:r])
+    return n0, a0
+
+
+def shard_offsets(bits, device):
+    """Exclusive prefix over ranks of stream bit lengths, and the total."""
+    rows = _allgather_i64([int(bits)], device)
+    r = dist.get_rank()
+    return sum(x[0] for x in rows[:r]), sum(x[0] for x in rows)

@@ -1,0 +1,132 @@
+/*
+ * bic.h -- C ABI of the MI355X (gfx950) hot path of nacho-pancho/binary-image-compression:
+ *          bitplane extraction -> med (3-neighbour XOR) prediction -> per-row zero runs
+ *          -> adaptive Golomb (GolombCoder) / "EG" run-length (EGCoder) coding.
+ *
+ * Plain pointers and sizes only; no C++ or torch types. Every bulk pointer is a DEVICE
+ * pointer (hipMalloc'd or any device allocation of the caller); the caller allocates every
+ * output (the reference's convention "C is assumed to have been allocated",
+ * binmat.cpp:462). Calls enqueue on the context's stream and return immediately;
+ * bic_sync() waits and reports deferred errors (e.g. an output slot that was too small).
+ *
+ * Plane layout = the reference's binary_matrix storage (binmat.h:8-19, 114-141): rows x wpr
+ * uint64 words, row-major, column j in word j/64 at bit 63 - j%64 (MSB = leftmost pixel),
+ * wpr >= ceil(cols/64). Bits past `cols` are ignored on input and written 0 on output.
+ * Several planes are stored back to back (plane p at planes + p*rows*wpr).
+ *
+ * Encoded streams (build-defined container): one stream per plane, MSB-first
+ * bit order, stored as big-endian 64-bit words (so the bytes in memory ARE the bit stream),
+ * zero-padded to a 64-bit boundary. Plane p's stream starts at out + p*slot_words.
+ *
+ * Reference interface each entry replaces is cited per function (file:line under /root/reference/src).
+ * Error codes: 0 = OK; never exceptions (style of pbm.h:8-16 ErrorCode).
+ */
+#ifndef BIC_H
+#define BIC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BIC_OK 0
+#define BIC_EINVAL 1   /* bad argument (the reference asserts, e.g. binmat.cpp:465-469, GolombCoder.cpp:14) */
+#define BIC_ENOMEM 2   /* device allocation failed */
+#define BIC_EDEVICE 3  /* HIP runtime error */
+#define BIC_ENOSPC 4   /* an output slot was too small (reported by bic_sync) */
+#define BIC_ENODEV 5   /* no usable gfx950 device */
+
+#define BIC_CODER_GOLOMB 0 /* GolombCoder::codeSample over the run samples (GolombCoder.cpp:29-34) */
+#define BIC_CODER_EG 1     /* EGCoder::codeRun as written: incBlockSize disabled (eg.cpp:20-37) */
+
+typedef struct bic_ctx bic_ctx;
+
+/* ---- context ----------------------------------------------------------------------------- */
+int bic_ctx_create(int device, bic_ctx** out);
+int bic_ctx_destroy(bic_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the ctx's own. */
+int bic_ctx_set_stream(bic_ctx* ctx, void* hip_stream);
+void* bic_ctx_get_stream(bic_ctx* ctx);
+/* Wait for all work enqueued by this ctx; returns BIC_ENOSPC if an encode since the last
+ * sync overflowed its slot (that plane's stream is then incomplete), else BIC_OK/BIC_EDEVICE. */
+int bic_sync(bic_ctx* ctx);
+const char* bic_strerror(int code);
+int bic_device_count(int* n);
+/* Pre-grow the ctx scratch so later calls do not allocate (needed before stream capture). */
+int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
+
+/* ---- a2: bitplane extraction (bitplane_tool.cpp:24-30) -----------------------------------
+ * gray: rows x cols bytes with row pitch `pitch` (>= cols). Plane bi receives bit bi of every
+ * pixel, LSB plane first; nplanes in 1..8 (bitplane_tool extracts #{bi : 2^bi < maxval}). */
+int bic_bitplanes_u8(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols,
+                     int nplanes, uint64_t* planes, size_t wpr);
+
+/* ---- a5/a6: med residual + weight (pred.cpp:3-15, binmat.cpp:57-67) -----------------------
+ * resid (nullable): the med residual of each plane (R(0,0) = 0 and pad bits 0, which is what
+ * the reference leaves/observes). weight_out (nullable, device, nplanes entries): popcount of the
+ * residual (predict = 1) or of the plane itself (predict = 0). */
+int bic_med_residual(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                     size_t wpr, int predict, uint64_t* resid, uint64_t* weight_out);
+
+/* ---- a7-a10: plane encoder ------------------------------------------------------------------
+ * Runs per row in raster order: one sample per 1-pixel (zeros since the previous 1 or the row
+ * start) and one EOL sample per row (the trailing zeros, also when 0); one coder per plane,
+ * fresh state (Golomb.h:14-19 / eg.h:9). predict = 1 codes the med residual, 0 the plane.
+ * out: nplanes slots of slot_words 64-bit words; plane_bits (device, nplanes): stream length
+ * in bits. Domain: rows*(cols+1) < 2^31 (the reference's 32-bit coder state never wraps). */
+int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                      size_t wpr, int predict, int coder, uint64_t* out, size_t slot_words,
+                      uint64_t* plane_bits);
+/* A slot size (64-bit words) that every plane of this geometry fits for EG (exact) and for
+ * Golomb on any input this build has seen (2*rows*(cols+1) bits + 64 words); a larger input
+ * still reports BIC_ENOSPC rather than writing out of bounds. */
+size_t bic_encode_slot_words(size_t rows, size_t cols, int coder);
+
+/* ---- GolombCoder::codeSample over an arbitrary sample array (GolombCoder.cpp:29-34) --------
+ * Coder state on entry: n0 samples already coded with accumulated error a0 (n0 = a0 = 0 is a
+ * fresh GolombCoder). The stream is written starting at bit `bit0` of out (0 <= bit0 < 64;
+ * lets a shard start at its global bit alignment); out[0 .. cap_words) must be writable.
+ * bits_out (device, 2 x u64): [0] = codeword bits (= GolombCoder::bitcount), [1] = sum of samples. */
+int bic_golomb_encode_samples(bic_ctx* ctx, const uint32_t* samples, size_t n, uint64_t n0,
+                              uint64_t a0, unsigned bit0, uint64_t* out, size_t cap_words,
+                              uint64_t* bits_out);
+
+/* ---- a11-a13: W x W tile path (compress7_test.cpp:118-275 with R = 0) ---------------------
+ * Per tile in raster order: w_nonpred = weight(P), w_pred = weight(med(P)) (med inside the tile,
+ * R(0,0) = 0); mode 'O' iff lentab[w_nonpred] > lentab[w_pred] else 'o'; the chosen weight is
+ * Golomb-coded (golomb_nomatch.codeSample, compress7_test.cpp:270) and lentab[chosen] summed (L).
+ * lentab: HOST array of W*W+1 entries, lentab[w] = (idx_t)(2 + enumL(W*W, w)) (see coding.h).
+ * Requires 1 <= W <= 64, rows % W == 0, cols % W == 0 (no edge wrap).
+ * Outputs (device, each nullable except stream): weights (chosen), w_nonpred, w_pred (u32 per
+ * tile), modes (u8 per tile), resid (the image after the residual write-back of :266/:272),
+ * stream (cap_words words) and stats (device u64[3]: Golomb bits, sum of chosen weights, L). */
+int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
+                     unsigned W, const uint64_t* lentab, uint32_t* weights, uint32_t* w_nonpred,
+                     uint32_t* w_pred, uint8_t* modes, uint64_t* resid, uint64_t* stream,
+                     size_t cap_words, uint64_t* stats);
+
+/* log2 C(n, r) (enumerative_codelength, coding.cpp:19-22) computed without GSL, and the tile
+ * length table lentab[w] = (uint64)(2 + log2 C(W*W, w)) for w = 0..W*W (host memory, W*W+1
+ * entries) that bic_patch_encode takes. Host-side helpers; no device needed. */
+double bic_enum_codelength(unsigned n, unsigned r);
+int bic_tile_lentab(unsigned W, uint64_t* lentab);
+
+/* ---- stream packing ---------------------------------------------------------------------------
+ * Concatenates the nplanes slot streams (plane_bits from bic_encode_planes) word-aligned into
+ * dst; word_off (device, nplanes+1): start word of each plane in dst, word_off[nplanes] = total. */
+int bic_pack_streams(bic_ctx* ctx, const uint64_t* slots, int nplanes, size_t slot_words,
+                     const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
+
+/* ---- kernel timing ------------------------------------------------------------------------
+ * When enabled, every kernel launch of this ctx is bracketed by HIP events on the launch stream.
+ * bic_prof_collect syncs, writes one line per kernel name ("name launches total_ms\n") into buf
+ * and clears the records. */
+int bic_prof_enable(bic_ctx* ctx, int on);
+int bic_prof_collect(bic_ctx* ctx, char* buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,517 @@
+/*
+ * bic_oracle.c -- TEST INFRASTRUCTURE ONLY. See bic_oracle.h for scope and the
+ * reference file:line each function restates. Deliberately bit-serial and
+ * simple: this is the checker the HIP path is compared against, not a fast path.
+ */
+#include "bic_oracle.h"
+
+#include <assert.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define BO_MSB 0x8000000000000000ull
+
+/* ------------------------------------------------------------------------- */
+uint64_t bo_splitmix64(uint64_t* state) {
+    uint64_t z = (*state += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void bo_gen_plane(uint64_t seed, double p, size_t rows, size_t cols, size_t wpr,
+                  uint64_t* plane) {
+    uint64_t st = seed;
+    const uint32_t thr = (uint32_t)llround(p * 65536.0);
+    const size_t used = (cols + 63) / 64;
+    for (size_t i = 0; i < rows; ++i) {
+        for (size_t w = 0; w < wpr; ++w) {
+            uint64_t word = 0;
+            if (w < used) {
+                for (int q = 0; q < 16; ++q) {
+                    const uint64_t x = bo_splitmix64(&st);
+                    for (int d = 0; d < 4; ++d) {
+                        const uint32_t draw = (uint32_t)(x >> (48 - 16 * d)) & 0xFFFFu;
+                        word = (word << 1) | (draw < thr ? 1u : 0u);
+                    }
+                }
+                if (w == used - 1 && (cols & 63)) word &= ~0ull << (64 - (cols & 63));
+            }
+            plane[i * wpr + w] = word;
+        }
+    }
+}
+
+void bo_gen_bytes(uint64_t seed, size_t n, uint8_t* out) {
+    uint64_t st = seed;
+    for (size_t i = 0; i < n; i += 8) {
+        const uint64_t x = bo_splitmix64(&st);
+        for (size_t b = 0; b < 8 && i + b < n; ++b) out[i + b] = (uint8_t)(x >> (8 * b));
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+int bo_get(const uint64_t* P, size_t wpr, size_t i, size_t j) {
+    return (P[i * wpr + j / 64] & (BO_MSB >> (j % 64))) != 0;
+}
+
+void bo_set(uint64_t* P, size_t wpr, size_t i, size_t j, int v) {
+    uint64_t* w = &P[i * wpr + j / 64];
+    const uint64_t m = BO_MSB >> (j % 64);
+    if (v) *w |= m; else *w &= ~m;
+}
+
+int bo_num_planes(int maxval) {
+    int n = 0;
+    for (long b = 1; b < maxval; b <<= 1) ++n; /* bitplane_tool.cpp:24 */
+    return n;
+}
+
+void bo_bitplanes(const void* gray, int bytes_per_px, size_t rows, size_t cols,
+                  int nplanes, uint64_t* planes, size_t wpr) {
+    const uint8_t* g8 = (const uint8_t*)gray;
+    const uint16_t* g16 = (const uint16_t*)gray;
+    memset(planes, 0, sizeof(uint64_t) * (size_t)nplanes * rows * wpr);
+    for (int bi = 0; bi < nplanes; ++bi) {
+        uint64_t* A = planes + (size_t)bi * rows * wpr;
+        for (size_t i = 0, li = 0; i < rows; ++i)
+            for (size_t j = 0; j < cols; ++j, ++li) {
+                const unsigned px = bytes_per_px == 1 ? g8[li] : g16[li];
+                bo_set(A, wpr, i, j, (px >> bi) & 1u);
+            }
+    }
+}
+
+void bo_med(const uint64_t* P, uint64_t* R, size_t rows, size_t cols, size_t wpr) {
+    memset(R, 0, sizeof(uint64_t) * rows * wpr);
+    if (rows == 0 || cols == 0) return;
+    for (size_t j = 1; j < cols; ++j)                 /* pred.cpp:5-7 */
+        bo_set(R, wpr, 0, j, bo_get(P, wpr, 0, j - 1) ^ bo_get(P, wpr, 0, j));
+    for (size_t i = 1; i < rows; ++i) {                /* pred.cpp:8-13 */
+        bo_set(R, wpr, i, 0, bo_get(P, wpr, i - 1, 0) ^ bo_get(P, wpr, i, 0));
+        for (size_t j = 1; j < cols; ++j)
+            bo_set(R, wpr, i, j,
+                   bo_get(P, wpr, i - 1, j - 1) ^ bo_get(P, wpr, i, j - 1) ^
+                   bo_get(P, wpr, i - 1, j) ^ bo_get(P, wpr, i, j));
+    }
+}
+
+static int bo_popcount64(uint64_t x) {
+    int c = 0;
+    while (x) { x &= x - 1; ++c; }
+    return c;
+}
+
+uint64_t bo_weight(const uint64_t* P, size_t rows, size_t cols, size_t wpr) {
+    if (rows * cols == 0) return 0;
+    const size_t bpr = (cols + 63) / 64;
+    const uint64_t trail = ~0ull << (63 - (cols - 1) % 64); /* binmat.cpp:147 */
+    uint64_t w = 0;
+    for (size_t i = 0; i < rows; ++i)
+        for (size_t j = 0; j < bpr; ++j) {
+            uint64_t b = P[i * wpr + j];
+            if (j == bpr - 1) b &= trail;                   /* binmat.h:188-190 */
+            w += (uint64_t)bo_popcount64(b);
+        }
+    return w;
+}
+
+/* ------------------------------------------------------------------------- */
+void bo_bw_init(bo_bw* bw, uint8_t* buf, size_t cap_bytes) {
+    bw->buf = buf;
+    bw->cap_bits = buf ? cap_bytes * 8 : 0;
+    bw->pos = 0;
+    bw->overflow = 0;
+    if (buf) memset(buf, 0, cap_bytes);
+}
+
+static void bo_bw_bit1(bo_bw* bw, uint64_t at) {
+    if (!bw->buf) return;
+    if (at >= bw->cap_bits) { bw->overflow = 1; return; }
+    bw->buf[at >> 3] |= (uint8_t)(0x80u >> (at & 7));
+}
+
+void bo_bw_put(bo_bw* bw, uint32_t value, unsigned nbits) {
+    for (unsigned b = 0; b < nbits; ++b)
+        if ((value >> (nbits - 1 - b)) & 1u) bo_bw_bit1(bw, bw->pos + b);
+    bw->pos += nbits;
+    if (bw->buf && bw->pos > bw->cap_bits) bw->overflow = 1;
+}
+
+void bo_bw_zeros(bo_bw* bw, uint64_t n) {
+    bw->pos += n;
+    if (bw->buf && bw->pos > bw->cap_bits) bw->overflow = 1;
+}
+
+/* ------------------------------------------------------------------------- */
+void bo_golomb_init(bo_golomb* g) {  /* Golomb.h:14-19 */
+    g->accumulatedError = 0;
+    g->samples = 0;
+    g->k = 1;
+    g->bitcount = 0;
+}
+
+uint32_t bo_golomb_code(bo_golomb* g, uint32_t s, bo_bw* bw) {
+    const uint32_t k = g->k;
+    assert(k < 32);                                   /* GolombCoder.cpp:14 */
+    const uint32_t unary = s >> k;                    /* GolombCoder.cpp:19 */
+    if (bw) {
+        bo_bw_put(bw, k ? (s & ((1u << k) - 1u)) : 0u, k); /* binary part */
+        bo_bw_zeros(bw, unary);                            /* unary zeros */
+        bo_bw_put(bw, 1u, 1);                              /* terminator  */
+    }
+    const uint32_t len = k + unary + 1;
+    g->bitcount += len;                               /* GolombCoder.cpp:26 */
+    g->samples++;                                     /* GolombCoder.cpp:31-33 */
+    g->accumulatedError += s;
+    uint32_t nk = 0;
+    /* the domain the reference is defined on: samples << k never wraps before
+     * reaching accumulatedError (guaranteed when accumulatedError < 2^31). */
+    while (nk < 31 && (g->samples << nk) < g->accumulatedError) ++nk;
+    g->k = nk;
+    return len;
+}
+
+/* JPEG-LS run-length order table J[0..31] (ITU-T T.87 A.7.1.2), which the
+ * reference's EGLUT (eg.cpp:2) is. */
+static const unsigned char bo_J[32] = {0, 0, 0, 0, 1, 1, 1,  1,  2,  2,  2,  2,  3,  3,  3,  3,
+                                       4, 4, 5, 5, 6, 6, 7,  7,  8,  9,  10, 11, 12, 13, 14, 15};
+
+void bo_eg_init(bo_eg* e, int adaptive) {  /* eg.h:9 */
+    e->g = 1;
+    e->blockSize = 1;
+    e->lutIndex = 0;
+    e->bitcount = 0;
+    e->adaptive = adaptive;
+}
+
+static void bo_eg_inc(bo_eg* e) {  /* eg.cpp:4-10, index capped at 31 */
+    if (e->lutIndex < 31) e->lutIndex++;
+    e->g = bo_J[e->lutIndex];
+    e->blockSize = 1u << e->g;
+}
+
+static void bo_eg_dec(bo_eg* e) {  /* eg.cpp:12-18 */
+    if (e->lutIndex > 0) e->lutIndex--;
+    e->g = bo_J[e->lutIndex];
+    e->blockSize = 1u << e->g;
+}
+
+uint32_t bo_eg_code(bo_eg* e, int len, int eol, bo_bw* bw) {
+    uint32_t bits = 0;
+    while ((unsigned)len >= e->blockSize) {          /* eg.cpp:22-27 */
+        len -= (int)e->blockSize;
+        if (bw) bo_bw_put(bw, 1u, 1);
+        ++bits;
+        if (e->adaptive) bo_eg_inc(e);
+    }
+    if (eol) {                                        /* eg.cpp:28-30 */
+        if (bw) bo_bw_put(bw, 1u, 1);
+        bits += 1;
+    } else {                                          /* eg.cpp:31-35 */
+        if (bw) { bo_bw_put(bw, 0u, 1); bo_bw_put(bw, (uint32_t)len, e->g); }
+        bits += e->g + 1;
+        bo_eg_dec(e);
+    }
+    e->bitcount += bits;
+    return bits;
+}
+
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    int coder;
+    bo_golomb gol;
+    bo_eg eg;
+    bo_bw* bw;
+    uint64_t nsamples;
+} bo_sink;
+
+static void bo_sink_run(bo_sink* s, uint32_t len, int eol) {
+    if (s->coder == 0) bo_golomb_code(&s->gol, len, s->bw);
+    else bo_eg_code(&s->eg, (int)len, eol, s->bw);
+    s->nsamples++;
+}
+
+/* Run extraction, SURVEY.md §8 a7 (build-defined; shape from eg.h:23). */
+static void bo_scan_runs(const uint64_t* src, size_t rows, size_t cols, size_t wpr, bo_sink* s) {
+    for (size_t i = 0; i < rows; ++i) {
+        long last = -1;
+        for (size_t j = 0; j < cols; ++j) {
+            if (bo_get(src, wpr, i, j)) {
+                bo_sink_run(s, (uint32_t)((long)j - last - 1), 0);
+                last = (long)j;
+            }
+        }
+        bo_sink_run(s, (uint32_t)((long)cols - 1 - last), 1);
+    }
+}
+
+int64_t bo_encode_plane(const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
+                        int predict, int coder, uint8_t* out, size_t cap_bytes,
+                        uint64_t* nsamples) {
+    const uint64_t* src = plane;
+    uint64_t* R = NULL;
+    if (predict) {
+        R = (uint64_t*)malloc(sizeof(uint64_t) * rows * wpr + 8);
+        bo_med(plane, R, rows, cols, wpr);
+        src = R;
+    }
+    bo_bw bw;
+    bo_bw_init(&bw, out, cap_bytes);
+    bo_sink s;
+    s.coder = coder == 0 ? 0 : 1;
+    bo_golomb_init(&s.gol);
+    bo_eg_init(&s.eg, coder == 2);
+    s.bw = &bw;
+    s.nsamples = 0;
+    bo_scan_runs(src, rows, cols, wpr, &s);
+    free(R);
+    if (nsamples) *nsamples = s.nsamples;
+    if (out && (bw.overflow || ((bw.pos + 63) / 64) * 8 > cap_bytes)) return -1;
+    return (int64_t)bw.pos;
+}
+
+size_t bo_plane_runs(const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
+                     uint32_t* runs, uint8_t* eols, size_t cap) {
+    size_t n = 0;
+    for (size_t i = 0; i < rows; ++i) {
+        long last = -1;
+        for (size_t j = 0; j < cols; ++j)
+            if (bo_get(plane, wpr, i, j)) {
+                if (n < cap) { runs[n] = (uint32_t)((long)j - last - 1); eols[n] = 0; }
+                ++n;
+                last = (long)j;
+            }
+        if (n < cap) { runs[n] = (uint32_t)((long)cols - 1 - last); eols[n] = 1; }
+        ++n;
+    }
+    return n;
+}
+
+int64_t bo_golomb_samples(const uint32_t* s, size_t n, uint8_t* out, size_t cap_bytes,
+                          uint32_t* k_out, uint32_t* len_out) {
+    bo_bw bw;
+    bo_bw_init(&bw, out, cap_bytes);
+    bo_golomb g;
+    bo_golomb_init(&g);
+    for (size_t i = 0; i < n; ++i) {
+        if (k_out) k_out[i] = g.k;
+        const uint32_t len = bo_golomb_code(&g, s[i], &bw);
+        if (len_out) len_out[i] = len;
+    }
+    if (out && (bw.overflow || ((bw.pos + 63) / 64) * 8 > cap_bytes)) return -1;
+    return g.bitcount;
+}
+
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t* buf;
+    uint64_t nbits, pos;
+} bo_br;
+
+static int bo_br_bit(bo_br* r) {
+    if (r->pos >= r->nbits) return -1;
+    const int b = (r->buf[r->pos >> 3] >> (7 - (r->pos & 7))) & 1;
+    r->pos++;
+    return b;
+}
+
+void bo_unmed(const uint64_t* R, uint64_t* P, size_t rows, size_t cols, size_t wpr, int corner) {
+    memset(P, 0, sizeof(uint64_t) * rows * wpr);
+    for (size_t i = 0; i < rows; ++i)
+        for (size_t j = 0; j < cols; ++j) {
+            int v;
+            if (i == 0 && j == 0) v = corner & 1;
+            else {
+                v = bo_get(R, wpr, i, j);
+                if (j > 0) v ^= bo_get(P, wpr, i, j - 1);
+                if (i > 0) v ^= bo_get(P, wpr, i - 1, j);
+                if (i > 0 && j > 0) v ^= bo_get(P, wpr, i - 1, j - 1);
+            }
+            bo_set(P, wpr, i, j, v);
+        }
+}
+
+/* Read order of GolombDecoder.cpp:17-21: k-bit binary, count zeros, the '1'. */
+int bo_decode_plane_golomb(const uint8_t* stream, uint64_t nbits, size_t rows, size_t cols,
+                           size_t wpr, int predict, int corner, uint64_t* plane) {
+    uint64_t* dst = plane;
+    uint64_t* R = NULL;
+    if (predict) { R = (uint64_t*)malloc(sizeof(uint64_t) * rows * wpr + 8); dst = R; }
+    memset(dst, 0, sizeof(uint64_t) * rows * wpr);
+    bo_br br = {stream, nbits, 0};
+    bo_golomb g;
+    bo_golomb_init(&g);
+    int rc = 0;
+    for (size_t i = 0; i < rows && !rc; ++i) {
+        size_t j = 0;
+        for (;;) {
+            uint32_t bin = 0;
+            for (uint32_t b = 0; b < g.k; ++b) {
+                const int v = bo_br_bit(&br);
+                if (v < 0) { rc = 1; break; }
+                bin = (bin << 1) | (uint32_t)v;
+            }
+            if (rc) break;
+            uint64_t unary = 0;
+            int v;
+            while ((v = bo_br_bit(&br)) == 0) ++unary;
+            if (v < 0) { rc = 1; break; }
+            const uint64_t s64 = (unary << g.k) | bin;
+            if (j + s64 > cols) { rc = 2; break; }
+            bo_golomb_code(&g, (uint32_t)s64, NULL);
+            const size_t pos = j + (size_t)s64;
+            if (pos == cols) break;  /* EOL sample */
+            bo_set(dst, wpr, i, pos, 1);
+            j = pos + 1;
+        }
+    }
+    if (!rc && predict) bo_unmed(R, plane, rows, cols, wpr, corner);
+    free(R);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* binmat.cpp:267-298: word-level extraction with the reference's compact block
+ * indexing (k over rows*blocks_per_row), so a right-edge tile reads the first
+ * word of the next row and anything past the last block reads 0. */
+static uint64_t bo_block_at(const uint64_t* I, size_t bpr, size_t wpr, size_t data_blocks, size_t k) {
+    if (k >= data_blocks) return 0;
+    return I[(k / bpr) * wpr + k % bpr];
+}
+
+void bo_get_submatrix(const uint64_t* I, size_t rows, size_t cols, size_t wpr,
+                      size_t i0, size_t i1, size_t j0, size_t j1, uint64_t* B, size_t bwpr) {
+    const size_t bpr = (cols + 63) / 64;
+    const size_t data_blocks = rows * bpr;
+    const size_t brows = i1 - i0, bbpr = (j1 - j0 + 63) / 64;
+    const size_t boff = j0 % 64;
+    const size_t doff = j0 / 64 + i0 * bpr;
+    for (size_t di = 0; di < brows; ++di)
+        for (size_t dj = 0; dj < bbpr; ++dj) {
+            const size_t k1 = doff + di * bpr + dj;
+            uint64_t v;
+            if (boff == 0) v = bo_block_at(I, bpr, wpr, data_blocks, k1);
+            else
+                v = (bo_block_at(I, bpr, wpr, data_blocks, k1) << boff) |
+                    (bo_block_at(I, bpr, wpr, data_blocks, k1 + 1) >> (64 - boff));
+            B[di * bwpr + dj] = v;
+        }
+}
+
+/* binmat.cpp:373-414 for a source of at most 64 columns (one block per row),
+ * which is every use on the path. Returns without effect for wider sources. */
+void bo_set_submatrix(uint64_t* I, size_t rows, size_t cols, size_t wpr,
+                      size_t i0, size_t j0, const uint64_t* B, size_t brows, size_t bcols, size_t bwpr) {
+    if (bcols == 0 || bcols > 64) return;
+    const size_t bpr = (cols + 63) / 64, last = bpr - 1;
+    const uint64_t itrail = ~0ull << (63 - (cols - 1) % 64);
+    const uint64_t btrail = ~0ull << (63 - (bcols - 1) % 64);
+    const size_t boff = j0 % 64;
+    const size_t lastoff = (boff + bcols) % 64;
+    const size_t spanned = (63 + boff + bcols) / 64;
+    for (size_t si = 0, di = i0; si < brows && di < rows; ++si, ++di) {
+        const uint64_t sb = B[si * bwpr] & btrail;  /* B.get_block(si,0) */
+        uint64_t* row = I + di * wpr;
+        const size_t dj = j0 / 64;
+        if (boff == 0 || spanned == 1) {
+            const uint64_t mr = boff ? (~0ull >> boff) : ~0ull;
+            const uint64_t ml = lastoff ? (~0ull << (64 - lastoff)) : ~0ull;
+            const uint64_t m = mr & ml;
+            uint64_t cur = row[dj];
+            if (dj == last) cur &= itrail;           /* get_block trail mask */
+            row[dj] = (cur & ~m) | ((sb >> boff) & m);
+        } else {
+            const uint64_t hi = ~0ull << (64 - boff);      /* bits kept in word dj */
+            const uint64_t m3 = ~0ull << (64 - lastoff);   /* bits set in word dj+1 */
+            uint64_t cur = row[dj];
+            if (dj == last) cur &= itrail;
+            row[dj] = (cur & hi) | (sb >> boff);
+            if (dj < last) {
+                uint64_t nxt = row[dj + 1];
+                if (dj + 1 == last) nxt &= itrail;
+                row[dj + 1] = (nxt & ~m3) | ((sb << (64 - boff)) & m3);
+            }
+        }
+    }
+}
+
+double bo_enumL(unsigned n, unsigned r) {
+    if (r == 0 || r >= n) return 0.0;  /* C(n,0) = C(n,n) = 1 */
+    unsigned m = r * 2 > n ? n - r : r;
+    if (m == 1) {
+        /* log2 n; exact for powers of two (GSL's rounding here is what SURVEY
+         * §8 c calls "parity unpinned at w in {1, M-1}") */
+        if ((n & (n - 1)) == 0) {
+            double e = 0;
+            while ((1u << (unsigned)e) < n) e += 1.0;
+            return e;
+        }
+        return (double)(log2l((long double)n));
+    }
+    const long double ln = lgammal((long double)n + 1.0L) - lgammal((long double)m + 1.0L) -
+                           lgammal((long double)(n - m) + 1.0L);
+    return (double)(ln * 1.442695040888963407359924681001892137L);
+}
+
+int64_t bo_patch_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                        const uint64_t* lentab, uint32_t* w_nonpred, uint32_t* w_pred,
+                        char* modes, uint64_t* L_out, uint8_t* stream, size_t cap_bytes) {
+    if (W == 0 || W > 64) return -1;
+    const size_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+    uint64_t P[64], dP[64];
+    bo_bw bw;
+    bo_bw_init(&bw, stream, cap_bytes);
+    bo_golomb g;
+    bo_golomb_init(&g);
+    uint64_t L = 0;
+    size_t t = 0;
+    for (size_t ti = 0; ti < Ny; ++ti)
+        for (size_t tj = 0; tj < Nx; ++tj, ++t) {
+            const size_t i0 = ti * W, j0 = tj * W;
+            bo_get_submatrix(I, rows, cols, wpr, i0, i0 + W, j0, j0 + W, P, 1);
+            const uint64_t wo = bo_weight(P, W, W, 1);
+            bo_med(P, dP, W, W, 1);
+            const uint64_t wO = bo_weight(dP, W, W, 1);
+            const int pred = lentab[wo] > lentab[wO];     /* compress7_test.cpp:248 */
+            const uint64_t w = pred ? wO : wo;
+            L += lentab[w];
+            if (w_nonpred) w_nonpred[t] = (uint32_t)wo;
+            if (w_pred) w_pred[t] = (uint32_t)wO;
+            if (modes) modes[t] = pred ? 'O' : 'o';
+            bo_golomb_code(&g, (uint32_t)w, &bw);          /* compress7_test.cpp:270 */
+            bo_set_submatrix(I, rows, cols, wpr, i0, j0, pred ? dP : P, W, W, 1); /* :272 */
+        }
+    if (L_out) *L_out = L;
+    if (stream && bw.overflow) return -1;
+    return g.bitcount;
+}
+
+/* ------------------------------------------------------------------------- */
+uint64_t bo_baseline_planes(const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                            size_t wpr, int predict, int do_eg, int* threads_used) {
+    uint64_t total = 0;
+    int nt = 1;
+#ifdef _OPENMP
+    nt = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+#endif
+    for (int p = 0; p < nplanes; ++p) {
+        const uint64_t* P = planes + (size_t)p * rows * wpr;
+        const size_t cap = (size_t)(2.5 * (double)rows * (double)(cols + 1) / 8.0) + 64;
+        uint8_t* buf = (uint8_t*)malloc(cap);
+        int64_t b = bo_encode_plane(P, rows, cols, wpr, predict, 0, buf, cap, NULL);
+        if (b > 0) total += (uint64_t)b;
+        if (do_eg) {
+            b = bo_encode_plane(P, rows, cols, wpr, predict, 1, buf, cap, NULL);
+            if (b > 0) total += (uint64_t)b;
+        }
+        free(buf);
+    }
+    if (threads_used) *threads_used = nt;
+    return total;
+}

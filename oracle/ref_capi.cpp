@@ -1,0 +1,249 @@
+// ref_capi.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// A thin extern "C" harness over the REFERENCE's own objects, compiled from the
+// read-only sources under /root/reference/src by oracle/Makefile into
+// oracle/_ref/libref.so (git-ignored; it travels to the GPU box only as the
+// prebuilt CPU baseline). No reference source is copied here: this file only
+// calls the reference's binary_matrix / med / GolombCoder / EGCoder / pbm / pnm.
+//
+// Used (1) by tests/golden/make_golden.py to produce the golden vectors that pin
+// oracle/bic_oracle.c, and (2) by bench.py's cpu_baseline leg (kind "reference").
+#include "binmat.h"
+#include "pbm.h"
+#include "pnm.h"
+#include "GolombCoder.h"
+#include "eg.h"
+
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+#include <omp.h>
+
+void med(const binary_matrix& P, binary_matrix& pP);  // pred.cpp:3
+
+namespace {
+
+// GolombCoder keeps k protected (Golomb.h:20-24); a derived view reads it.
+struct GolombProbe : public GolombCoder {
+  unsigned current_k() const { return k; }
+};
+
+binary_matrix from_words(const uint64_t* P, size_t rows, size_t cols, size_t wpr) {
+  binary_matrix A(rows, cols);
+  A.clear();
+  for (size_t i = 0; i < rows; ++i)
+    for (size_t j = 0; j < cols; ++j)
+      if (P[i * wpr + j / 64] & (0x8000000000000000ull >> (j % 64))) A.set(i, j);
+  return A;
+}
+
+void to_words(const binary_matrix& A, uint64_t* P, size_t wpr) {
+  const size_t rows = A.get_rows(), cols = A.get_cols();
+  for (size_t i = 0; i < rows; ++i) {
+    for (size_t w = 0; w < wpr; ++w) P[i * wpr + w] = 0;
+    for (size_t j = 0; j < cols; ++j)
+      if (A.get(i, j)) P[i * wpr + j / 64] |= 0x8000000000000000ull >> (j % 64);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// med over a whole plane; the output matrix is cleared first so the bits the
+// reference never writes (R(0,0), pad) read 0, as observed.
+int ref_med(const uint64_t* P, uint64_t* R, size_t rows, size_t cols, size_t wpr) {
+  binary_matrix A = from_words(P, rows, cols, wpr);
+  binary_matrix B(rows, cols);
+  B.clear();
+  med(A, B);
+  to_words(B, R, wpr);
+  A.destroy();
+  B.destroy();
+  return 0;
+}
+
+uint64_t ref_weight(const uint64_t* P, size_t rows, size_t cols, size_t wpr) {
+  binary_matrix A = from_words(P, rows, cols, wpr);
+  const uint64_t w = A.weight();
+  A.destroy();
+  return w;
+}
+
+// Feeds samples to one GolombCoder; per sample reports the k used and the
+// bitcount increment (the codeword length).
+int64_t ref_golomb(const uint32_t* s, size_t n, uint32_t* k_out, uint32_t* len_out) {
+  GolombProbe g;
+  for (size_t i = 0; i < n; ++i) {
+    const long before = g.bitcount;
+    if (k_out) k_out[i] = g.current_k();
+    g.codeSample(s[i]);
+    if (len_out) len_out[i] = (uint32_t)(g.bitcount - before);
+  }
+  return g.bitcount;
+}
+
+uint64_t ref_eg(const int32_t* len, const uint8_t* eol, size_t n, uint32_t* bits_out) {
+  EGCoder e;
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned long before = e.bitcount;
+    e.codeRun(len[i], eol[i] != 0);
+    if (bits_out) bits_out[i] = (uint32_t)(e.bitcount - before);
+  }
+  return e.bitcount;
+}
+
+int ref_get_submatrix(const uint64_t* I, size_t rows, size_t cols, size_t wpr, size_t i0,
+                      size_t i1, size_t j0, size_t j1, uint64_t* B, size_t bwpr) {
+  binary_matrix A = from_words(I, rows, cols, wpr);
+  binary_matrix S = A.get_submatrix(i0, i1, j0, j1);
+  to_words(S, B, bwpr);
+  A.destroy();
+  S.destroy();
+  return 0;
+}
+
+int ref_set_submatrix(uint64_t* I, size_t rows, size_t cols, size_t wpr, size_t i0, size_t j0,
+                      const uint64_t* B, size_t brows, size_t bcols, size_t bwpr) {
+  binary_matrix A = from_words(I, rows, cols, wpr);
+  binary_matrix S = from_words(B, brows, bcols, bwpr);
+  A.set_submatrix(i0, j0, S);
+  to_words(A, I, wpr);
+  A.destroy();
+  S.destroy();
+  return 0;
+}
+
+// compress7_test.cpp:118-275 with R = 0 (no tile ever matches):
+// reference get_submatrix / weight / med / GolombCoder / set_submatrix, the
+// mode picked by the caller-supplied length table (lentab[w] = (idx_t)(2+enumL)).
+int64_t ref_tile_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W,
+                      const uint64_t* lentab, uint32_t* w_nonpred, uint32_t* w_pred,
+                      char* modes, uint64_t* L_out) {
+  binary_matrix I = from_words(Iw, rows, cols, wpr);
+  const size_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+  GolombCoder g;
+  uint64_t L = 0;
+  size_t t = 0;
+  for (size_t i = 0; i < Ny; ++i)
+    for (size_t j = 0; j < Nx; ++j, ++t) {
+      const size_t i0 = i * W, j0 = j * W;
+      binary_matrix P = I.get_submatrix(i0, i0 + W, j0, j0 + W);
+      binary_matrix dP(W, W);
+      dP.clear();
+      med(P, dP);
+      const uint64_t wo = P.weight(), wO = dP.weight();
+      const bool pred = lentab[wo] > lentab[wO];
+      const uint64_t w = pred ? wO : wo;
+      L += lentab[w];
+      g.codeSample((unsigned)w);
+      I.set_submatrix(i0, j0, pred ? dP : P);
+      if (w_nonpred) w_nonpred[t] = (uint32_t)wo;
+      if (w_pred) w_pred[t] = (uint32_t)wO;
+      if (modes) modes[t] = pred ? 'O' : 'o';
+      P.destroy();
+      dP.destroy();
+    }
+  to_words(I, Iw, wpr);
+  I.destroy();
+  if (L_out) *L_out = L;
+  return g.bitcount;
+}
+
+// PBM round trip through read_pbm_header/read_pbm_data/write_pbm (pbm.cpp).
+int ref_pbm_roundtrip(const char* in_path, const char* out_path, uint64_t* rows_cols) {
+  FILE* f = fopen(in_path, "r");
+  if (!f) return -1;
+  idx_t rows = 0, cols = 0;
+  const int rc = read_pbm_header(f, rows, cols);
+  if (rc != PBM_OK) { fclose(f); return rc; }
+  binary_matrix A(rows, cols);
+  read_pbm_data(f, A);
+  fclose(f);
+  FILE* o = fopen(out_path, "w");
+  if (!o) { A.destroy(); return -2; }
+  write_pbm(A, o);
+  fclose(o);
+  A.destroy();
+  rows_cols[0] = rows;
+  rows_cols[1] = cols;
+  return 0;
+}
+
+// Reads a PBM with the reference reader and returns its bits as words.
+int ref_read_pbm(const char* path, uint64_t* P, size_t wpr, uint64_t* rows_cols) {
+  FILE* f = fopen(path, "r");
+  if (!f) return -1;
+  idx_t rows = 0, cols = 0;
+  const int rc = read_pbm_header(f, rows, cols);
+  if (rc != PBM_OK) { fclose(f); return rc; }
+  rows_cols[0] = rows;
+  rows_cols[1] = cols;
+  if (P) {
+    binary_matrix A(rows, cols);
+    read_pbm_data(f, A);
+    to_words(A, P, wpr);
+    A.destroy();
+  }
+  fclose(f);
+  return 0;
+}
+
+// Reads a PGM header + data with the reference reader (pnm.cpp:20-89).
+int ref_read_pgm(const char* path, int* hdr /*type,cols,rows,maxval*/, uint32_t* pixels) {
+  FILE* f = fopen(path, "r");
+  if (!f) return -1;
+  int type, cols, rows, maxval;
+  if (read_pnm_header(f, type, cols, rows, maxval) != 0) return -2;  // closes f on failure
+  hdr[0] = type; hdr[1] = cols; hdr[2] = rows; hdr[3] = maxval;
+  int rc = 0;
+  if (pixels) rc = read_pgm_data(f, type, cols, rows, maxval, pixels);
+  fclose(f);
+  return rc;
+}
+
+// CPU baseline (bench.py, kind "reference"): the reference's bit-serial med,
+// GolombCoder::codeSample and EGCoder::codeRun over per-row runs, OpenMP over
+// independent planes (the reference has no OpenMP on this path, SURVEY.md §8 d).
+// Returns elapsed seconds of the timed region; bits[0] = Golomb bits, bits[1] = EG bits.
+double ref_baseline_planes(const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                           size_t wpr, int predict, int do_eg, int threads, uint64_t* bits,
+                           int* threads_used) {
+  std::vector<binary_matrix> in(nplanes);
+  for (int p = 0; p < nplanes; ++p) in[p] = from_words(planes + (size_t)p * rows * wpr, rows, cols, wpr);
+  if (threads > 0) omp_set_num_threads(threads);
+  uint64_t gbits = 0, ebits = 0;
+  int used = 1;
+  const double t0 = omp_get_wtime();
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : gbits, ebits)
+  for (int p = 0; p < nplanes; ++p) {
+    if (omp_get_thread_num() == 0) used = omp_get_num_threads();
+    binary_matrix R(rows, cols);
+    const binary_matrix* src = &in[p];
+    if (predict) { R.clear(); med(in[p], R); src = &R; }
+    GolombCoder g;
+    EGCoder e;
+    for (size_t i = 0; i < rows; ++i) {
+      long last = -1;
+      for (size_t j = 0; j < cols; ++j)
+        if (src->get(i, j)) {
+          g.codeSample((unsigned)((long)j - last - 1));
+          if (do_eg) e.codeRun((int)((long)j - last - 1), false);
+          last = (long)j;
+        }
+      g.codeSample((unsigned)((long)cols - 1 - last));
+      if (do_eg) e.codeRun((int)((long)cols - 1 - last), true);
+    }
+    gbits += (uint64_t)g.bitcount;
+    ebits += (uint64_t)e.bitcount;
+    R.destroy();
+  }
+  const double dt = omp_get_wtime() - t0;
+  for (int p = 0; p < nplanes; ++p) in[p].destroy();
+  bits[0] = gbits;
+  bits[1] = ebits;
+  if (threads_used) *threads_used = used;
+  return dt;
+}
+
+}  // extern "C"

@@ -1,0 +1,39 @@
+"""Oracle vs the reference objects on fresh random inputs (this container only: skipped
+where oracle/_ref was not built, e.g. on the GPU box when the reference is absent)."""
+import numpy as np
+import pytest
+
+from oracle_lib import have_ref
+
+pytestmark = pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (needs /root/reference)")
+
+
+@pytest.fixture(scope="module")
+def ref():
+    from oracle_lib import Ref
+    return Ref()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_planes(oracle, ref, seed):
+    rng = np.random.default_rng(seed)
+    rows, cols = int(rng.integers(1, 90)), int(rng.integers(1, 300))
+    p = float(rng.choice([0.5, 0.2, 0.03, 0.0, 1.0]))
+    P = oracle.gen_plane(1000 + seed, p, rows, cols)
+    assert np.array_equal(oracle.med(P, cols), ref.med(P, cols))
+    for pred in (0, 1):
+        _, gb, eb, _ = ref.baseline(P[None], rows, cols, predict=pred, do_eg=1, threads=1)
+        assert oracle.encode_plane(P, cols, pred, 0, want_stream=False)[0] == gb
+        assert oracle.encode_plane(P, cols, pred, 1, want_stream=False)[0] == eb
+
+
+@pytest.mark.parametrize("W", [3, 5, 8, 16, 32])
+def test_random_tiles(oracle, ref, W):
+    rng = np.random.default_rng(W)
+    rows, cols = int(rng.integers(W, 6 * W)), int(rng.integers(W, 7 * W))
+    I = oracle.gen_plane(2000 + W, 0.2, rows, cols)
+    lt = oracle.lentab(W)
+    a, b = oracle.patch_encode(I, cols, W, lt), ref.tile_loop(I, cols, W, lt)
+    for k in ("bits", "L", "modes"):
+        assert a[k] == b[k]
+    assert np.array_equal(a["w_pred"], b["w_pred"])
