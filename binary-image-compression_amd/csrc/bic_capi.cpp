@@ -161,9 +161,11 @@ int bic_ctx_destroy(bic_ctx* ctx) {
 
 int bic_ctx_set_stream(bic_ctx* ctx, void* hip_stream) {
   if (!ctx) return BIC_EINVAL;
-  ctx->cur = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own;
+  ctx->cur = reinterpret_cast<hipStream_t>(hip_stream);  // NULL = the HIP null stream
   return BIC_OK;
 }
+
+void* bic_ctx_own_stream(bic_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->own) : nullptr; }
 
 void* bic_ctx_get_stream(bic_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->cur) : nullptr; }
 
@@ -192,7 +194,7 @@ int bic_bitplanes_u8(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t row
                      int nplanes, uint64_t* planes, size_t wpr) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if (!gray || !planes || nplanes < 1 || nplanes > 8 || pitch < cols) return BIC_EINVAL;
+  if (nplanes < 1 || nplanes > 8 || pitch < cols || (rows && (!gray || !planes))) return BIC_EINVAL;
   if (!geom_ok(rows, cols, wpr)) return BIC_EINVAL;
   if (rows == 0) return BIC_OK;
   timed(ctx, "bitplanes_u8", [&] {
@@ -207,7 +209,7 @@ int bic_med_residual(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t r
                      size_t wpr, int predict, uint64_t* resid, uint64_t* weight_out) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if (!planes || nplanes < 1 || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (nplanes < 1 || !geom_ok(rows, cols, wpr) || (rows && !planes)) return BIC_EINVAL;
   if (weight_out) BIC_HIP(hipMemsetAsync(weight_out, 0, sizeof(uint64_t) * nplanes, ctx->cur));
   if (rows == 0) return BIC_OK;
   const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
@@ -229,9 +231,10 @@ int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t 
                       uint64_t* plane_bits) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if (!planes || !out || !plane_bits || nplanes < 1 || slot_words == 0) return BIC_EINVAL;
+  if (!plane_bits || nplanes < 1 || slot_words == 0) return BIC_EINVAL;
   if (coder != BIC_CODER_GOLOMB && coder != BIC_CODER_EG) return BIC_EINVAL;
   if (!geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (rows && (!planes || !out)) return BIC_EINVAL;
   if (rows == 0) {
     BIC_HIP(hipMemsetAsync(plane_bits, 0, sizeof(uint64_t) * nplanes, ctx->cur));
     return BIC_OK;

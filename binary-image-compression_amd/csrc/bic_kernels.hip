@@ -250,8 +250,9 @@ __global__ __launch_bounds__(kBlock) void k_bitplanes_u8(const uint8_t* __restri
     if (b < nplanes && t0 < total) {
       const uint64_t wi = t0 >> 2;
       const uint32_t row = (uint32_t)(wi / used), w = (uint32_t)(wi % used);
-      planes[b * plane_words + (uint64_t)row * wpr + w] =
-          *reinterpret_cast<const uint64_t*>(&lds[wave][b][g2][0]);
+      uint64_t v;
+      __builtin_memcpy(&v, &lds[wave][b][g2][0], sizeof(v));  // (no type-punned load)
+      planes[b * plane_words + (uint64_t)row * wpr + w] = v;
     }
   }
 }
@@ -757,7 +758,8 @@ __global__ __launch_bounds__(kBlock) void k_eg_emit(Geom g, const uint64_t* __re
     } else {
       const uint32_t q = (uint32_t)(f0 + 1 - b0);  // 1..63: position of the inserted '0'
       const uint64_t X = eg_window<PREDICT>(P, g, b0);
-      const uint64_t Y = eg_window<PREDICT>(P, g, b0 - 1);
+      // Y bit t = S0[b0 - 1 + t]; only bits t >= q+1 >= 2 are used, so at b0 = 0 X >> 1 serves
+      const uint64_t Y = b0 ? eg_window<PREDICT>(P, g, b0 - 1) : (X >> 1);
       const uint64_t hi = ~(~0ull >> q);
       const uint64_t lo = (q == 63) ? 0ull : (~0ull >> (q + 1));
       v = (X & hi) | (Y & lo);

@@ -20,7 +20,8 @@ CODER_GOLOMB, CODER_EG = 0, 1
 
 # every symbol include/bic.h declares (tests check the library exports all of them)
 EXPORTS = [
-    "bic_ctx_create", "bic_ctx_destroy", "bic_ctx_set_stream", "bic_ctx_get_stream", "bic_sync",
+    "bic_ctx_create", "bic_ctx_destroy", "bic_ctx_set_stream", "bic_ctx_get_stream", "bic_ctx_own_stream",
+    "bic_sync",
     "bic_strerror", "bic_device_count", "bic_reserve", "bic_bitplanes_u8", "bic_med_residual",
     "bic_encode_planes", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
@@ -61,6 +62,7 @@ def load(path=LIB_PATH):
     sig("bic_ctx_destroy", i32, [vp])
     sig("bic_ctx_set_stream", i32, [vp, vp])
     sig("bic_ctx_get_stream", vp, [vp])
+    sig("bic_ctx_own_stream", vp, [vp])
     sig("bic_sync", i32, [vp])
     sig("bic_strerror", C.c_char_p, [i32])
     sig("bic_device_count", i32, [C.POINTER(i32)])
@@ -125,8 +127,10 @@ class Context:
 
     # -- plumbing ---------------------------------------------------------------------
     def _bind_stream(self):
+        # torch's current stream of the device (handle 0 = the null stream, which is what
+        # bic_ctx_set_stream(NULL) selects), so kernels order with torch's copies/allocations
         s = self.torch.cuda.current_stream(self.dev).cuda_stream
-        self.lib.bic_ctx_set_stream(self.h, C.c_void_p(s))
+        self.lib.bic_ctx_set_stream(self.h, C.c_void_p(s) if s else None)
 
     def _chk(self, rc, what):
         if rc != BIC_OK:
@@ -208,7 +212,9 @@ class Context:
     def golomb_encode_samples(self, samples, n0=0, a0=0, bit0=0, cap_words=None, out=None):
         """samples: int32 device tensor (uint32 values) -> (stream int64 [cap], bits int64[2])."""
         n = samples.numel()
-        cap_words = cap_words or max(1, (n * 40 + bit0 + 63) // 64 + 2)
+        if cap_words is None:  # always enough: sum(s >> k) <= sum(s), k + 1 <= 32 per sample
+            tot = int(samples.to(self.torch.int64).bitwise_and(0xFFFFFFFF).sum().item()) if n else 0
+            cap_words = max(1, (tot + 32 * n + bit0 + 63) // 64 + 1)
         if out is None:
             out = self.empty_i64(cap_words)
         bits = self.empty_i64(2)
@@ -227,7 +233,8 @@ class Context:
         wO = t.empty(nt, dtype=t.int32, device=self.dev)
         modes = t.empty(nt, dtype=t.uint8, device=self.dev)
         resid = self.empty_i64(rows, wpr) if want_resid else None
-        cap_words = cap_words or max(1, (nt * 48 + 63) // 64 + 2)
+        # sum of tile weights <= rows*cols, and k + 1 <= 32 per tile: always enough
+        cap_words = cap_words or max(1, (rows * cols + 32 * nt + 63) // 64 + 1)
         stream = self.empty_i64(cap_words)
         stats = self.empty_i64(3)
         lt = np.ascontiguousarray(lentab, np.uint64)

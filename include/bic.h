@@ -46,9 +46,12 @@ typedef struct bic_ctx bic_ctx;
 /* ---- context ----------------------------------------------------------------------------- */
 int bic_ctx_create(int device, bic_ctx** out);
 int bic_ctx_destroy(bic_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the ctx's own. */
+/* Enqueue on an external hipStream_t (e.g. torch's current stream); NULL is the HIP null
+ * (legacy default) stream. A new ctx enqueues on its own non-blocking stream, which
+ * bic_ctx_own_stream returns. */
 int bic_ctx_set_stream(bic_ctx* ctx, void* hip_stream);
 void* bic_ctx_get_stream(bic_ctx* ctx);
+void* bic_ctx_own_stream(bic_ctx* ctx);
 /* Wait for all work enqueued by this ctx; returns BIC_ENOSPC if an encode since the last
  * sync overflowed its slot (that plane's stream is then incomplete), else BIC_OK/BIC_EDEVICE. */
 int bic_sync(bic_ctx* ctx);
