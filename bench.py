@@ -132,8 +132,8 @@ class C3:
     def step(self):
         c, p = self.ctx, self.pybic
         c.bitplanes_u8(self.gray[self.k & 1], nplanes=8, out=self.planes)
-        c.encode_planes(self.planes, self.cols, True, p.CODER_GOLOMB, self.slot_g, self.out_g, self.bits_g)
-        c.encode_planes(self.planes, self.cols, True, p.CODER_EG, self.slot_e, self.out_e, self.bits_e)
+        c.encode_planes2(self.planes, self.cols, True, slots=(self.slot_g, self.slot_e),
+                         outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
         self.k += 1
 
     def out_bytes(self):
@@ -146,7 +146,7 @@ class C3:
         g = int(self.pybic.as_u64(self.bits_g).astype(np.int64).sum()) // 8
         e = int(self.pybic.as_u64(self.bits_e).astype(np.int64).sum()) // 8
         return {"bitplanes_u8": self.rows * self.cols + plane_b, "med_count": plane_b, "golomb_bits": plane_b,
-                "golomb_emit": plane_b + g, "eg_emit": plane_b + e}
+                "golomb_emit": plane_b + g, "eg_emit": plane_b + e, "encode_rows_golomb_eg": plane_b + g + e}
 
     def host_planes(self, rows):
         return self.pybic.as_u64(self.planes[:, :rows])
@@ -195,7 +195,8 @@ class C2(C3):
     def kernel_bytes(self):
         plane_b = self.rows * self.wpr * 8
         g = int(self.pybic.as_u64(self.bits_g)[0]) // 8
-        return {"med_count": plane_b, "golomb_bits": plane_b, "golomb_emit": plane_b + g}
+        return {"med_count": plane_b, "golomb_bits": plane_b, "golomb_emit": plane_b + g,
+                "encode_rows_golomb": plane_b + g}
 
     def check(self, oracle):
         P = self.pybic.as_u64(self.planes[0])
@@ -246,7 +247,8 @@ class C4(C3):
     def kernel_bytes(self):
         plane_b = self.nplanes * self.rows * self.wpr * 8
         g = int(self.pybic.as_u64(self.bits_g).astype(np.int64).sum()) // 8
-        return {"med_count": plane_b, "golomb_bits": plane_b, "golomb_emit": plane_b + g}
+        return {"med_count": plane_b, "golomb_bits": plane_b, "golomb_emit": plane_b + g,
+                "encode_rows_golomb": plane_b + g}
 
     def check(self, oracle):
         P = self.pybic.as_u64(self.planes[0])

@@ -20,13 +20,14 @@ struct bic_ctx {
   hipStream_t cur = nullptr;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
-  uint32_t* flags = nullptr;      // device [2]: overflow, domain
+  uint32_t* flags = nullptr;      // device [4]: overflow, domain, look-back timeout, spare
   uint64_t* lentab = nullptr;     // device copy of the tile length table
   size_t lentab_cap = 0;          // entries
   uint64_t* staging = nullptr;    // pinned host staging for lentab
   size_t staging_cap = 0;         // entries
   // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
   bool prof_on = false;
+  bool force_multipass = false;
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -134,8 +135,8 @@ int bic_ctx_create(int device, bic_ctx** out) {
     return BIC_EDEVICE;
   }
   ctx->cur = ctx->own;
-  if (hipMalloc(&ctx->flags, 2 * sizeof(uint32_t)) != hipSuccess ||
-      hipMemset(ctx->flags, 0, 2 * sizeof(uint32_t)) != hipSuccess) {
+  if (hipMalloc(&ctx->flags, 4 * sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(ctx->flags, 0, 4 * sizeof(uint32_t)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);
     delete ctx;
     return BIC_ENOMEM;
@@ -174,9 +175,10 @@ int bic_sync(bic_ctx* ctx) {
   if (rc) return rc;
   BIC_HIP(hipStreamSynchronize(ctx->cur));
   BIC_HIP(hipGetLastError());
-  uint32_t f[2] = {0, 0};
+  uint32_t f[4] = {0, 0, 0, 0};
   BIC_HIP(hipMemcpy(f, ctx->flags, sizeof(f), hipMemcpyDeviceToHost));
-  if (f[0] || f[1]) BIC_HIP(hipMemset(ctx->flags, 0, sizeof(f)));
+  if (f[0] || f[1] || f[2]) BIC_HIP(hipMemset(ctx->flags, 0, sizeof(f)));
+  if (f[2]) return BIC_EDEVICE;  // a look-back record never arrived (should not happen)
   if (f[1]) return BIC_EINVAL;
   if (f[0]) return BIC_ENOSPC;
   return BIC_OK;
@@ -188,6 +190,15 @@ int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols) {
   if (nplanes < 1 || !geom_ok(rows, cols, (cols + 63) / 64)) return BIC_EINVAL;
   const bic::Geom g = bic::make_geom(rows, cols, (cols + 63) / 64, nplanes);
   return ensure_scratch(ctx, bic::chunk_scratch_bytes(g));
+}
+
+int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
+  if (!ctx) return BIC_EINVAL;
+  if (option == BIC_OPT_MULTIPASS) {
+    ctx->force_multipass = value != 0;
+    return BIC_OK;
+  }
+  return BIC_EINVAL;
 }
 
 int bic_bitplanes_u8(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols,
@@ -226,38 +237,67 @@ size_t bic_encode_slot_words(size_t rows, size_t cols, int coder) {
   return (size_t)((2 * base + 63) / 64 + 64);
 }
 
-int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
-                      size_t wpr, int predict, int coder, uint64_t* out, size_t slot_words,
-                      uint64_t* plane_bits) {
+int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                       size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                       uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if (!plane_bits || nplanes < 1 || slot_words == 0) return BIC_EINVAL;
-  if (coder != BIC_CODER_GOLOMB && coder != BIC_CODER_EG) return BIC_EINVAL;
-  if (!geom_ok(rows, cols, wpr)) return BIC_EINVAL;
-  if (rows && (!planes || !out)) return BIC_EINVAL;
+  if (nplanes < 1 || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (!out_golomb && !out_eg) return BIC_EINVAL;
+  if (out_golomb && (!bits_golomb || slot_golomb == 0)) return BIC_EINVAL;
+  if (out_eg && (!bits_eg || slot_eg == 0)) return BIC_EINVAL;
+  if (rows && !planes) return BIC_EINVAL;
   if (rows == 0) {
-    BIC_HIP(hipMemsetAsync(plane_bits, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+    if (out_golomb) BIC_HIP(hipMemsetAsync(bits_golomb, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+    if (out_eg) BIC_HIP(hipMemsetAsync(bits_eg, 0, sizeof(uint64_t) * nplanes, ctx->cur));
     return BIC_OK;
   }
   const int pr = predict ? 1 : 0;
   const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
+  if (bic::fused_supported(g) && !ctx->force_multipass) {
+    // one pass: residual -> runs -> both streams (bic_fused.hip)
+    if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
+    const bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
+    timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg", [&] {
+      bic::launch_fused(ctx->cur, g, planes, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
+                        bits_eg, ctx->flags);
+    });
+    BIC_HIP(hipGetLastError());
+    return BIC_OK;
+  }
+  // rows wider than 16384 columns: multi-pass chunk kernels (bic_kernels.hip)
   if ((rc = ensure_scratch(ctx, bic::chunk_scratch_bytes(g)))) return rc;
   const bic::ChunkScratch cs = bic::carve_chunk_scratch(ctx->scratch, g);
   timed(ctx, "med_count", [&] { bic::launch_count(ctx->cur, g, planes, pr, cs, nullptr, nullptr); });
   timed(ctx, "scan_rows", [&] { bic::launch_scan_rows(ctx->cur, g, cs); });
-  if (coder == BIC_CODER_GOLOMB) {
+  if (out_golomb) {
     timed(ctx, "golomb_bits", [&] { bic::launch_golomb_bits(ctx->cur, g, planes, pr, cs); });
     timed(ctx, "golomb_offsets", [&] {
-      bic::launch_golomb_offsets(ctx->cur, g, cs, out, slot_words, plane_bits, ctx->flags);
+      bic::launch_golomb_offsets(ctx->cur, g, cs, out_golomb, slot_golomb, bits_golomb, ctx->flags);
     });
-    timed(ctx, "golomb_emit", [&] { bic::launch_golomb_emit(ctx->cur, g, planes, pr, cs, out, slot_words); });
-  } else {
+    timed(ctx, "golomb_emit", [&] {
+      bic::launch_golomb_emit(ctx->cur, g, planes, pr, cs, out_golomb, slot_golomb);
+    });
+  }
+  if (out_eg) {
     timed(ctx, "eg_emit", [&] {
-      bic::launch_eg_emit(ctx->cur, g, planes, pr, cs, out, slot_words, plane_bits, ctx->flags);
+      bic::launch_eg_emit(ctx->cur, g, planes, pr, cs, out_eg, slot_eg, bits_eg, ctx->flags);
     });
   }
   BIC_HIP(hipGetLastError());
   return BIC_OK;
+}
+
+int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                      size_t wpr, int predict, int coder, uint64_t* out, size_t slot_words,
+                      uint64_t* plane_bits) {
+  if (coder == BIC_CODER_GOLOMB)
+    return bic_encode_planes2(ctx, planes, nplanes, rows, cols, wpr, predict, out, slot_words, plane_bits,
+                              nullptr, 0, nullptr);
+  if (coder == BIC_CODER_EG)
+    return bic_encode_planes2(ctx, planes, nplanes, rows, cols, wpr, predict, nullptr, 0, nullptr, out,
+                              slot_words, plane_bits);
+  return BIC_EINVAL;
 }
 
 int bic_golomb_encode_samples(bic_ctx* ctx, const uint32_t* samples, size_t n, uint64_t n0,

@@ -1,0 +1,265 @@
+// bic_device.h -- device-side helpers shared by the HIP kernels (wave64 primitives, the
+// Golomb k rule, the med residual word, chunk/row bookkeeping). Included by .hip files only.
+#pragma once
+#include "bic_internal.h"
+
+#include <climits>
+
+namespace bic {
+
+#define BIC_MSB 0x8000000000000000ull
+constexpr int kBlock = 256;   // 4 waves
+constexpr int kWaves = kBlock / 64;
+constexpr int kLdsWords = 1024;  // u32 staging words per wave in the emitter (32768 bits)
+
+// ------------------------------------------------------------------------------------
+// wave / block primitives (wave64)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((unsigned)(v & 0xffffffffu), src);
+  const uint32_t hi = __shfl((unsigned)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+  const uint32_t lo = __shfl_up((unsigned)(v & 0xffffffffu), d);
+  const uint32_t hi = __shfl_up((unsigned)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_incl_sum_u64(uint64_t x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = shfl_up_u64(x, d);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_incl_max(int x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (l >= d) x = max(x, y);
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += shfl_u64(x, lane_id() ^ d);
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  return x;
+}
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = max(x, __shfl_xor(x, d));
+  return x;
+}
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d));
+  return x;
+}
+
+// Exclusive block scan for blockDim.x <= 1024 (<= 16 waves). tmp: >= 17 entries of LDS.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T x, T* tmp, T& total) {
+  const int l = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T inc;
+  if constexpr (sizeof(T) == 8) inc = wave_incl_sum_u64(x);
+  else inc = wave_incl_sum_u32(x);
+  if (l == 63) tmp[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    const T v = l < nw ? tmp[l] : T(0);
+    T vi;
+    if constexpr (sizeof(T) == 8) vi = wave_incl_sum_u64(v);
+    else vi = wave_incl_sum_u32(v);
+    if (l < nw) tmp[l] = vi - v;
+    if (l == nw - 1) tmp[16] = vi;
+  }
+  __syncthreads();
+  const T res = tmp[w] + inc - x;
+  total = tmp[16];
+  __syncthreads();
+  return res;
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// blocks that share an XCD (b % 8 equal) get a contiguous range of logical ids, so the
+// chunks of consecutive rows -- which re-read each other as the row above -- share an L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
+  if (nb < 16) return b;
+  const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// GolombCoder.cpp:33 for n >= 1 samples with accumulated error A (A < 2^31):
+// the smallest k >= 0 with (n << k) >= A, found from the two leading-one positions.
+__device__ __forceinline__ uint32_t golomb_k(uint32_t n, uint32_t A) {
+  if (A <= n) return 0;
+  uint32_t k = (uint32_t)(__clz((int)n) - __clz((int)A));
+  return k + ((n << k) < A ? 1u : 0u);
+}
+__device__ __forceinline__ uint32_t golomb_k_state(uint32_t n, uint32_t A) {
+  return n == 0 ? 1u : golomb_k(n, A);  // Golomb.h:18 -- a fresh coder starts at k = 1
+}
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// ------------------------------------------------------------------------------------
+// residual word of a chunk step (med in word form), shared by every chunk kernel
+// ------------------------------------------------------------------------------------
+struct RowCtx {
+  const uint64_t* cur;  // row i
+  const uint64_t* up;   // row i-1 (nullptr for i = 0)
+  uint64_t pcarry, ucarry;  // left neighbours of lane 0 for the next step
+};
+
+__device__ __forceinline__ RowCtx row_ctx(const uint64_t* planes, const Geom& g, uint32_t plane,
+                                          uint32_t row, uint32_t c0) {
+  RowCtx rc;
+  rc.cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
+  rc.up = row ? rc.cur - g.wpr : nullptr;
+  rc.pcarry = c0 ? rc.cur[c0 - 1] : 0;
+  rc.ucarry = (c0 && rc.up) ? rc.up[c0 - 1] : 0;
+  return rc;
+}
+
+template <bool PREDICT>
+__device__ __forceinline__ uint64_t resid_word(RowCtx& rc, const Geom& g, uint32_t row, uint32_t w) {
+  const bool valid = w < g.used;
+  const uint64_t p = valid ? rc.cur[w] : 0;
+  uint64_t r;
+  if constexpr (PREDICT) {
+    const uint64_t u = (valid && rc.up) ? rc.up[w] : 0;
+    uint64_t pl = shfl_up_u64(p, 1), ul = shfl_up_u64(u, 1);
+    if (lane_id() == 0) { pl = rc.pcarry; ul = rc.ucarry; }
+    rc.pcarry = shfl_u64(p, 63);
+    rc.ucarry = shfl_u64(u, 63);
+    r = p ^ u ^ ((p >> 1) | (pl << 63)) ^ ((u >> 1) | (ul << 63));
+    if (row == 0 && w == 0) r &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+  } else {
+    r = p;
+  }
+  if (w == g.used - 1) r &= g.trail;
+  return valid ? r : 0;
+}
+
+struct ChunkId {
+  uint32_t plane, row, c;
+  uint64_t id;
+  bool ok;
+};
+__device__ __forceinline__ ChunkId chunk_id(const Geom& g) {
+  ChunkId ci;
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  ci.id = (uint64_t)b * kWaves + (threadIdx.x >> 6);
+  ci.ok = ci.id < g.nchunks;
+  const uint64_t id = ci.ok ? ci.id : 0;
+  ci.plane = (uint32_t)(id / g.chunks_per_plane);
+  const uint64_t r = id % g.chunks_per_plane;
+  ci.row = (uint32_t)(r / g.cpr);
+  ci.c = (uint32_t)(r % g.cpr);
+  return ci;
+}
+
+// ------------------------------------------------------------------------------------
+// Shared per-step bookkeeping of the Golomb kernels: for the lane's word, the sample
+// index of its first 1 and the column of the last 1 before it in the row.
+// ------------------------------------------------------------------------------------
+struct StepState {
+  uint32_t n_carry;
+  int jp_carry;
+};
+
+__device__ __forceinline__ void step_prefix(uint64_t r, uint32_t w, StepState& st, uint32_t& n_w,
+                                            int& jp_w) {
+  const uint32_t pc = (uint32_t)__popcll(r);
+  const uint32_t inc = wave_incl_sum_u32(pc);
+  n_w = st.n_carry + inc - pc;
+  st.n_carry += __shfl(inc, 63);
+  const int lastc = r ? (int)(w * 64 + 63 - __builtin_ctzll(r)) : -1;
+  const int mx = wave_incl_max(lastc);
+  int ex = __shfl_up(mx, 1);
+  if (lane_id() == 0) ex = -1;
+  jp_w = max(st.jp_carry, ex);
+  st.jp_carry = max(st.jp_carry, __shfl(mx, 63));
+}
+
+
+// Codeword sinks: OR the bits of a codeword (k-bit binary part, then the '1' after the
+// unary zeros) into an LDS image (u32 words) or into global big-endian 64-bit words.
+struct LdsSink {
+  uint32_t* buf;
+  uint32_t idx, cur;
+  __device__ __forceinline__ void flush() {
+    if (cur) atomicOr(&buf[idx], cur);
+    cur = 0;
+  }
+  __device__ __forceinline__ void orw(uint32_t i, uint32_t v) {
+    if (i != idx) { flush(); idx = i; }
+    cur |= v;
+  }
+  // nb <= 32 bits of v at local bit offset off (MSB-first)
+  __device__ __forceinline__ void put(uint32_t off, uint32_t v, uint32_t nb) {
+    const uint32_t i = off >> 5, sh = off & 31;
+    if (sh + nb <= 32) {
+      orw(i, v << (32 - sh - nb));
+    } else {
+      orw(i, v >> (sh + nb - 32));
+      orw(i + 1, v << (64 - sh - nb));
+    }
+  }
+  __device__ __forceinline__ void bit(uint32_t off) { orw(off >> 5, 0x80000000u >> (off & 31)); }
+};
+
+struct GlobalSink {
+  unsigned long long* buf;  // big-endian 64-bit words
+  uint64_t idx, cur;
+  __device__ __forceinline__ void flush() {
+    if (cur) atomicOr(&buf[idx], (unsigned long long)bswap64(cur));
+    cur = 0;
+  }
+  __device__ __forceinline__ void orw(uint64_t i, uint64_t v) {
+    if (i != idx) { flush(); idx = i; }
+    cur |= v;
+  }
+  __device__ __forceinline__ void put(uint64_t off, uint32_t v, uint32_t nb) {
+    const uint64_t i = off >> 6;
+    const uint32_t sh = (uint32_t)(off & 63);
+    if (sh + nb <= 64) {
+      orw(i, (uint64_t)v << (64 - sh - nb));
+    } else {
+      orw(i, (uint64_t)v >> (sh + nb - 64));
+      orw(i + 1, (uint64_t)v << (128 - sh - nb));
+    }
+  }
+  __device__ __forceinline__ void bit(uint64_t off) { orw(off >> 6, BIC_MSB >> (off & 63)); }
+};
+
+template <typename Sink, typename Off>
+__device__ __forceinline__ void emit_codeword(Sink& sk, Off off, uint32_t s, uint32_t k) {
+  if (k) {
+    const uint32_t bin = s & ((1u << k) - 1u);
+    if (bin) sk.put(off, bin, k);
+  }
+  sk.bit(off + k + (s >> k));
+}
+
+}  // namespace bic

@@ -1,0 +1,554 @@
+// bic_fused.hip -- single-pass row encoder for rows of up to 256 words (16384 columns):
+// med residual -> per-row runs -> Golomb stream and/or EG stream, one wavefront per row.
+//
+// Semantics are those of bic_kernels.hip (GolombCoder.cpp:13-34, eg.cpp:20-37, pred.cpp:3-15);
+// the difference is the schedule:
+//  * rows are claimed in order through an atomic counter, so every row a wave looks back at
+//    was claimed earlier and is resident or finished (no deadlock);
+//  * the row's 1-count is published at once and a decoupled look-back over the earlier rows
+//    of the plane yields the number of samples before the row (the Golomb coder state);
+//  * every codeword is computed ONCE: each lane turns its word into a register string
+//    (first codeword's binary part, its unary zeros, then <= 128 bits), or -- when the k
+//    bounds prove k = 0 for every codeword of the word -- copies the word's bits (a k = 0
+//    codeword is exactly the run's zeros and its 1);
+//  * lane strings are OR'd into an LDS row image; the row's bit length is published and a
+//    second look-back gives its offset; whole 64-bit words go to HBM with plain stores and
+//    the (at most two) words shared with neighbouring rows go to a fragment table that the
+//    fixup kernel combines (no atomics on the output, no pre-zeroing of the output).
+// Inter-workgroup records are 8-byte {flag, value} granules written and polled with
+// agent-scope atomics (cdna_hip_programming.md §6 Guideline 16, R2), spins bounded.
+#include "bic_device.h"
+
+namespace bic {
+
+constexpr int kGImg = 1536;   // u32 words of Golomb row image per wave (49152 bits)
+constexpr int kEImg = 520;    // u32 words of EG row image per wave (cols <= 16384)
+constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads ahead)
+constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+__device__ __forceinline__ void rec_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t rec_load(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix of the record values [base, me): decoupled look-back by one wave, 64
+// predecessors per probe; stops at the nearest inclusive record. Bounded spin.
+__device__ uint64_t lookback(uint64_t* recs, uint64_t base, uint64_t me, uint32_t* flags) {
+  uint64_t excl = 0;
+  int64_t pos = (int64_t)me - 1;
+  const int lane = lane_id();
+  uint32_t spins = 0;
+  while (pos >= (int64_t)base) {
+    const int64_t idx = pos - lane;
+    const uint64_t r = idx >= (int64_t)base ? rec_load(&recs[idx]) : kInc;
+    const uint64_t fl = r >> 62;
+    const uint64_t inc = __ballot(fl == 2);
+    const uint64_t bad = __ballot(fl == 0);
+    const int stop = inc ? __builtin_ctzll(inc) : 64;
+    const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
+    if (bad & need) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {  // ~seconds: a record never arrived
+        if (lane == 0) atomicOr(&flags[2], 1u);
+        return excl;
+      }
+      continue;
+    }
+    excl += wave_sum_u64(lane <= stop ? (r & kValMask) : 0);
+    if (stop < 64) break;
+    pos -= 64;
+  }
+  return excl;
+}
+
+// One lane's codewords for one residual word.
+struct LaneEnc {
+  uint32_t head, k0, z;  // first codeword: k0-bit binary part, then z unary zeros
+  uint64_t t0, t1;       // the rest (starting with the first codeword's '1'), MSB-first
+  uint32_t tlen;
+  uint32_t len;          // total bits
+  bool lng;              // rest longer than 128 bits: placed by re-iteration
+};
+
+__device__ __forceinline__ void tail_put(LaneEnc& e, uint64_t cw, uint32_t nb) {  // nb 1..64
+  const uint32_t pos = e.tlen;
+  e.tlen = pos + nb;
+  if (pos + nb > 128) { e.lng = true; return; }
+  const uint32_t sh = 128 - pos - nb;
+  if (sh >= 64) {
+    e.t0 |= cw << (sh - 64);
+  } else {
+    e.t1 |= cw << sh;
+    if (sh + nb > 64) e.t0 |= cw >> (64 - sh);
+  }
+}
+
+__device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t n, int jp, uint32_t arow,
+                                               bool eol, uint32_t cols) {
+  LaneEnc e{0, 0, 0, 0, 0, 0, 0, false};
+  if (!x && !eol) return e;
+  if (x && n) {
+    // A never decreases, n only grows: if even the largest A of this word is <= its smallest n,
+    // every codeword here (and the EOL's, n + m >= n) has k = 0 and is the run's bits verbatim.
+    const uint32_t m = (uint32_t)__popcll(x);
+    const uint32_t plast = w * 64 + 63 - (uint32_t)__builtin_ctzll(x);
+    const uint32_t aup = arow + plast - (n + m - 1);
+    if (aup <= n) {
+      e.z = w * 64 - (uint32_t)(jp + 1);
+      e.t0 = x;
+      if (!eol) {
+        e.tlen = plast - w * 64 + 1;
+      } else {
+        const uint32_t p = cols - w * 64;  // the EOL codeword's '1'
+        if (p < 64) e.t0 |= BIC_MSB >> p; else e.t1 = BIC_MSB;
+        e.tlen = p + 1;
+      }
+      e.len = e.z + e.tlen;
+      return e;
+    }
+  }
+  bool first = true;
+  for (;;) {
+    int j;
+    uint32_t s;
+    if (x) {
+      const int cz = __builtin_clzll(x);
+      x ^= BIC_MSB >> cz;
+      j = (int)(w * 64) + cz;
+      s = (uint32_t)(j - jp - 1);
+    } else if (eol) {
+      j = (int)cols;
+      s = cols - 1 - (uint32_t)jp;
+      eol = false;
+    } else {
+      break;
+    }
+    const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
+    const uint32_t q = s >> k;
+    const uint32_t bin = s & ((1u << k) - 1u);
+    if (first) {
+      e.head = bin;
+      e.k0 = k;
+      e.z = q;
+      tail_put(e, 1, 1);
+      first = false;
+    } else {
+      tail_put(e, ((uint64_t)bin << (q + 1)) | 1ull, k + q + 1);  // s <= 63 here: k + q + 1 <= 64
+    }
+    e.len += k + q + 1;
+    ++n;
+    jp = j;
+  }
+  return e;
+}
+
+// Emit one word's codewords through a sink at bit offset `off` (fallback paths).
+template <typename Sink, typename Off>
+__device__ __forceinline__ void emit_word(Sink& sk, Off off, uint64_t x, uint32_t w, uint32_t n, int jp,
+                                          uint32_t arow, bool eol, uint32_t cols) {
+  for (;;) {
+    int j;
+    uint32_t s;
+    if (x) {
+      const int cz = __builtin_clzll(x);
+      x ^= BIC_MSB >> cz;
+      j = (int)(w * 64) + cz;
+      s = (uint32_t)(j - jp - 1);
+    } else if (eol) {
+      j = (int)cols;
+      s = cols - 1 - (uint32_t)jp;
+      eol = false;
+    } else {
+      break;
+    }
+    const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
+    if (k) {
+      const uint32_t bin = s & ((1u << k) - 1u);
+      if (bin) sk.put(off, bin, k);
+    }
+    sk.bit(off + k + (s >> k));
+    off += k + (s >> k) + 1;
+    ++n;
+    jp = j;
+  }
+}
+
+__device__ __forceinline__ void lds_or(uint32_t* img, uint32_t i, uint32_t v) {
+  if (v) atomicOr(&img[i], v);
+}
+
+// OR tlen (<= 128) bits (A:B, MSB-first) into the image at bit `off`.
+__device__ __forceinline__ void place128(uint32_t* img, uint32_t off, uint64_t A, uint64_t B, uint32_t tlen) {
+  if (!tlen) return;
+  const uint32_t i = off >> 5, sh = off & 31;
+  uint64_t D0 = A, D1 = B, D2 = 0;
+  if (sh) {
+    D0 = A >> sh;
+    D1 = (A << (64 - sh)) | (B >> sh);
+    D2 = B << (64 - sh);
+  }
+  const uint32_t nw = (sh + tlen + 31) >> 5;
+  lds_or(img, i, (uint32_t)(D0 >> 32));
+  if (nw > 1) lds_or(img, i + 1, (uint32_t)D0);
+  if (nw > 2) lds_or(img, i + 2, (uint32_t)(D1 >> 32));
+  if (nw > 3) lds_or(img, i + 3, (uint32_t)D1);
+  if (nw > 4) lds_or(img, i + 4, (uint32_t)(D2 >> 32));
+}
+
+__device__ __forceinline__ void place_small(uint32_t* img, uint32_t off, uint32_t v, uint32_t nb) {
+  if (!nb || !v) return;
+  const uint32_t i = off >> 5, sh = off & 31;
+  if (sh + nb <= 32) {
+    lds_or(img, i, v << (32 - sh - nb));
+  } else {
+    lds_or(img, i, v >> (sh + nb - 32));
+    lds_or(img, i + 1, v << (64 - sh - nb));
+  }
+}
+
+// 64 image bits starting at bit a (a may be negative: leading zeros).
+__device__ __forceinline__ uint64_t raw64(const uint32_t* img, int64_t a) {
+  if (a <= -64) return 0;
+  if (a < 0) return raw64(img, 0) >> (-a);
+  const uint32_t i = (uint32_t)(a >> 5), sh = (uint32_t)(a & 31);
+  const uint64_t hi = ((uint64_t)img[i] << 32) | img[i + 1];
+  return sh ? (hi << sh) | (img[i + 2] >> (32 - sh)) : hi;
+}
+
+// Same, of the image with a '0' inserted at position ins (ins < 0: no insertion).
+__device__ __forceinline__ uint64_t img64(const uint32_t* img, int64_t a, int64_t ins) {
+  if (ins < 0 || ins >= a + 64) return raw64(img, a);
+  const uint64_t Y = raw64(img, a - 1);
+  if (ins < a) return Y;
+  const uint32_t q = (uint32_t)(ins - a);
+  const uint64_t X = raw64(img, a);
+  const uint64_t hi = q ? ~(~0ull >> q) : 0ull;
+  const uint64_t lo = q == 63 ? 0ull : (~0ull >> (q + 1));
+  return (X & hi) | (Y & lo);
+}
+
+// Is output word w entirely inside the row's bit range [G, G+L)?
+__device__ __forceinline__ bool word_complete(uint64_t w, uint64_t G, uint64_t L) {
+  return w * 64 >= G && w * 64 + 64 <= G + L;
+}
+
+// Write a row image of L bits to absolute bit G of out: whole words with plain stores, the
+// first/last word (when shared with another row) into frag[0]/frag[1].
+__device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint64_t G, int64_t ins,
+                                          uint64_t* out, uint64_t* frag) {
+  const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6, nw = w1 - w0 + 1;
+  for (uint64_t t = lane_id(); t < nw; t += 64) {
+    const uint64_t wb = (w0 + t) * 64;
+    const uint64_t v = img64(img, (int64_t)wb - (int64_t)G, ins);
+    if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
+    else frag[t == 0 ? 0 : 1] = v;
+  }
+}
+
+struct FusedArgs {
+  Geom g;
+  const uint64_t* planes;
+  uint32_t* counter;   // zeroed per launch
+  uint64_t* ones_rec;  // zeroed per launch
+  uint64_t* bits_rec;  // zeroed per launch
+  uint64_t *gboff, *glen, *gfrag;
+  uint64_t *eboff, *elen, *efrag;
+  uint64_t* out_g;
+  uint64_t slot_g;
+  uint64_t* bits_g;
+  uint64_t* out_e;
+  uint64_t slot_e;
+  uint64_t* bits_e;
+  uint32_t* flags;
+};
+
+// Global-memory emission for a row whose Golomb image does not fit the LDS window: codeword
+// bits landing in the row's first/last output word are kept for the fragment table, the rest
+// is OR'd into words this wave zeroed first.
+struct FragSink {
+  unsigned long long* out;
+  uint64_t wh, wt;
+  bool hpart, tpart;
+  uint64_t acc_h, acc_t;
+  uint64_t idx, cur;
+  __device__ __forceinline__ void flush() {
+    if (!cur) return;
+    if (idx == wh && hpart) acc_h |= cur;
+    else if (idx == wt && tpart) acc_t |= cur;
+    else atomicOr(&out[idx], (unsigned long long)bswap64(cur));
+    cur = 0;
+  }
+  __device__ __forceinline__ void orw(uint64_t i, uint64_t v) {
+    if (i != idx) { flush(); idx = i; }
+    cur |= v;
+  }
+  __device__ __forceinline__ void put(uint64_t off, uint32_t v, uint32_t nb) {
+    const uint64_t i = off >> 6;
+    const uint32_t sh = (uint32_t)(off & 63);
+    if (sh + nb <= 64) {
+      orw(i, (uint64_t)v << (64 - sh - nb));
+    } else {
+      orw(i, (uint64_t)v >> (sh + nb - 64));
+      orw(i + 1, (uint64_t)v << (128 - sh - nb));
+    }
+  }
+  __device__ __forceinline__ void bit(uint64_t off) { orw(off >> 6, BIC_MSB >> (off & 63)); }
+};
+
+template <int WPL, bool PREDICT>
+__device__ __noinline__ void golomb_row_global(const FusedArgs& a, const uint64_t (&r)[WPL], uint32_t row,
+                                               uint32_t nbase, uint64_t G, uint64_t L, uint64_t* frag) {
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  const uint64_t wh = G >> 6, wt = (G + L - 1) >> 6;
+  const bool hpart = !word_complete(wh, G, L);
+  const bool tpart = !word_complete(wt, G, L);
+  for (uint64_t i = wh + lane; i <= wt; i += 64)
+    if (!((i == wh && hpart) || (i == wt && tpart))) a.out_g[i] = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  FragSink fs{reinterpret_cast<unsigned long long*>(a.out_g), wh, wt, hpart, tpart, 0, 0, 0, 0};
+  StepState st{nbase, -1};
+  const uint32_t arow = row * (g.cols + 1);
+  uint64_t carry = G;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = t * 64 + lane;
+    uint32_t n;
+    int jp;
+    step_prefix(r[t], w, st, n, jp);
+    const bool eol = w == g.used - 1;
+    const LaneEnc e = encode_word(r[t], w, n, jp, arow, eol, g.cols);
+    const uint32_t inc = wave_incl_sum_u32(e.len);
+    const uint64_t off = carry + inc - e.len;
+    carry += __shfl(inc, 63);
+    emit_word(fs, off, r[t], w, n, jp, arow, eol, g.cols);
+  }
+  fs.flush();
+  uint64_t h = fs.acc_h, tl = fs.acc_t;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    h |= shfl_u64(h, lane ^ d);
+    tl |= shfl_u64(tl, lane ^ d);
+  }
+  if (lane == 0) {
+    if (hpart) frag[0] = h | (wh == wt ? tl : 0);
+    if (tpart && wt != wh) frag[1] = tl;
+  }
+}
+
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+__global__ __launch_bounds__(256) void k_encode_rows(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * (kGImg + kEImg)];
+  const Geom& g = a.g;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t* gimg = lds + wave * (kGImg + kEImg);
+  uint32_t* eimg = gimg + kGImg;
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  uint32_t id32 = 0;
+  if (lane == 0) id32 = atomicAdd(a.counter, 1u);
+  const uint64_t id = (uint64_t)__shfl(id32, 0);
+  if (id >= nrows) return;
+  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+  const uint64_t pbase = (uint64_t)plane * g.rows;
+  RowCtx rc = row_ctx(a.planes, g, plane, row, 0);
+
+  uint64_t r[WPL];
+  uint32_t ones = 0;
+  int fcol = INT_MAX;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = t * 64 + lane;
+    r[t] = resid_word<PREDICT>(rc, g, row, w);
+    ones += (uint32_t)__popcll(r[t]);
+    if (r[t] && fcol == INT_MAX) fcol = (int)(w * 64 + __builtin_clzll(r[t]));
+  }
+  ones = wave_sum_u32(ones);
+
+  // ---- samples before this row: ones of earlier rows (+ one EOL sample per row) ----
+  uint64_t O;
+  if (row == 0) {
+    O = 0;
+    if (lane == 0) rec_store(&a.ones_rec[id], kInc | ones);
+  } else {
+    if (lane == 0) rec_store(&a.ones_rec[id], kAgg | ones);
+    O = lookback(a.ones_rec, pbase, id, a.flags);
+    if (lane == 0) rec_store(&a.ones_rec[id], kInc | (O + ones));
+  }
+
+  // ---- EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1 ----
+  if constexpr (DO_E) {
+    const bool f_here = O == 0 && ones > 0;
+    fcol = wave_min(fcol);
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = t * 64 + lane;
+      if (w < g.used) {
+        const uint64_t v = ~r[t] & (w == g.used - 1 ? g.trail : ~0ull);
+        eimg[2 * w] = (uint32_t)(v >> 32);
+        eimg[2 * w + 1] = (uint32_t)v;
+      }
+    }
+    if (lane < kPad + 1) eimg[2 * g.used + lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) eimg[g.cols >> 5] |= 0x80000000u >> (g.cols & 31);  // EOL '1'
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
+    const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
+    const uint64_t cap = a.slot_e * 64;
+    const uint64_t Ge = (uint64_t)plane * cap + Ge_rel;
+    if (Ge_rel + Le <= cap) {
+      write_row(eimg, Le, Ge, f_here ? (int64_t)fcol + 1 : -1, a.out_e, a.efrag + 2 * id);
+      if (lane == 0) { a.eboff[id] = Ge; a.elen[id] = Le; }
+    } else if (lane == 0) {
+      a.eboff[id] = Ge;
+      a.elen[id] = 0;  // overflowed: nothing written, fixup skips
+      atomicOr(&a.flags[0], 1u);
+    }
+    if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
+  }
+
+  // ---- Golomb ------------------------------------------------------------------------------
+  if constexpr (DO_G) {
+    StepState st{(uint32_t)(O + row), -1};
+    const uint32_t arow = row * (g.cols + 1);
+    constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+    uint64_t loc = 0;
+    bool fits = true;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = t * 64 + lane;
+      uint32_t n;
+      int jp;
+      step_prefix(r[t], w, st, n, jp);
+      const bool eol = w == g.used - 1;
+      const LaneEnc e = encode_word(r[t], w, n, jp, arow, eol, g.cols);
+      const uint32_t inc = wave_incl_sum_u32(e.len);
+      const uint64_t off = loc + inc - e.len;
+      const uint64_t start = loc;
+      loc += __shfl(inc, 63);
+      if (fits && loc <= kCapBits) {
+        for (uint32_t i = (uint32_t)((start + 31) >> 5) + lane; i < (uint32_t)((loc + 31) >> 5); i += 64) gimg[i] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (!e.lng) {
+          place_small(gimg, (uint32_t)off, e.head, e.k0);
+          place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
+        } else {
+          LdsSink ls{gimg, 0, 0};
+          emit_word(ls, (uint32_t)off, r[t], w, n, jp, arow, eol, g.cols);
+          ls.flush();
+        }
+      } else {
+        fits = false;
+      }
+    }
+    const uint64_t L = loc;
+    uint64_t Grel;
+    if (row == 0) {
+      Grel = 0;
+      if (lane == 0) rec_store(&a.bits_rec[id], kInc | L);
+    } else {
+      if (lane == 0) rec_store(&a.bits_rec[id], kAgg | L);
+      Grel = lookback(a.bits_rec, pbase, id, a.flags);
+      if (lane == 0) rec_store(&a.bits_rec[id], kInc | (Grel + L));
+    }
+    const uint64_t cap = a.slot_g * 64;
+    const uint64_t G = (uint64_t)plane * cap + Grel;
+    if (lane == 0 && row == g.rows - 1) a.bits_g[plane] = Grel + L;
+    if (Grel + L <= cap) {
+      if (fits) {
+        const uint32_t endw = (uint32_t)((L + 31) >> 5);
+        if (lane < kPad) gimg[endw + lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        write_row(gimg, L, G, -1, a.out_g, a.gfrag + 2 * id);
+      } else {
+        golomb_row_global<WPL, PREDICT>(a, r, row, (uint32_t)(O + row), G, L, a.gfrag + 2 * id);
+      }
+      if (lane == 0) { a.gboff[id] = G; a.glen[id] = L; }
+    } else if (lane == 0) {
+      a.gboff[id] = G;
+      a.glen[id] = 0;
+      atomicOr(&a.flags[0], 1u);
+    }
+  }
+}
+
+// Combine the fragments of the words rows share: the row holding a shared word's first bit
+// owns it and ORs in the head fragments of the following rows that start inside that word.
+__global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff, const uint64_t* __restrict__ len,
+                                               const uint64_t* __restrict__ frag, uint64_t* __restrict__ out,
+                                               uint32_t rows, uint64_t nrows) {
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= nrows) return;
+  const uint64_t G = boff[id], L = len[id];
+  if (L == 0) return;
+  const uint64_t wt = (G + L - 1) >> 6, wh = G >> 6;
+  const uint64_t wb = wt * 64;
+  if (wb < G) return;                     // the word's first bit belongs to an earlier row
+  if (wb + 64 <= G + L) return;           // a whole word of this row: already stored
+  uint64_t v = (wh == wt) ? frag[2 * id] : frag[2 * id + 1];
+  const uint64_t pend = (id / rows + 1) * (uint64_t)rows;
+  for (uint64_t r2 = id + 1; r2 < pend; ++r2) {
+    if (len[r2] == 0 || boff[r2] >= wb + 64) break;
+    v |= frag[2 * r2];
+  }
+  out[wt] = bswap64(v);
+}
+
+// ------------------------------------------------------------------------------------
+size_t fused_scratch_bytes(const Geom& g) {
+  const size_t n = (size_t)g.rows * g.nplanes;
+  return 256 + n * 8 * 2 + n * 8 * 8 + 1024;
+}
+
+FusedScratch carve_fused_scratch(void* base, const Geom& g) {
+  const size_t n = (size_t)g.rows * g.nplanes;
+  char* p = reinterpret_cast<char*>(base);
+  FusedScratch fs;
+  fs.counter = reinterpret_cast<uint32_t*>(p);
+  fs.ones_rec = reinterpret_cast<uint64_t*>(p + 256);
+  fs.bits_rec = fs.ones_rec + n;
+  fs.zero_bytes = 256 + n * 16;
+  uint64_t* q = fs.bits_rec + n;
+  fs.gboff = q; q += n;
+  fs.glen = q; q += n;
+  fs.gfrag = q; q += 2 * n;
+  fs.eboff = q; q += n;
+  fs.elen = q; q += n;
+  fs.efrag = q;
+  return fs;
+}
+
+bool fused_supported(const Geom& g) { return g.used <= 256; }
+
+void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, const FusedScratch& fs,
+                  uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
+                  uint64_t* bits_e, uint32_t* flags) {
+  (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
+  FusedArgs a{g, planes, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.eboff,
+              fs.elen, fs.efrag, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  const uint32_t grid = (uint32_t)((nrows + 3) / 4);
+  const bool dg = out_g != nullptr, de = out_e != nullptr;
+#define BIC_FUSED(W, P)                                                               \
+  if (dg && de) k_encode_rows<W, P, true, true><<<grid, 256, 0, s>>>(a);              \
+  else if (dg) k_encode_rows<W, P, true, false><<<grid, 256, 0, s>>>(a);              \
+  else k_encode_rows<W, P, false, true><<<grid, 256, 0, s>>>(a);
+  const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
+  if (predict) {
+    if (wpl == 1) { BIC_FUSED(1, true) } else if (wpl == 2) { BIC_FUSED(2, true) } else { BIC_FUSED(4, true) }
+  } else {
+    if (wpl == 1) { BIC_FUSED(1, false) } else if (wpl == 2) { BIC_FUSED(2, false) } else { BIC_FUSED(4, false) }
+  }
+#undef BIC_FUSED
+  const uint32_t fgrid = (uint32_t)((nrows + 255) / 256);
+  if (dg) k_fixup<<<fgrid, 256, 0, s>>>(fs.gboff, fs.glen, fs.gfrag, out_g, g.rows, nrows);
+  if (de) k_fixup<<<fgrid, 256, 0, s>>>(fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows);
+}
+
+}  // namespace bic

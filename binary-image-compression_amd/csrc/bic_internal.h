@@ -77,6 +77,20 @@ void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t 
                   uint32_t* w_nonpred, uint32_t* w_pred, uint8_t* modes, uint64_t* resid,
                   uint64_t* stats);
 
+// Single-pass row encoder (bic_fused.hip), rows of at most 256 words.
+struct FusedScratch {
+  uint32_t* counter;
+  uint64_t *ones_rec, *bits_rec;
+  size_t zero_bytes;  // counter + records, zeroed per launch
+  uint64_t *gboff, *glen, *gfrag, *eboff, *elen, *efrag;
+};
+size_t fused_scratch_bytes(const Geom& g);
+FusedScratch carve_fused_scratch(void* base, const Geom& g);
+bool fused_supported(const Geom& g);
+void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, const FusedScratch& fs,
+                  uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
+                  uint64_t* bits_e, uint32_t* flags);
+
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
 

@@ -23,7 +23,7 @@ EXPORTS = [
     "bic_ctx_create", "bic_ctx_destroy", "bic_ctx_set_stream", "bic_ctx_get_stream", "bic_ctx_own_stream",
     "bic_sync",
     "bic_strerror", "bic_device_count", "bic_reserve", "bic_bitplanes_u8", "bic_med_residual",
-    "bic_encode_planes", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
+    "bic_encode_planes", "bic_encode_planes2", "bic_ctx_set_option", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
 ]
 
@@ -71,6 +71,8 @@ def load(path=LIB_PATH):
     sig("bic_med_residual", i32, [vp, vp, i32, sz, sz, sz, i32, vp, vp])
     sig("bic_encode_planes", i32, [vp, vp, i32, sz, sz, sz, i32, i32, vp, sz, vp])
     sig("bic_encode_slot_words", sz, [sz, sz, i32])
+    sig("bic_encode_planes2", i32, [vp, vp, i32, sz, sz, sz, i32, vp, sz, vp, vp, sz, vp])
+    sig("bic_ctx_set_option", i32, [vp, i32, C.c_long])
     sig("bic_golomb_encode_samples", i32, [vp, vp, sz, u64, u64, u32, vp, sz, vp])
     sig("bic_patch_encode", i32, [vp, vp, sz, sz, sz, u32, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_pack_streams", i32, [vp, vp, i32, sz, vp, vp, vp])
@@ -208,6 +210,30 @@ class Context:
         self._chk(self.lib.bic_encode_planes(self.h, _p(planes), n, rows, cols, wpr, int(predict), coder,
                                              _p(out), slot_words, _p(plane_bits)), "bic_encode_planes")
         return out, plane_bits
+
+    def encode_planes2(self, planes, cols, predict=True, golomb=True, eg=True, slots=(None, None),
+                       outs=(None, None), bits=(None, None)):
+        """both streams in one pass -> ((out_g, bits_g) or None, (out_e, bits_e) or None)."""
+        planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
+        n, rows, wpr = planes.shape
+        res = []
+        for on, coder, slot, out, b in ((golomb, CODER_GOLOMB, slots[0], outs[0], bits[0]),
+                                        (eg, CODER_EG, slots[1], outs[1], bits[1])):
+            if not on:
+                res.append((None, 0, None))
+                continue
+            slot = slot or self.slot_words(rows, cols, coder)
+            out = self.empty_i64(n, slot) if out is None else out
+            b = self.empty_i64(n) if b is None else b
+            res.append((out, slot, b))
+        (og, sg, bg), (oe, se, be) = res
+        self._bind_stream()
+        self._chk(self.lib.bic_encode_planes2(self.h, _p(planes), n, rows, cols, wpr, int(predict), _p(og), sg,
+                                              _p(bg), _p(oe), se, _p(be)), "bic_encode_planes2")
+        return (og, bg) if golomb else None, (oe, be) if eg else None
+
+    def set_multipass(self, on=True):
+        self._chk(self.lib.bic_ctx_set_option(self.h, 1, int(on)), "bic_ctx_set_option")
 
     def golomb_encode_samples(self, samples, n0=0, a0=0, bit0=0, cap_words=None, out=None):
         """samples: int32 device tensor (uint32 values) -> (stream int64 [cap], bits int64[2])."""

@@ -59,6 +59,10 @@ const char* bic_strerror(int code);
 int bic_device_count(int* n);
 /* Pre-grow the ctx scratch so later calls do not allocate (needed before stream capture). */
 int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
+/* Options: BIC_OPT_MULTIPASS = 1 forces the multi-pass chunk kernels for every geometry
+ * (cross-checking the fused encoder); 0 (default) picks the fused encoder where it applies. */
+#define BIC_OPT_MULTIPASS 1
+int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
 
 /* ---- a2: bitplane extraction (bitplane_tool.cpp:24-30) -----------------------------------
  * gray: rows x cols bytes with row pitch `pitch` (>= cols). Plane bi receives bit bi of every
@@ -82,6 +86,13 @@ int bic_med_residual(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t r
 int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
                       size_t wpr, int predict, int coder, uint64_t* out, size_t slot_words,
                       uint64_t* plane_bits);
+/* Both streams of the same planes in one pass (either output may be NULL, not both):
+ * Golomb into out_golomb/slot_golomb/bits_golomb, EG into out_eg/slot_eg/bits_eg. Same layout
+ * and semantics as two bic_encode_planes calls; rows of up to 16384 columns run as a single
+ * fused kernel (plus a fixup of the words adjacent rows share). */
+int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                       size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                       uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg);
 /* A slot size (64-bit words) that every plane of this geometry fits for EG (exact) and for
  * Golomb on any input this build has seen (2*rows*(cols+1) bits + 64 words); a larger input
  * still reports BIC_ENOSPC rather than writing out of bounds. */

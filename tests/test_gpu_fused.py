@@ -1,0 +1,115 @@
+"""The single-pass row encoder (bic_fused.hip) against the oracle and against the multi-pass
+chunk kernels, with inputs built to reach each of its paths: k = 0 copy mode, lanes whose
+codewords exceed the 128-bit register string, rows whose output exceeds the LDS window
+(global fallback), many short rows sharing one output word (fixup chains)."""
+import numpy as np
+import pytest
+
+import pybic
+from pybic import CODER_EG, CODER_GOLOMB, as_u64, stream_bytes
+
+pytestmark = pytest.mark.gpu
+
+ONES = np.uint64(0xFFFFFFFFFFFFFFFF)
+ALT = np.uint64(0xAAAAAAAAAAAAAAAA)
+
+
+def check(ctx, oracle, P, cols, pred, both=True):
+    P = np.asarray(P)
+    if P.ndim == 2:
+        P = P[None]
+    (og, bg), (oe, be) = ctx.encode_planes2(ctx.to_dev(P), cols, pred)
+    ctx.sync()
+    for k in range(P.shape[0]):
+        for coder, out, bits in ((0, og, bg), (1, oe, be)):
+            eb, est, _ = oracle.encode_plane(P[k], cols, pred, coder)
+            nb = int(as_u64(bits)[k])
+            assert nb == eb, (k, coder)
+            assert stream_bytes(out[k], nb) == est.tobytes(), (k, coder)
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (3, 64), (7, 65), (64, 100), (50, 1000), (40, 4096), (20, 8191),
+                                       (16, 16384), (130, 640)])
+@pytest.mark.parametrize("p", [0.5, 0.25, 0.03, 0.0, 1.0])
+def test_fused_random(ctx, oracle, rows, cols, p):
+    P = np.stack([oracle.gen_plane(1000 * rows + cols + k + int(p * 97), p, rows, cols) for k in range(2)])
+    for pred in (1, 0):
+        check(ctx, oracle, P, cols, pred)
+
+
+def test_fused_vs_multipass(ctx, oracle):
+    rows, cols = 200, 3000
+    P = np.stack([oracle.gen_plane(77 + k, p, rows, cols) for k, p in enumerate([0.5, 0.1, 0.01])])
+    d = ctx.to_dev(P)
+    res = {}
+    for mp in (False, True):
+        ctx.set_multipass(mp)
+        (og, bg), (oe, be) = ctx.encode_planes2(d, cols, True)
+        ctx.sync()
+        res[mp] = [(as_u64(bg), [stream_bytes(og[k], as_u64(bg)[k]) for k in range(3)]),
+                   (as_u64(be), [stream_bytes(oe[k], as_u64(be)[k]) for k in range(3)])]
+    ctx.set_multipass(False)
+    for c in range(2):
+        assert np.array_equal(res[False][c][0], res[True][c][0])
+        assert res[False][c][1] == res[True][c][1]
+
+
+def test_long_lane_and_global_fallback(ctx, oracle):
+    """zero rows drive k up (A grows, n grows by one EOL per row); then a dense word yields a
+    lane string > 128 bits, and a dense row yields a row longer than the LDS window."""
+    rows, cols = 160, 16384
+    wpr = cols // 64
+    P = np.zeros((rows, wpr), np.uint64)
+    P[100, 7] = ONES                      # one dense word: long lane, row fits LDS
+    P[120, :] = ONES                      # a whole dense row at large k: global fallback
+    P[121, :] = ALT                       # alternating pixels: dense residual for med
+    P[130:, :] = np.stack([oracle.gen_plane(5, 0.5, 30, cols)])[0]
+    for pred in (0, 1):
+        check(ctx, oracle, P, cols, pred)
+
+
+def test_many_short_rows_share_words(ctx, oracle):
+    """sparse rows of a few bits each: dozens of rows end inside one output word."""
+    rows, cols = 3000, 64
+    P = np.zeros((rows, 1), np.uint64)
+    P[::97, 0] = np.uint64(1)
+    for pred in (0, 1):
+        check(ctx, oracle, P, cols, pred)
+
+
+def test_copy_mode_runs_across_words(ctx, oracle):
+    """p = 0.5 keeps k in {0, 1}; long stretches of k = 0 take the copy path, including runs
+    that start in an earlier word."""
+    rows, cols = 64, 16384
+    P = oracle.gen_plane(99, 0.5, rows, cols)
+    P[10, 3:9] = 0                         # a run spanning several words inside a k = 0 stretch
+    check(ctx, oracle, P, cols, 0)
+    check(ctx, oracle, P, cols, 1)
+
+
+def test_single_stream_calls_match_dual(ctx, oracle):
+    rows, cols = 33, 2000
+    P = oracle.gen_plane(3, 0.2, rows, cols)[None]
+    d = ctx.to_dev(P)
+    og, bg = ctx.encode_planes(d, cols, True, CODER_GOLOMB)
+    oe, be = ctx.encode_planes(d, cols, True, CODER_EG)
+    (og2, bg2), (oe2, be2) = ctx.encode_planes2(d, cols, True)
+    ctx.sync()
+    assert int(as_u64(bg)[0]) == int(as_u64(bg2)[0]) and int(as_u64(be)[0]) == int(as_u64(be2)[0])
+    assert stream_bytes(og[0], as_u64(bg)[0]) == stream_bytes(og2[0], as_u64(bg2)[0])
+    assert stream_bytes(oe[0], as_u64(be)[0]) == stream_bytes(oe2[0], as_u64(be2)[0])
+
+
+def test_fused_overflow(ctx, oracle):
+    rows, cols = 64, 1024
+    P = oracle.gen_plane(8, 0.5, rows, cols)
+    t = ctx.torch
+    slot = 100
+    buf = t.full((2 * slot + 8,), 0x77, dtype=t.int64, device=ctx.dev)
+    ctx.encode_planes(ctx.to_dev(np.stack([P, P])), cols, True, CODER_GOLOMB, slot_words=slot,
+                      out=buf[: 2 * slot].view(2, slot))
+    with pytest.raises(pybic.BicError) as e:
+        ctx.sync()
+    assert e.value.code == pybic.BIC_ENOSPC
+    assert (as_u64(buf[2 * slot:]) == 0x77).all()
+    ctx.sync()
