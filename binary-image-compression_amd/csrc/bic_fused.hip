@@ -35,7 +35,7 @@ __device__ __forceinline__ uint64_t rec_load(uint64_t* p) {
 
 // Exclusive prefix of the record values [base, me): decoupled look-back by one wave, 64
 // predecessors per probe; stops at the nearest inclusive record. Bounded spin.
-__device__ uint64_t lookback(uint64_t* recs, uint64_t base, uint64_t me, uint32_t* flags) {
+__device__ __forceinline__ uint64_t lookback(uint64_t* recs, uint64_t base, uint64_t me, uint32_t* flags) {
   uint64_t excl = 0;
   int64_t pos = (int64_t)me - 1;
   const int lane = lane_id();
@@ -211,10 +211,11 @@ __device__ __forceinline__ void place_small(uint32_t* img, uint32_t off, uint32_
 // 64 image bits starting at bit a (a may be negative: leading zeros).
 __device__ __forceinline__ uint64_t raw64(const uint32_t* img, int64_t a) {
   if (a <= -64) return 0;
-  if (a < 0) return raw64(img, 0) >> (-a);
-  const uint32_t i = (uint32_t)(a >> 5), sh = (uint32_t)(a & 31);
+  const int64_t b = a < 0 ? 0 : a;
+  const uint32_t i = (uint32_t)(b >> 5), sh = (uint32_t)(b & 31);
   const uint64_t hi = ((uint64_t)img[i] << 32) | img[i + 1];
-  return sh ? (hi << sh) | (img[i + 2] >> (32 - sh)) : hi;
+  const uint64_t v = sh ? (hi << sh) | (img[i + 2] >> (32 - sh)) : hi;
+  return a < 0 ? v >> (-a) : v;
 }
 
 // Same, of the image with a '0' inserted at position ins (ins < 0: no insertion).
@@ -253,7 +254,7 @@ struct FusedArgs {
   uint32_t* counter;   // zeroed per launch
   uint64_t* ones_rec;  // zeroed per launch
   uint64_t* bits_rec;  // zeroed per launch
-  uint64_t *gboff, *glen, *gfrag;
+  uint64_t *gboff, *glen, *gfrag, *gslow;
   uint64_t *eboff, *elen, *efrag;
   uint64_t* out_g;
   uint64_t slot_g;
@@ -297,11 +298,30 @@ struct FragSink {
   __device__ __forceinline__ void bit(uint64_t off) { orw(off >> 6, BIC_MSB >> (off & 63)); }
 };
 
-template <int WPL, bool PREDICT>
-__device__ __noinline__ void golomb_row_global(const FusedArgs& a, const uint64_t (&r)[WPL], uint32_t row,
-                                               uint32_t nbase, uint64_t G, uint64_t L, uint64_t* frag) {
+// The residual word w of the row, read back from the EG image (~R, pad-masked): the image is
+// written for every row, so the Golomb steps need no registers for the row.
+__device__ __forceinline__ uint64_t img_resid(const uint32_t* eimg, const Geom& g, uint32_t w) {
+  if (w >= g.used) return 0;
+  const uint64_t v = ((uint64_t)eimg[2 * w] << 32) | eimg[2 * w + 1];
+  return ~v & (w == g.used - 1 ? g.trail : ~0ull);
+}
+
+// Rows whose Golomb output exceeds the LDS window (a long dense stretch at large k): the main
+// kernel records their offset and sample base; this kernel (one wave per row, idle waves exit
+// at once) recomputes the row and writes it straight to global memory -- its inner words are
+// zeroed and OR'd, the bits landing in its first/last (shared) word go to the fragment table.
+template <bool PREDICT>
+__global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
   const Geom& g = a.g;
   const int lane = lane_id();
+  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  if (id >= nrows) return;
+  const uint64_t slow = a.gslow[id];
+  if (!slow) return;
+  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+  const uint64_t G = a.gboff[id], L = a.glen[id];
+  uint64_t* frag = a.gfrag + 2 * id;
   const uint64_t wh = G >> 6, wt = (G + L - 1) >> 6;
   const bool hpart = !word_complete(wh, G, L);
   const bool tpart = !word_complete(wt, G, L);
@@ -309,21 +329,22 @@ __device__ __noinline__ void golomb_row_global(const FusedArgs& a, const uint64_
     if (!((i == wh && hpart) || (i == wt && tpart))) a.out_g[i] = 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   FragSink fs{reinterpret_cast<unsigned long long*>(a.out_g), wh, wt, hpart, tpart, 0, 0, 0, 0};
-  StepState st{nbase, -1};
+  StepState st{(uint32_t)(slow - 1), -1};
   const uint32_t arow = row * (g.cols + 1);
+  RowCtx rc = row_ctx(a.planes, g, plane, row, 0);
   uint64_t carry = G;
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) {
-    const uint32_t w = t * 64 + lane;
+  for (uint32_t w0 = 0; w0 < g.used; w0 += 64) {
+    const uint32_t w = w0 + lane;
+    const uint64_t x = resid_word<PREDICT>(rc, g, row, w);
     uint32_t n;
     int jp;
-    step_prefix(r[t], w, st, n, jp);
+    step_prefix(x, w, st, n, jp);
     const bool eol = w == g.used - 1;
-    const LaneEnc e = encode_word(r[t], w, n, jp, arow, eol, g.cols);
+    const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols);
     const uint32_t inc = wave_incl_sum_u32(e.len);
     const uint64_t off = carry + inc - e.len;
     carry += __shfl(inc, 63);
-    emit_word(fs, off, r[t], w, n, jp, arow, eol, g.cols);
+    emit_word(fs, off, x, w, n, jp, arow, eol, g.cols);
   }
   fs.flush();
   uint64_t h = fs.acc_h, tl = fs.acc_t;
@@ -338,68 +359,85 @@ __device__ __noinline__ void golomb_row_global(const FusedArgs& a, const uint64_
   }
 }
 
+// One workgroup = one TILE of 4 consecutive rows of one plane (one wave per row). Tiles are
+// claimed in order through an atomic counter with the planes interleaved (tile t -> plane
+// t % nplanes), so the 8 planes' look-back chains advance side by side; one look-back per tile
+// (by wave 0) serves its 4 rows, which combine their counts through LDS.
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
-__global__ __launch_bounds__(256) void k_encode_rows(FusedArgs a) {
+__global__ __launch_bounds__(256, 4) void k_encode_rows(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * (kGImg + kEImg)];
+  __shared__ uint64_t sh_cnt[4], sh_pre[2];
+  __shared__ uint32_t sh_tile;
   const Geom& g = a.g;
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* gimg = lds + wave * (kGImg + kEImg);
   uint32_t* eimg = gimg + kGImg;
-  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  uint32_t id32 = 0;
-  if (lane == 0) id32 = atomicAdd(a.counter, 1u);
-  const uint64_t id = (uint64_t)__shfl(id32, 0);
-  if (id >= nrows) return;
-  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
-  const uint64_t pbase = (uint64_t)plane * g.rows;
-  RowCtx rc = row_ctx(a.planes, g, plane, row, 0);
+  const uint32_t tpp = (g.rows + 3) / 4;  // tiles per plane
+  const uint64_t ntiles = (uint64_t)tpp * g.nplanes;
+  if (threadIdx.x == 0) sh_tile = atomicAdd(a.counter, 1u);
+  __syncthreads();
+  const uint64_t tile = sh_tile;
+  if (tile >= ntiles) return;  // uniform over the workgroup
+  const uint32_t plane = (uint32_t)(tile % g.nplanes), trow = (uint32_t)(tile / g.nplanes);
+  const uint64_t rbase = (uint64_t)plane * tpp;  // this plane's first tile record
+  const uint64_t rid = rbase + trow;             // this tile's record
+  const uint32_t row = trow * 4 + wave;
+  const bool valid = row < g.rows;
+  const uint64_t id = (uint64_t)plane * g.rows + row;  // per-row output records
 
-  uint64_t r[WPL];
+  // ---- residual row -> EG image (~R, pad-masked, EOL '1'); 1-count; first 1 ----------------
   uint32_t ones = 0;
   int fcol = INT_MAX;
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) {
-    const uint32_t w = t * 64 + lane;
-    r[t] = resid_word<PREDICT>(rc, g, row, w);
-    ones += (uint32_t)__popcll(r[t]);
-    if (r[t] && fcol == INT_MAX) fcol = (int)(w * 64 + __builtin_clzll(r[t]));
-  }
-  ones = wave_sum_u32(ones);
-
-  // ---- samples before this row: ones of earlier rows (+ one EOL sample per row) ----
-  uint64_t O;
-  if (row == 0) {
-    O = 0;
-    if (lane == 0) rec_store(&a.ones_rec[id], kInc | ones);
-  } else {
-    if (lane == 0) rec_store(&a.ones_rec[id], kAgg | ones);
-    O = lookback(a.ones_rec, pbase, id, a.flags);
-    if (lane == 0) rec_store(&a.ones_rec[id], kInc | (O + ones));
-  }
-
-  // ---- EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1 ----
-  if constexpr (DO_E) {
-    const bool f_here = O == 0 && ones > 0;
-    fcol = wave_min(fcol);
+  if (valid) {
+    RowCtx rc = row_ctx(a.planes, g, plane, row, 0);
 #pragma unroll
     for (int t = 0; t < WPL; ++t) {
       const uint32_t w = t * 64 + lane;
+      const uint64_t r = resid_word<PREDICT>(rc, g, row, w);
+      ones += (uint32_t)__popcll(r);
+      if (r && fcol == INT_MAX) fcol = (int)(w * 64 + __builtin_clzll(r));
       if (w < g.used) {
-        const uint64_t v = ~r[t] & (w == g.used - 1 ? g.trail : ~0ull);
+        const uint64_t v = ~r & (w == g.used - 1 ? g.trail : ~0ull);
         eimg[2 * w] = (uint32_t)(v >> 32);
         eimg[2 * w + 1] = (uint32_t)v;
       }
     }
     if (lane < kPad + 1) eimg[2 * g.used + lane] = 0;
+    ones = wave_sum_u32(ones);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) eimg[g.cols >> 5] |= 0x80000000u >> (g.cols & 31);  // EOL '1'
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0) sh_cnt[wave] = ones;
+  __syncthreads();
+
+  // ---- samples before this row: ones of earlier rows (+ one EOL sample per row) ----
+  if (wave == 0) {
+    const uint64_t tile_ones = sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
+    uint64_t O = 0;
+    if (trow == 0) {
+      if (lane == 0) rec_store(&a.ones_rec[rid], kInc | tile_ones);
+    } else {
+      if (lane == 0) rec_store(&a.ones_rec[rid], kAgg | tile_ones);
+      O = lookback(a.ones_rec, rbase, rid, a.flags);
+      if (lane == 0) rec_store(&a.ones_rec[rid], kInc | (O + tile_ones));
+    }
+    if (lane == 0) sh_pre[0] = O;
+  }
+  __syncthreads();
+  uint64_t O = sh_pre[0];
+  for (int q = 0; q < wave; ++q) O += sh_cnt[q];
+
+  // ---- EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1 ----
+  if (DO_E && valid) {
+    const bool f_here = O == 0 && ones > 0;
+    fcol = wave_min(fcol);
     const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
     const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
     const uint64_t cap = a.slot_e * 64;
     const uint64_t Ge = (uint64_t)plane * cap + Ge_rel;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     if (Ge_rel + Le <= cap) {
       write_row(eimg, Le, Ge, f_here ? (int64_t)fcol + 1 : -1, a.out_e, a.efrag + 2 * id);
       if (lane == 0) { a.eboff[id] = Ge; a.elen[id] = Le; }
@@ -413,67 +451,84 @@ __global__ __launch_bounds__(256) void k_encode_rows(FusedArgs a) {
 
   // ---- Golomb ------------------------------------------------------------------------------
   if constexpr (DO_G) {
-    StepState st{(uint32_t)(O + row), -1};
-    const uint32_t arow = row * (g.cols + 1);
-    constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
-    uint64_t loc = 0;
+    uint64_t L = 0;
     bool fits = true;
-#pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      const uint32_t w = t * 64 + lane;
-      uint32_t n;
-      int jp;
-      step_prefix(r[t], w, st, n, jp);
-      const bool eol = w == g.used - 1;
-      const LaneEnc e = encode_word(r[t], w, n, jp, arow, eol, g.cols);
-      const uint32_t inc = wave_incl_sum_u32(e.len);
-      const uint64_t off = loc + inc - e.len;
-      const uint64_t start = loc;
-      loc += __shfl(inc, 63);
-      if (fits && loc <= kCapBits) {
-        for (uint32_t i = (uint32_t)((start + 31) >> 5) + lane; i < (uint32_t)((loc + 31) >> 5); i += 64) gimg[i] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (!e.lng) {
-          place_small(gimg, (uint32_t)off, e.head, e.k0);
-          place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
+    if (valid) {
+      StepState st{(uint32_t)(O + row), -1};
+      const uint32_t arow = row * (g.cols + 1);
+      constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+      uint64_t loc = 0;
+      for (uint32_t w0 = 0; w0 < g.used; w0 += 64) {
+        const uint32_t w = w0 + lane;
+        const uint64_t x = img_resid(eimg, g, w);
+        uint32_t n;
+        int jp;
+        step_prefix(x, w, st, n, jp);
+        const bool eol = w == g.used - 1;
+        const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols);
+        const uint32_t inc = wave_incl_sum_u32(e.len);
+        const uint64_t off = loc + inc - e.len;
+        const uint64_t start = loc;
+        loc += __shfl(inc, 63);
+        if (fits && loc <= kCapBits) {
+          for (uint32_t i = (uint32_t)((start + 31) >> 5) + lane; i < (uint32_t)((loc + 31) >> 5); i += 64)
+            gimg[i] = 0;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          if (!e.lng) {
+            place_small(gimg, (uint32_t)off, e.head, e.k0);
+            place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
+          } else {
+            LdsSink ls{gimg, 0, 0};
+            emit_word(ls, (uint32_t)off, x, w, n, jp, arow, eol, g.cols);
+            ls.flush();
+          }
         } else {
-          LdsSink ls{gimg, 0, 0};
-          emit_word(ls, (uint32_t)off, r[t], w, n, jp, arow, eol, g.cols);
-          ls.flush();
+          fits = false;
         }
-      } else {
-        fits = false;
       }
+      L = loc;
     }
-    const uint64_t L = loc;
-    uint64_t Grel;
-    if (row == 0) {
-      Grel = 0;
-      if (lane == 0) rec_store(&a.bits_rec[id], kInc | L);
-    } else {
-      if (lane == 0) rec_store(&a.bits_rec[id], kAgg | L);
-      Grel = lookback(a.bits_rec, pbase, id, a.flags);
-      if (lane == 0) rec_store(&a.bits_rec[id], kInc | (Grel + L));
-    }
-    const uint64_t cap = a.slot_g * 64;
-    const uint64_t G = (uint64_t)plane * cap + Grel;
-    if (lane == 0 && row == g.rows - 1) a.bits_g[plane] = Grel + L;
-    if (Grel + L <= cap) {
-      if (fits) {
-        const uint32_t endw = (uint32_t)((L + 31) >> 5);
-        if (lane < kPad) gimg[endw + lane] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        write_row(gimg, L, G, -1, a.out_g, a.gfrag + 2 * id);
+    if (lane == 0) sh_cnt[wave] = L;
+    __syncthreads();
+    if (wave == 0) {
+      const uint64_t tile_bits = sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
+      uint64_t Gt = 0;
+      if (trow == 0) {
+        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | tile_bits);
       } else {
-        golomb_row_global<WPL, PREDICT>(a, r, row, (uint32_t)(O + row), G, L, a.gfrag + 2 * id);
+        if (lane == 0) rec_store(&a.bits_rec[rid], kAgg | tile_bits);
+        Gt = lookback(a.bits_rec, rbase, rid, a.flags);
+        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | (Gt + tile_bits));
       }
-      if (lane == 0) { a.gboff[id] = G; a.glen[id] = L; }
-    } else if (lane == 0) {
-      a.gboff[id] = G;
-      a.glen[id] = 0;
-      atomicOr(&a.flags[0], 1u);
+      if (lane == 0) sh_pre[1] = Gt;
+    }
+    __syncthreads();
+    if (valid) {
+      uint64_t Grel = sh_pre[1];
+      for (int q = 0; q < wave; ++q) Grel += sh_cnt[q];
+      const uint64_t cap = a.slot_g * 64;
+      const uint64_t G = (uint64_t)plane * cap + Grel;
+      if (lane == 0 && row == g.rows - 1) a.bits_g[plane] = Grel + L;
+      if (Grel + L <= cap) {
+        if (fits) {
+          const uint32_t endw = (uint32_t)((L + 31) >> 5);
+          if (lane < kPad) gimg[endw + lane] = 0;
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          write_row(gimg, L, G, -1, a.out_g, a.gfrag + 2 * id);
+        }
+        if (lane == 0) {
+          a.gboff[id] = G;
+          a.glen[id] = L;
+          a.gslow[id] = fits ? 0 : O + row + 1;  // k_rows_global writes the row
+        }
+      } else if (lane == 0) {
+        a.gboff[id] = G;
+        a.glen[id] = 0;
+        a.gslow[id] = 0;
+        atomicOr(&a.flags[0], 1u);
+      }
     }
   }
 }
@@ -503,7 +558,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 8 + 1024;
+  return 256 + n * 8 * 2 + n * 8 * 9 + 1024;
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -518,6 +573,7 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
   fs.gboff = q; q += n;
   fs.glen = q; q += n;
   fs.gfrag = q; q += 2 * n;
+  fs.gslow = q; q += n;
   fs.eboff = q; q += n;
   fs.elen = q; q += n;
   fs.efrag = q;
@@ -530,10 +586,10 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, int pred
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
                   uint64_t* bits_e, uint32_t* flags) {
   (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
-  FusedArgs a{g, planes, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.eboff,
-              fs.elen, fs.efrag, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
+  FusedArgs a{g, planes, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
+              fs.eboff, fs.elen, fs.efrag, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  const uint32_t grid = (uint32_t)((nrows + 3) / 4);
+  const uint32_t grid = (uint32_t)((g.rows + 3) / 4 * (uint64_t)g.nplanes);  // one workgroup per tile
   const bool dg = out_g != nullptr, de = out_e != nullptr;
 #define BIC_FUSED(W, P)                                                               \
   if (dg && de) k_encode_rows<W, P, true, true><<<grid, 256, 0, s>>>(a);              \
@@ -547,6 +603,10 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, int pred
   }
 #undef BIC_FUSED
   const uint32_t fgrid = (uint32_t)((nrows + 255) / 256);
+  if (dg) {
+    if (predict) k_rows_global<true><<<grid, 256, 0, s>>>(a);
+    else k_rows_global<false><<<grid, 256, 0, s>>>(a);
+  }
   if (dg) k_fixup<<<fgrid, 256, 0, s>>>(fs.gboff, fs.glen, fs.gfrag, out_g, g.rows, nrows);
   if (de) k_fixup<<<fgrid, 256, 0, s>>>(fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows);
 }

@@ -82,7 +82,7 @@ struct FusedScratch {
   uint32_t* counter;
   uint64_t *ones_rec, *bits_rec;
   size_t zero_bytes;  // counter + records, zeroed per launch
-  uint64_t *gboff, *glen, *gfrag, *eboff, *elen, *efrag;
+  uint64_t *gboff, *glen, *gfrag, *gslow, *eboff, *elen, *efrag;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
