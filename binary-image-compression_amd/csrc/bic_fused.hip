@@ -21,7 +21,7 @@
 
 namespace bic {
 
-constexpr int kGImg = 1536;   // u32 words of Golomb row image per wave (49152 bits)
+constexpr int kGImg = 736;    // u32 words of Golomb row image per wave (23552 bits; 8 workgroups per CU fit)
 constexpr int kEImg = 520;    // u32 words of EG row image per wave (cols <= 16384)
 constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads ahead)
 constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
@@ -33,22 +33,29 @@ __device__ __forceinline__ uint64_t rec_load(uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Exclusive prefix of the record values [base, me): decoupled look-back by one wave, 64
-// predecessors per probe; stops at the nearest inclusive record. Bounded spin.
+// Exclusive prefix of the record values [base, me): decoupled look-back by one wave. Each probe
+// reads 256 predecessors (4 per lane; position p = 4*lane + q counts back from me-1) and stops
+// at the nearest inclusive record, so the inclusive front advances 256 tiles per round trip.
+// Bounded spin.
 __device__ __forceinline__ uint64_t lookback(uint64_t* recs, uint64_t base, uint64_t me, uint32_t* flags) {
   uint64_t excl = 0;
   int64_t pos = (int64_t)me - 1;
   const int lane = lane_id();
   uint32_t spins = 0;
   while (pos >= (int64_t)base) {
-    const int64_t idx = pos - lane;
-    const uint64_t r = idx >= (int64_t)base ? rec_load(&recs[idx]) : kInc;
-    const uint64_t fl = r >> 62;
-    const uint64_t inc = __ballot(fl == 2);
-    const uint64_t bad = __ballot(fl == 0);
-    const int stop = inc ? __builtin_ctzll(inc) : 64;
-    const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
-    if (bad & need) {
+    uint64_t r[4];
+    int stop = 256;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t idx = pos - (4 * lane + q);
+      r[q] = idx >= (int64_t)base ? rec_load(&recs[idx]) : kInc;
+      const uint64_t inc = __ballot((r[q] >> 62) == 2);
+      if (inc) stop = min(stop, 4 * (int)__builtin_ctzll(inc) + q);
+    }
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bad |= (4 * lane + q <= stop) && (r[q] >> 62) == 0;
+    if (__ballot(bad)) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1u << 24)) {  // ~seconds: a record never arrived
         if (lane == 0) atomicOr(&flags[2], 1u);
@@ -56,9 +63,12 @@ __device__ __forceinline__ uint64_t lookback(uint64_t* recs, uint64_t base, uint
       }
       continue;
     }
-    excl += wave_sum_u64(lane <= stop ? (r & kValMask) : 0);
-    if (stop < 64) break;
-    pos -= 64;
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v += (4 * lane + q <= stop) ? (r[q] & kValMask) : 0;
+    excl += wave_sum_u64(v);
+    if (stop < 256) break;
+    pos -= 256;
   }
   return excl;
 }
@@ -364,7 +374,7 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
 // t % nplanes), so the 8 planes' look-back chains advance side by side; one look-back per tile
 // (by wave 0) serves its 4 rows, which combine their counts through LDS.
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
-__global__ __launch_bounds__(256, 4) void k_encode_rows(FusedArgs a) {
+__global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * (kGImg + kEImg)];
   __shared__ uint64_t sh_cnt[4], sh_pre[2];
   __shared__ uint32_t sh_tile;
