@@ -14,12 +14,19 @@
 #include <string>
 #include <vector>
 
+#ifdef BIC_STAMPS
+namespace bic {
+int read_stamps(uint64_t* host, size_t n);
+}
+#endif
+
 struct bic_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  uint64_t* lut = nullptr;        // device [3][256] byte table of the fused encoder
   uint32_t* flags = nullptr;      // device [4]: overflow, domain, look-back timeout, spare
   uint64_t* lentab = nullptr;     // device copy of the tile length table
   size_t lentab_cap = 0;          // entries
@@ -135,6 +142,16 @@ int bic_ctx_create(int device, bic_ctx** out) {
     return BIC_EDEVICE;
   }
   ctx->cur = ctx->own;
+  {
+    uint64_t host_lut[3 * 256];
+    bic::build_byte_lut(host_lut);
+    if (hipMalloc(&ctx->lut, sizeof(host_lut)) != hipSuccess ||
+        hipMemcpy(ctx->lut, host_lut, sizeof(host_lut), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipStreamDestroy(ctx->own);
+      delete ctx;
+      return BIC_ENOMEM;
+    }
+  }
   if (hipMalloc(&ctx->flags, 4 * sizeof(uint32_t)) != hipSuccess ||
       hipMemset(ctx->flags, 0, 4 * sizeof(uint32_t)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);
@@ -153,6 +170,7 @@ int bic_ctx_destroy(bic_ctx* ctx) {
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->flags) (void)hipFree(ctx->flags);
+  if (ctx->lut) (void)hipFree(ctx->lut);
   if (ctx->lentab) (void)hipFree(ctx->lentab);
   if (ctx->staging) (void)hipHostFree(ctx->staging);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
@@ -259,7 +277,7 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
     if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
     const bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
     timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg", [&] {
-      bic::launch_fused(ctx->cur, g, planes, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
+      bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags);
     });
     BIC_HIP(hipGetLastError());
@@ -433,5 +451,9 @@ int bic_prof_collect(bic_ctx* ctx, char* buf, size_t cap) {
   std::snprintf(buf, cap, "%s", outs.c_str());
   return outs.size() < cap ? BIC_OK : BIC_ENOSPC;
 }
+
+#ifdef BIC_STAMPS
+int bic_debug_stamps(uint64_t* host, size_t n) { return bic::read_stamps(host, n); }
+#endif
 
 }  // extern "C"

@@ -21,6 +21,19 @@
 
 namespace bic {
 
+#ifdef BIC_STAMPS  // diagnostic build only (make stamps): per-wave phase clocks, never in the product
+__device__ unsigned long long g_stamps[1 << 21];
+#define STAMP(slot)                                                                        \
+  do {                                                                                     \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
+    if (lane == 0 && (uint64_t)id * 8 + (slot) < (1u << 21)) g_stamps[(uint64_t)id * 8 + (slot)] = t_; \
+  } while (0)
+#else
+#define STAMP(slot) \
+  do {              \
+  } while (0)
+#endif
+
 constexpr int kGImg = 736;    // u32 words of Golomb row image per wave (23552 bits; 8 workgroups per CU fit)
 constexpr int kEImg = 520;    // u32 words of EG row image per wave (cols <= 16384)
 constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads ahead)
@@ -95,17 +108,29 @@ __device__ __forceinline__ void tail_put(LaneEnc& e, uint64_t cw, uint32_t nb) {
   }
 }
 
+// Byte table for words whose codewords all share one k in 1..3 (built on the host,
+// bic_capi.cpp build_byte_lut): entry [k-1][v] for a byte v != 0 holds the codewords that lie
+// wholly inside the byte (after its first 1) -- bits 0..31 the pattern (right-aligned), 32..37
+// its length -- plus the byte's leading zeros (40..43) and trailing zeros (44..47).
+__device__ __forceinline__ void tail_put_n(LaneEnc& e, uint64_t cw, uint32_t nb) {
+  if (nb) tail_put(e, cw, nb);
+}
+
 __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t n, int jp, uint32_t arow,
-                                               bool eol, uint32_t cols) {
+                                               bool eol, uint32_t cols, const uint64_t* __restrict__ lut) {
   LaneEnc e{0, 0, 0, 0, 0, 0, 0, false};
   if (!x && !eol) return e;
   if (x && n) {
-    // A never decreases, n only grows: if even the largest A of this word is <= its smallest n,
-    // every codeword here (and the EOL's, n + m >= n) has k = 0 and is the run's bits verbatim.
+    // A never decreases and n only grows along the word, so every codeword's k lies between
+    // k(n_last, A_first) and k(n_first, A_last); when the two agree, k is the same throughout.
     const uint32_t m = (uint32_t)__popcll(x);
     const uint32_t plast = w * 64 + 63 - (uint32_t)__builtin_ctzll(x);
-    const uint32_t aup = arow + plast - (n + m - 1);
-    if (aup <= n) {
+    const uint32_t aup = arow + plast - (n + m - 1);  // >= A of the last codeword (and = A of the EOL's)
+    const uint32_t afirst = arow + (uint32_t)(jp + 1) - n;
+    const uint32_t khi = golomb_k(n, aup);
+    const uint32_t klo = golomb_k(n + m - 1 + (eol ? 1u : 0u), afirst);
+    if (khi == klo && khi == 0) {
+      // k = 0: a codeword is its run's zeros and the 1 -- the word's bits verbatim
       e.z = w * 64 - (uint32_t)(jp + 1);
       e.t0 = x;
       if (!eol) {
@@ -116,6 +141,47 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
         e.tlen = p + 1;
       }
       e.len = e.z + e.tlen;
+      return e;
+    }
+    if (khi == klo && khi <= 3) {
+      const uint32_t k = khi, kmask = (1u << k) - 1u;
+      const uint64_t* L = lut + (k - 1) * 256;
+      uint32_t c = w * 64 - (uint32_t)(jp + 1);  // zeros of the open run
+      bool first = true;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint32_t v = (uint32_t)(x >> (56 - 8 * b)) & 0xffu;
+        if (v) {
+          const uint64_t en = L[v];
+          const uint32_t t = (uint32_t)(en >> 40) & 15u, tz = (uint32_t)(en >> 44) & 15u;
+          const uint32_t lr = (uint32_t)(en >> 32) & 63u, R = (uint32_t)en;
+          const uint32_t sr = c + t, q = sr >> k, bin = sr & kmask;
+          if (first) {
+            e.head = bin;
+            e.k0 = k;
+            e.z = q;
+            tail_put(e, (1ull << lr) | R, 1 + lr);
+            first = false;
+          } else {
+            const uint32_t nb = k + q + 1;  // sr <= 63 here
+            if (nb + lr <= 64) {
+              tail_put(e, ((((uint64_t)bin << (q + 1)) | 1ull) << lr) | R, nb + lr);
+            } else {
+              tail_put(e, ((uint64_t)bin << (q + 1)) | 1ull, nb);
+              tail_put_n(e, R, lr);
+            }
+          }
+          e.len += k + q + 1 + lr;
+          c = tz;
+        } else {
+          c += 8;
+        }
+      }
+      if (eol) {  // the row's trailing zeros (pad columns excluded)
+        const uint32_t sr = c - (w * 64 + 64 - cols), q = sr >> k;
+        tail_put(e, ((uint64_t)(sr & kmask) << (q + 1)) | 1ull, k + q + 1);
+        e.len += k + q + 1;
+      }
       return e;
     }
   }
@@ -261,6 +327,7 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
 struct FusedArgs {
   Geom g;
   const uint64_t* planes;
+  const uint64_t* lut;  // [3][256] byte table (see encode_word)
   uint32_t* counter;   // zeroed per launch
   uint64_t* ones_rec;  // zeroed per launch
   uint64_t* bits_rec;  // zeroed per launch
@@ -350,7 +417,7 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
     int jp;
     step_prefix(x, w, st, n, jp);
     const bool eol = w == g.used - 1;
-    const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols);
+    const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols, a.lut);
     const uint32_t inc = wave_incl_sum_u32(e.len);
     const uint64_t off = carry + inc - e.len;
     carry += __shfl(inc, 63);
@@ -394,6 +461,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
   const uint32_t row = trow * 4 + wave;
   const bool valid = row < g.rows;
   const uint64_t id = (uint64_t)plane * g.rows + row;  // per-row output records
+  STAMP(0);
 
   // ---- residual row -> EG image (~R, pad-masked, EOL '1'); 1-count; first 1 ----------------
   uint32_t ones = 0;
@@ -418,6 +486,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) eimg[g.cols >> 5] |= 0x80000000u >> (g.cols & 31);  // EOL '1'
   }
+  STAMP(1);
   if (lane == 0) sh_cnt[wave] = ones;
   __syncthreads();
 
@@ -435,6 +504,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
     if (lane == 0) sh_pre[0] = O;
   }
   __syncthreads();
+  STAMP(2);
   uint64_t O = sh_pre[0];
   for (int q = 0; q < wave; ++q) O += sh_cnt[q];
 
@@ -459,6 +529,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
     if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
   }
 
+  STAMP(3);
   // ---- Golomb ------------------------------------------------------------------------------
   if constexpr (DO_G) {
     uint64_t L = 0;
@@ -475,7 +546,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
         int jp;
         step_prefix(x, w, st, n, jp);
         const bool eol = w == g.used - 1;
-        const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols);
+        const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols, a.lut);
         const uint32_t inc = wave_incl_sum_u32(e.len);
         const uint64_t off = loc + inc - e.len;
         const uint64_t start = loc;
@@ -499,6 +570,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
       }
       L = loc;
     }
+    STAMP(4);
     if (lane == 0) sh_cnt[wave] = L;
     __syncthreads();
     if (wave == 0) {
@@ -514,6 +586,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
       if (lane == 0) sh_pre[1] = Gt;
     }
     __syncthreads();
+    STAMP(5);
     if (valid) {
       uint64_t Grel = sh_pre[1];
       for (int q = 0; q < wave; ++q) Grel += sh_cnt[q];
@@ -540,6 +613,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
         atomicOr(&a.flags[0], 1u);
       }
     }
+    STAMP(6);
   }
 }
 
@@ -592,11 +666,18 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
 
 bool fused_supported(const Geom& g) { return g.used <= 256; }
 
-void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, const FusedScratch& fs,
+#ifdef BIC_STAMPS
+int read_stamps(uint64_t* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+}
+#endif
+
+void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
+                  const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
                   uint64_t* bits_e, uint32_t* flags) {
   (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
-  FusedArgs a{g, planes, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
+  FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
               fs.eboff, fs.elen, fs.efrag, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t grid = (uint32_t)((g.rows + 3) / 4 * (uint64_t)g.nplanes);  // one workgroup per tile

@@ -777,6 +777,33 @@ void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_
 }
 
 // ------------------------------------------------------------------------------------
+// Host: the fused encoder's byte table (bic_fused.hip encode_word). For k in 1..3 and byte v
+// (MSB = first pixel), the codewords of the runs that start AND end inside v -- between its
+// first and last 1 -- as one MSB-first pattern, with the byte's leading and trailing zeros.
+void build_byte_lut(uint64_t* lut) {
+  for (unsigned k = 1; k <= 3; ++k)
+    for (unsigned v = 0; v < 256; ++v) {
+      uint64_t& en = lut[(k - 1) * 256 + v];
+      if (!v) {
+        en = 8ull << 40;
+        continue;
+      }
+      int pos[8], m = 0;
+      for (int b = 0; b < 8; ++b)
+        if ((v >> (7 - b)) & 1u) pos[m++] = b;
+      uint64_t R = 0;
+      unsigned lr = 0;
+      for (int i = 1; i < m; ++i) {
+        const unsigned s = (unsigned)(pos[i] - pos[i - 1] - 1);
+        R = (R << k) | (s & ((1u << k) - 1u));  // binary part
+        R <<= (s >> k);                          // unary zeros
+        R = (R << 1) | 1u;                       // terminator
+        lr += k + (s >> k) + 1;
+      }
+      en = R | ((uint64_t)lr << 32) | ((uint64_t)pos[0] << 40) | ((uint64_t)(7 - pos[m - 1]) << 44);
+    }
+}
+
 Geom make_geom(size_t rows, size_t cols, size_t wpr, int nplanes) {
   Geom g{};
   g.rows = (uint32_t)rows;

@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "lib", "libbic.so")
+LIB_PATH = os.environ.get("BIC_LIB_PATH") or os.path.join(PKG, "lib", "libbic.so")
 
 BIC_OK, BIC_EINVAL, BIC_ENOMEM, BIC_EDEVICE, BIC_ENOSPC, BIC_ENODEV = range(6)
 CODER_GOLOMB, CODER_EG = 0, 1
