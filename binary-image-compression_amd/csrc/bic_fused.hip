@@ -34,6 +34,7 @@ __device__ unsigned long long g_stamps[1 << 21];
   } while (0)
 #endif
 
+constexpr int kTileRows = 8;  // rows (= waves) per workgroup tile
 constexpr int kGImg = 736;    // u32 words of Golomb row image per wave (23552 bits; 8 workgroups per CU fit)
 constexpr int kEImg = 520;    // u32 words of EG row image per wave (cols <= 16384)
 constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads ahead)
@@ -441,15 +442,15 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
 // t % nplanes), so the 8 planes' look-back chains advance side by side; one look-back per tile
 // (by wave 0) serves its 4 rows, which combine their counts through LDS.
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
-__global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * (kGImg + kEImg)];
-  __shared__ uint64_t sh_cnt[4], sh_pre[2];
+__global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * (kGImg + kEImg)];
+  __shared__ uint64_t sh_cnt[kTileRows], sh_pre[2];
   __shared__ uint32_t sh_tile;
   const Geom& g = a.g;
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* gimg = lds + wave * (kGImg + kEImg);
   uint32_t* eimg = gimg + kGImg;
-  const uint32_t tpp = (g.rows + 3) / 4;  // tiles per plane
+  const uint32_t tpp = (g.rows + kTileRows - 1) / kTileRows;  // tiles per plane
   const uint64_t ntiles = (uint64_t)tpp * g.nplanes;
   if (threadIdx.x == 0) sh_tile = atomicAdd(a.counter, 1u);
   __syncthreads();
@@ -458,7 +459,7 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
   const uint32_t plane = (uint32_t)(tile % g.nplanes), trow = (uint32_t)(tile / g.nplanes);
   const uint64_t rbase = (uint64_t)plane * tpp;  // this plane's first tile record
   const uint64_t rid = rbase + trow;             // this tile's record
-  const uint32_t row = trow * 4 + wave;
+  const uint32_t row = trow * kTileRows + wave;
   const bool valid = row < g.rows;
   const uint64_t id = (uint64_t)plane * g.rows + row;  // per-row output records
   STAMP(0);
@@ -492,7 +493,8 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
 
   // ---- samples before this row: ones of earlier rows (+ one EOL sample per row) ----
   if (wave == 0) {
-    const uint64_t tile_ones = sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
+    uint64_t tile_ones = 0;
+    for (int q = 0; q < kTileRows; ++q) tile_ones += sh_cnt[q];
     uint64_t O = 0;
     if (trow == 0) {
       if (lane == 0) rec_store(&a.ones_rec[rid], kInc | tile_ones);
@@ -574,7 +576,8 @@ __global__ __launch_bounds__(256, 8) void k_encode_rows(FusedArgs a) {
     if (lane == 0) sh_cnt[wave] = L;
     __syncthreads();
     if (wave == 0) {
-      const uint64_t tile_bits = sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
+      uint64_t tile_bits = 0;
+      for (int q = 0; q < kTileRows; ++q) tile_bits += sh_cnt[q];
       uint64_t Gt = 0;
       if (trow == 0) {
         if (lane == 0) rec_store(&a.bits_rec[rid], kInc | tile_bits);
@@ -680,12 +683,12 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
               fs.eboff, fs.elen, fs.efrag, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  const uint32_t grid = (uint32_t)((g.rows + 3) / 4 * (uint64_t)g.nplanes);  // one workgroup per tile
+  const uint32_t grid = (uint32_t)((g.rows + kTileRows - 1) / kTileRows * (uint64_t)g.nplanes);  // one per tile
   const bool dg = out_g != nullptr, de = out_e != nullptr;
 #define BIC_FUSED(W, P)                                                               \
-  if (dg && de) k_encode_rows<W, P, true, true><<<grid, 256, 0, s>>>(a);              \
-  else if (dg) k_encode_rows<W, P, true, false><<<grid, 256, 0, s>>>(a);              \
-  else k_encode_rows<W, P, false, true><<<grid, 256, 0, s>>>(a);
+  if (dg && de) k_encode_rows<W, P, true, true><<<grid, 64 * kTileRows, 0, s>>>(a);   \
+  else if (dg) k_encode_rows<W, P, true, false><<<grid, 64 * kTileRows, 0, s>>>(a);   \
+  else k_encode_rows<W, P, false, true><<<grid, 64 * kTileRows, 0, s>>>(a);
   const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
   if (predict) {
     if (wpl == 1) { BIC_FUSED(1, true) } else if (wpl == 2) { BIC_FUSED(2, true) } else { BIC_FUSED(4, true) }
@@ -695,8 +698,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
 #undef BIC_FUSED
   const uint32_t fgrid = (uint32_t)((nrows + 255) / 256);
   if (dg) {
-    if (predict) k_rows_global<true><<<grid, 256, 0, s>>>(a);
-    else k_rows_global<false><<<grid, 256, 0, s>>>(a);
+    const uint32_t rgrid = (uint32_t)((nrows + 3) / 4);
+    if (predict) k_rows_global<true><<<rgrid, 256, 0, s>>>(a);
+    else k_rows_global<false><<<rgrid, 256, 0, s>>>(a);
   }
   if (dg) k_fixup<<<fgrid, 256, 0, s>>>(fs.gboff, fs.glen, fs.gfrag, out_g, g.rows, nrows);
   if (de) k_fixup<<<fgrid, 256, 0, s>>>(fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows);
