@@ -210,6 +210,51 @@ int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols) {
   return ensure_scratch(ctx, bic::chunk_scratch_bytes(g));
 }
 
+int bic_malloc(bic_ctx* ctx, size_t bytes, void** dptr) {
+  if (!dptr) return BIC_EINVAL;
+  *dptr = nullptr;
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (bytes == 0) return BIC_OK;
+  return hipMalloc(dptr, bytes) == hipSuccess ? BIC_OK : BIC_ENOMEM;
+}
+
+int bic_free(bic_ctx* ctx, void* dptr) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (dptr) BIC_HIP(hipFree(dptr));
+  return BIC_OK;
+}
+
+int bic_memcpy_h2d(bic_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (bytes == 0) return BIC_OK;
+  if (!dst || !src) return BIC_EINVAL;
+  BIC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->cur));
+  BIC_HIP(hipStreamSynchronize(ctx->cur));
+  return BIC_OK;
+}
+
+int bic_memcpy_d2h(bic_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (bytes == 0) return BIC_OK;
+  if (!dst || !src) return BIC_EINVAL;
+  BIC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->cur));
+  BIC_HIP(hipStreamSynchronize(ctx->cur));
+  return BIC_OK;
+}
+
+int bic_memset(bic_ctx* ctx, void* dst, int value, size_t bytes) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (bytes == 0) return BIC_OK;
+  if (!dst) return BIC_EINVAL;
+  BIC_HIP(hipMemsetAsync(dst, value, bytes, ctx->cur));
+  return BIC_OK;
+}
+
 int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
   if (!ctx) return BIC_EINVAL;
   if (option == BIC_OPT_MULTIPASS) {

@@ -25,6 +25,7 @@ EXPORTS = [
     "bic_strerror", "bic_device_count", "bic_reserve", "bic_bitplanes_u8", "bic_med_residual",
     "bic_encode_planes", "bic_encode_planes2", "bic_ctx_set_option", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
+    "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset",
 ]
 
 

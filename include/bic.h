@@ -57,6 +57,14 @@ void* bic_ctx_own_stream(bic_ctx* ctx);
 int bic_sync(bic_ctx* ctx);
 const char* bic_strerror(int code);
 int bic_device_count(int* n);
+/* Device memory for callers without a runtime of their own (the C++ reference-API layer,
+ * ctypes/cgo bindings). bic_malloc/bic_free act on the ctx's device; the copies are ordered
+ * on the ctx stream and return after the copy has completed (host buffers are pageable). */
+int bic_malloc(bic_ctx* ctx, size_t bytes, void** dptr);
+int bic_free(bic_ctx* ctx, void* dptr);
+int bic_memcpy_h2d(bic_ctx* ctx, void* dst, const void* src, size_t bytes);
+int bic_memcpy_d2h(bic_ctx* ctx, void* dst, const void* src, size_t bytes);
+int bic_memset(bic_ctx* ctx, void* dst, int value, size_t bytes);
 /* Pre-grow the ctx scratch so later calls do not allocate (needed before stream capture). */
 int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
 /* Options: BIC_OPT_MULTIPASS = 1 forces the multi-pass chunk kernels for every geometry

@@ -1,0 +1,139 @@
+"""Drop-in check of the C++ reference API (include/*.h + libbicpp.so), SURVEY.md §8 b.
+
+The reference's own GSL-free driver programs (binmat_test, pbm_test, patch_test, bitplane_tool,
+plane2pgm_tool) are compiled twice by `make -C oracle drivers`: against the reference sources
+under /root/reference/src, and -- unchanged -- against this build's headers and library. Both
+binaries run on the same inputs in separate directories; stdout, exit status and every file they
+write must be identical. These programs exercise the host half of the API (binary_matrix, PBM/PGM
+I/O, tiles, vectorisation); none of them calls into the GPU.
+
+Needs /root/reference (this container only); skipped where it is absent (the GPU box).
+"""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from pnm_io import write_pbm, write_pgm
+
+REF_SRC = "/root/reference/src"
+DRV = os.path.join(ROOT, "oracle", "_ref")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+pytestmark = pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources absent")
+
+
+@pytest.fixture(scope="module")
+def drivers():
+    subprocess.run(["make", "-C", os.path.join(ROOT, "binary-image-compression_amd")], check=True,
+                   stdout=subprocess.DEVNULL)
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "drivers"], check=True, stdout=subprocess.DEVNULL)
+    return DRV
+
+
+def rand_plane(seed, rows, cols, p=0.4):
+    rng = np.random.default_rng(seed)
+    bits = rng.random((rows, cols)) < p
+    wpr = (cols + 63) // 64
+    pad = np.zeros((rows, wpr * 64), bool)
+    pad[:, :cols] = bits
+    return np.packbits(pad, axis=1).view(">u8").astype(np.uint64).reshape(rows, wpr)
+
+
+def pbm_inputs(tmp):
+    out = {"camera": os.path.join(GOLDEN, "camera_70x37.pbm")}
+    for seed, (r, c) in enumerate([(64, 64), (100, 130), (45, 200), (41, 77)]):
+        out[f"rand{r}x{c}"] = write_pbm(os.path.join(tmp, f"r{r}x{c}.pbm"), rand_plane(seed + 1, r, c), c)
+    return out
+
+
+def run_both(drivers, tmp, name, args, setup):
+    """run driver `name` from both builds in fresh directories prepared by setup(dir)"""
+    res = {}
+    for side in ("drv_ref", "drv_bic"):
+        d = os.path.join(tmp, side)
+        shutil.rmtree(d, ignore_errors=True)
+        os.makedirs(os.path.join(d, "data"))
+        setup(d)
+        before = set(os.listdir(d))
+        p = subprocess.run([os.path.join(drivers, side, name)] + args, cwd=d, capture_output=True, timeout=120)
+        files = {}
+        for root, _, names in os.walk(d):
+            for n in names:
+                path = os.path.join(root, n)
+                rel = os.path.relpath(path, d)
+                if rel not in before and not rel.startswith("data"):
+                    with open(path, "rb") as f:
+                        files[rel] = f.read()
+        res[side] = (p.returncode, p.stdout, files)
+    return res
+
+
+def assert_same(res, name):
+    (rc_r, out_r, f_r), (rc_b, out_b, f_b) = res["drv_ref"], res["drv_bic"]
+    assert rc_r == rc_b, (name, rc_r, rc_b)
+    if out_r != out_b:
+        a, b = out_r.decode(errors="replace").splitlines(), out_b.decode(errors="replace").splitlines()
+        first = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), min(len(a), len(b)))
+        pytest.fail(f"{name}: stdout differs at line {first}:\nref: {a[first:first + 2]}\nbic: {b[first:first + 2]}")
+    assert sorted(f_r) == sorted(f_b), name
+    for k in f_r:
+        assert f_r[k] == f_b[k], (name, k)
+
+
+@pytest.mark.parametrize("driver", ["binmat_test", "pbm_test"])
+def test_binmat_and_pbm(drivers, tmp_path, driver):
+    """binmat_test: element access, weights, parities, products, row/column/tile views, PBM
+    round trip and (at its end) the reference's own get_row(rows) assertion; pbm_test: P4 copy."""
+    ins = pbm_inputs(str(tmp_path))
+    for key, src in ins.items():
+        res = run_both(drivers, str(tmp_path), driver, [],
+                       lambda d, s=src: shutil.copy(s, os.path.join(d, "data", "camera.pbm")))
+        assert_same(res, f"{driver}/{key}")
+
+
+@pytest.mark.parametrize("W", [3, 5, 8, 16, 32])
+def test_patch_tiles(drivers, tmp_path, W):
+    """patch_test: W x W tiles via get_submatrix (incl. tiles running into the next row when W does
+    not divide the width), vectorise / unvectorise, set_submatrix, dist, PBM writes."""
+    ins = pbm_inputs(str(tmp_path))
+    for key, src in ins.items():
+        res = run_both(drivers, str(tmp_path), "patch_test", ["data/in.pbm", str(W)],
+                       lambda d, s=src: shutil.copy(s, os.path.join(d, "data", "in.pbm")))
+        assert_same(res, f"patch_test/{key}/W{W}")
+
+
+def gray_inputs(tmp):
+    rng = np.random.default_rng(11)
+    out = {"gray48x40": os.path.join(GOLDEN, "gray_48x40.pgm"),
+           "gray16_20x12": os.path.join(GOLDEN, "gray16_20x12.pgm")}
+    g = rng.integers(0, 200, (53, 77), dtype=np.uint16)
+    out["rand53x77_m199"] = write_pgm(os.path.join(tmp, "g1.pgm"), g, 199, comment="# a comment line")
+    g2 = rng.integers(0, 1024, (9, 130), dtype=np.uint16)
+    out["rand9x130_m1023"] = write_pgm(os.path.join(tmp, "g2.pgm"), g2, 1023)
+    p2 = os.path.join(tmp, "g3.pgm")
+    g3 = rng.integers(0, 16, (7, 11))
+    with open(p2, "w") as f:
+        f.write("P2\n# ascii\n11 7\n15\n" + "\n".join(" ".join(str(v) for v in row) for row in g3) + "\n")
+    out["ascii7x11"] = p2
+    return out
+
+
+def test_bitplane_and_plane2pgm(drivers, tmp_path):
+    """bitplane_tool: PGM (P5 8/16-bit, P2) -> plane_XX.pbm; plane2pgm_tool: planes -> PGM."""
+    for key, src in gray_inputs(str(tmp_path)).items():
+        res = run_both(drivers, str(tmp_path), "bitplane_tool", ["data/in.pgm"],
+                       lambda d, s=src: shutil.copy(s, os.path.join(d, "data", "in.pgm")))
+        assert_same(res, f"bitplane_tool/{key}")
+        planes = res["drv_ref"][2]
+        assert planes, key
+
+        def setup(d, planes=planes):
+            for n, b in planes.items():
+                with open(os.path.join(d, "data", n), "wb") as f:
+                    f.write(b)
+        res2 = run_both(drivers, str(tmp_path), "plane2pgm_tool", ["data/plane_%02d.pbm", "rec.pgm"], setup)
+        assert_same(res2, f"plane2pgm_tool/{key}")
