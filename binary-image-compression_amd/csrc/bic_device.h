@@ -161,6 +161,42 @@ __device__ __forceinline__ uint64_t resid_word(RowCtx& rc, const Geom& g, uint32
   return valid ? r : 0;
 }
 
+// The residual words of one row for lane words w = t*64 + lane (t < WPL), zero past the row.
+// Every load is issued before any is used (addresses clamped into the row), so the wave pays
+// one memory latency, not WPL of them. With D = P ^ U the med residual is D ^ (D >> 1 | Dl << 63)
+// (shifts distribute over XOR), one cross-lane shuffle per word.
+template <int WPL, bool PREDICT>
+__device__ __forceinline__ void resid_row(const uint64_t* planes, const Geom& g, uint32_t plane, uint32_t row,
+                                          uint64_t (&r)[WPL]) {
+  const int lane = lane_id();
+  const uint64_t* cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
+  const uint64_t* up = row ? cur - g.wpr : cur;
+  uint64_t p[WPL], u[WPL];
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = t * 64 + lane;
+    const uint32_t wc = w < g.used ? w : g.used - 1;
+    p[t] = cur[wc];
+    if constexpr (PREDICT) u[t] = up[wc];
+  }
+  uint64_t carry = 0;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = t * 64 + lane;
+    uint64_t d = p[t];
+    if constexpr (PREDICT) {
+      if (row) d ^= u[t];
+      uint64_t dl = shfl_up_u64(d, 1);
+      if (lane == 0) dl = carry;
+      carry = shfl_u64(d, 63);
+      d ^= (d >> 1) | (dl << 63);
+      if (row == 0 && w == 0) d &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+    }
+    if (w == g.used - 1) d &= g.trail;
+    r[t] = w < g.used ? d : 0;
+  }
+}
+
 struct ChunkId {
   uint32_t plane, row, c;
   uint64_t id;

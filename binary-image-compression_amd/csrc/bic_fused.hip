@@ -23,6 +23,9 @@ namespace bic {
 
 #ifdef BIC_STAMPS  // diagnostic build only (make stamps): per-wave phase clocks, never in the product
 __device__ unsigned long long g_stamps[1 << 21];
+// BIC_KNOWN=1 (diagnostic): replay the tile prefixes recorded by the previous normal launch
+// instead of looking them back, to measure what the look-back waits cost
+__device__ unsigned long long g_known[2][1 << 17];
 #define STAMP(slot)                                                                        \
   do {                                                                                     \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
@@ -35,7 +38,8 @@ __device__ unsigned long long g_stamps[1 << 21];
 #endif
 
 constexpr int kTileRows = 8;  // rows (= waves) per workgroup tile
-constexpr int kGImg = 736;    // u32 words of Golomb row image per wave (23552 bits; 8 workgroups per CU fit)
+constexpr int kGImg = 684;    // u32 words of Golomb row image per wave (21760 bits; with the EG image and
+                              // the k = 1, 2 byte tables 4 workgroups (32 waves) fit one CU's LDS)
 constexpr int kEImg = 520;    // u32 words of EG row image per wave (cols <= 16384)
 constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads ahead)
 constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
@@ -60,9 +64,13 @@ __device__ __forceinline__ uint64_t lookback(uint64_t* recs, uint64_t base, uint
     uint64_t r[4];
     int stop = 256;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 4; ++q) {  // all four loads in flight before any is used
       const int64_t idx = pos - (4 * lane + q);
-      r[q] = idx >= (int64_t)base ? rec_load(&recs[idx]) : kInc;
+      r[q] = rec_load(&recs[idx >= (int64_t)base ? idx : (int64_t)base]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (pos - (4 * lane + q) < (int64_t)base) r[q] = kInc;
       const uint64_t inc = __ballot((r[q] >> 62) == 2);
       if (inc) stop = min(stop, 4 * (int)__builtin_ctzll(inc) + q);
     }
@@ -94,6 +102,9 @@ struct LaneEnc {
   uint32_t tlen;
   uint32_t len;          // total bits
   bool lng;              // rest longer than 128 bits: placed by re-iteration
+#ifdef BIC_STAMPS
+  uint32_t path;         // diagnostic: 1 copy mode, 2 byte table, 3 per-codeword loop
+#endif
 };
 
 __device__ __forceinline__ void tail_put(LaneEnc& e, uint64_t cw, uint32_t nb) {  // nb 1..64
@@ -109,17 +120,22 @@ __device__ __forceinline__ void tail_put(LaneEnc& e, uint64_t cw, uint32_t nb) {
   }
 }
 
-// Byte table for words whose codewords all share one k in 1..3 (built on the host,
-// bic_capi.cpp build_byte_lut): entry [k-1][v] for a byte v != 0 holds the codewords that lie
-// wholly inside the byte (after its first 1) -- bits 0..31 the pattern (right-aligned), 32..37
-// its length -- plus the byte's leading zeros (40..43) and trailing zeros (44..47).
+// Byte tables for words whose codewords all share one k in 1..3 (built on the host,
+// bic_kernels.hip build_byte_lut): for a byte v != 0, the codewords that lie wholly inside the
+// byte (after its first 1) as one right-aligned pattern R of lr bits, plus the byte's leading (t)
+// and trailing (tz) zeros. k = 1, 2: packed u32 R | lr << 21 | t << 26 | tz << 29, staged in LDS
+// by the encoder; k = 3: u64 R | lr << 32 | t << 40 | tz << 44 from global memory.
+struct ByteTables {
+  const uint32_t* t12;  // [2][256]
+  const uint64_t* t3;   // [256]
+};
 __device__ __forceinline__ void tail_put_n(LaneEnc& e, uint64_t cw, uint32_t nb) {
   if (nb) tail_put(e, cw, nb);
 }
 
 __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t n, int jp, uint32_t arow,
-                                               bool eol, uint32_t cols, const uint64_t* __restrict__ lut) {
-  LaneEnc e{0, 0, 0, 0, 0, 0, 0, false};
+                                               bool eol, uint32_t cols, ByteTables lut) {
+  LaneEnc e{};
   if (!x && !eol) return e;
   if (x && n) {
     // A never decreases and n only grows along the word, so every codeword's k lies between
@@ -142,20 +158,37 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
         e.tlen = p + 1;
       }
       e.len = e.z + e.tlen;
+#ifdef BIC_STAMPS
+      e.path = 1;
+#endif
       return e;
     }
     if (khi == klo && khi <= 3) {
+#ifdef BIC_STAMPS
+      e.path = 2;
+#endif
       const uint32_t k = khi, kmask = (1u << k) - 1u;
-      const uint64_t* L = lut + (k - 1) * 256;
       uint32_t c = w * 64 - (uint32_t)(jp + 1);  // zeros of the open run
       bool first = true;
+      const uint32_t* T = lut.t12 + (k - 1) * 256;
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         const uint32_t v = (uint32_t)(x >> (56 - 8 * b)) & 0xffu;
         if (v) {
-          const uint64_t en = L[v];
-          const uint32_t t = (uint32_t)(en >> 40) & 15u, tz = (uint32_t)(en >> 44) & 15u;
-          const uint32_t lr = (uint32_t)(en >> 32) & 63u, R = (uint32_t)en;
+          uint32_t R, lr, t, tz;
+          if (k <= 2) {
+            const uint32_t en = T[v];
+            R = en & 0x1fffffu;
+            lr = (en >> 21) & 31u;
+            t = (en >> 26) & 7u;
+            tz = en >> 29;
+          } else {
+            const uint64_t en = lut.t3[v];
+            R = (uint32_t)en;
+            lr = (uint32_t)(en >> 32) & 63u;
+            t = (uint32_t)(en >> 40) & 15u;
+            tz = (uint32_t)(en >> 44) & 15u;
+          }
           const uint32_t sr = c + t, q = sr >> k, bin = sr & kmask;
           if (first) {
             e.head = bin;
@@ -187,6 +220,9 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
     }
   }
   bool first = true;
+#ifdef BIC_STAMPS
+  e.path = 3;
+#endif
   for (;;) {
     int j;
     uint32_t s;
@@ -328,7 +364,7 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
 struct FusedArgs {
   Geom g;
   const uint64_t* planes;
-  const uint64_t* lut;  // [3][256] byte table (see encode_word)
+  const uint64_t* lut;  // byte tables (see ByteTables): [256] u64 for k = 3, then [2][256] u32
   uint32_t* counter;   // zeroed per launch
   uint64_t* ones_rec;  // zeroed per launch
   uint64_t* bits_rec;  // zeroed per launch
@@ -341,6 +377,9 @@ struct FusedArgs {
   uint64_t slot_e;
   uint64_t* bits_e;
   uint32_t* flags;
+#ifdef BIC_STAMPS
+  int known;
+#endif
 };
 
 // Global-memory emission for a row whose Golomb image does not fit the LDS window: codeword
@@ -418,7 +457,8 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
     int jp;
     step_prefix(x, w, st, n, jp);
     const bool eol = w == g.used - 1;
-    const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols, a.lut);
+    const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols,
+                                  ByteTables{reinterpret_cast<const uint32_t*>(a.lut + 256), a.lut});
     const uint32_t inc = wave_incl_sum_u32(e.len);
     const uint64_t off = carry + inc - e.len;
     carry += __shfl(inc, 63);
@@ -446,6 +486,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * (kGImg + kEImg)];
   __shared__ uint64_t sh_cnt[kTileRows], sh_pre[2];
   __shared__ uint32_t sh_tile;
+  __shared__ uint32_t s_lut[512];  // k = 1, 2 byte tables
   const Geom& g = a.g;
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* gimg = lds + wave * (kGImg + kEImg);
@@ -453,6 +494,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   const uint32_t tpp = (g.rows + kTileRows - 1) / kTileRows;  // tiles per plane
   const uint64_t ntiles = (uint64_t)tpp * g.nplanes;
   if (threadIdx.x == 0) sh_tile = atomicAdd(a.counter, 1u);
+  s_lut[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lut + 256)[threadIdx.x];
   __syncthreads();
   const uint64_t tile = sh_tile;
   if (tile >= ntiles) return;  // uniform over the workgroup
@@ -468,11 +510,12 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   uint32_t ones = 0;
   int fcol = INT_MAX;
   if (valid) {
-    RowCtx rc = row_ctx(a.planes, g, plane, row, 0);
+    uint64_t rr[WPL];
+    resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
 #pragma unroll
     for (int t = 0; t < WPL; ++t) {
       const uint32_t w = t * 64 + lane;
-      const uint64_t r = resid_word<PREDICT>(rc, g, row, w);
+      const uint64_t r = rr[t];
       ones += (uint32_t)__popcll(r);
       if (r && fcol == INT_MAX) fcol = (int)(w * 64 + __builtin_clzll(r));
       if (w < g.used) {
@@ -492,6 +535,11 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   __syncthreads();
 
   // ---- samples before this row: ones of earlier rows (+ one EOL sample per row) ----
+#ifdef BIC_STAMPS
+  if (a.known) {
+    if (threadIdx.x == 0) sh_pre[0] = g_known[0][rid];
+  } else
+#endif
   if (wave == 0) {
     uint64_t tile_ones = 0;
     for (int q = 0; q < kTileRows; ++q) tile_ones += sh_cnt[q];
@@ -504,6 +552,9 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
       if (lane == 0) rec_store(&a.ones_rec[rid], kInc | (O + tile_ones));
     }
     if (lane == 0) sh_pre[0] = O;
+#ifdef BIC_STAMPS
+    if (lane == 0 && rid < (1u << 17)) g_known[0][rid] = O;
+#endif
   }
   __syncthreads();
   STAMP(2);
@@ -536,6 +587,9 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   if constexpr (DO_G) {
     uint64_t L = 0;
     bool fits = true;
+#ifdef BIC_STAMPS
+    uint32_t dbg_slow = 0;
+#endif
     if (valid) {
       StepState st{(uint32_t)(O + row), -1};
       const uint32_t arow = row * (g.cols + 1);
@@ -548,7 +602,10 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
         int jp;
         step_prefix(x, w, st, n, jp);
         const bool eol = w == g.used - 1;
-        const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols, a.lut);
+        const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols, ByteTables{s_lut, a.lut});
+#ifdef BIC_STAMPS
+        dbg_slow += (e.path == 3 ? 1u : 0u) + (e.lng ? 1000u : 0u) + (e.path == 1 ? 1000000u : 0u);
+#endif
         const uint32_t inc = wave_incl_sum_u32(e.len);
         const uint64_t off = loc + inc - e.len;
         const uint64_t start = loc;
@@ -573,8 +630,19 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
       L = loc;
     }
     STAMP(4);
+#ifdef BIC_STAMPS
+    {
+      const uint32_t tot = wave_sum_u32(dbg_slow);
+      if (lane == 0 && (uint64_t)id * 8 + 7 < (1u << 21)) g_stamps[(uint64_t)id * 8 + 7] = tot;
+    }
+#endif
     if (lane == 0) sh_cnt[wave] = L;
     __syncthreads();
+#ifdef BIC_STAMPS
+    if (a.known) {
+      if (threadIdx.x == 0) sh_pre[1] = g_known[1][rid];
+    } else
+#endif
     if (wave == 0) {
       uint64_t tile_bits = 0;
       for (int q = 0; q < kTileRows; ++q) tile_bits += sh_cnt[q];
@@ -587,6 +655,9 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
         if (lane == 0) rec_store(&a.bits_rec[rid], kInc | (Gt + tile_bits));
       }
       if (lane == 0) sh_pre[1] = Gt;
+#ifdef BIC_STAMPS
+      if (lane == 0 && rid < (1u << 17)) g_known[1][rid] = Gt;
+#endif
     }
     __syncthreads();
     STAMP(5);
@@ -682,6 +753,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
   FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
               fs.eboff, fs.elen, fs.efrag, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
+#ifdef BIC_STAMPS
+  a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
+#endif
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t grid = (uint32_t)((g.rows + kTileRows - 1) / kTileRows * (uint64_t)g.nplanes);  // one per tile
   const bool dg = out_g != nullptr, de = out_e != nullptr;

@@ -87,7 +87,9 @@ struct FusedScratch {
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
 bool fused_supported(const Geom& g);
-void build_byte_lut(uint64_t* lut);  // host: [3][256] entries for the fused encoder
+// host: the fused encoder's byte tables -- lut[0..255] 64-bit entries for k = 3, then (as u32)
+// [2][256] packed entries for k = 1, 2 (bic_fused.hip encode_word); 4 KiB
+void build_byte_lut(uint64_t* lut);
 void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
                   const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,

@@ -781,11 +781,12 @@ void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_
 // (MSB = first pixel), the codewords of the runs that start AND end inside v -- between its
 // first and last 1 -- as one MSB-first pattern, with the byte's leading and trailing zeros.
 void build_byte_lut(uint64_t* lut) {
+  uint32_t* lut32 = reinterpret_cast<uint32_t*>(lut + 256);
   for (unsigned k = 1; k <= 3; ++k)
     for (unsigned v = 0; v < 256; ++v) {
-      uint64_t& en = lut[(k - 1) * 256 + v];
-      if (!v) {
-        en = 8ull << 40;
+      if (!v) {  // never read: the encoder skips zero bytes
+        if (k == 3) lut[v] = 0;
+        else lut32[(k - 1) * 256 + v] = 0;
         continue;
       }
       int pos[8], m = 0;
@@ -800,7 +801,11 @@ void build_byte_lut(uint64_t* lut) {
         R = (R << 1) | 1u;                       // terminator
         lr += k + (s >> k) + 1;
       }
-      en = R | ((uint64_t)lr << 32) | ((uint64_t)pos[0] << 40) | ((uint64_t)(7 - pos[m - 1]) << 44);
+      const unsigned t = (unsigned)pos[0], tz = (unsigned)(7 - pos[m - 1]);
+      if (k == 3)  // R up to 28 bits: 64-bit entry
+        lut[v] = R | ((uint64_t)lr << 32) | ((uint64_t)t << 40) | ((uint64_t)tz << 44);
+      else         // R up to 21 bits: R | lr << 21 | t << 26 | tz << 29
+        lut32[(k - 1) * 256 + v] = (uint32_t)R | (lr << 21) | (t << 26) | (tz << 29);
     }
 }
 
