@@ -349,14 +349,32 @@ __device__ __forceinline__ bool word_complete(uint64_t w, uint64_t G, uint64_t L
 }
 
 // Write a row image of L bits to absolute bit G of out: whole words with plain stores, the
-// first/last word (when shared with another row) into frag[0]/frag[1].
+// first/last word (when shared with another row) into frag[0]/frag[1]. Output word t of the row
+// holds image bits [64t - G%64, 64t - G%64 + 64): the bit shift inside the image's u32 words is
+// the same for every t, so the common case (no inserted bit) is three LDS reads and a funnel
+// shift per word, branch-free and independent across iterations.
 __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint64_t G, int64_t ins,
                                           uint64_t* out, uint64_t* frag) {
   const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6, nw = w1 - w0 + 1;
-  for (uint64_t t = lane_id(); t < nw; t += 64) {
-    const uint64_t wb = (w0 + t) * 64;
-    const uint64_t v = img64(img, (int64_t)wb - (int64_t)G, ins);
-    if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
+  if (ins >= 0) {
+    for (uint64_t t = lane_id(); t < nw; t += 64) {
+      const uint64_t wb = (w0 + t) * 64;
+      const uint64_t v = img64(img, (int64_t)wb - (int64_t)G, ins);
+      if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
+      else frag[t == 0 ? 0 : 1] = v;
+    }
+    return;
+  }
+  const uint32_t g = (uint32_t)(G & 63);
+  for (uint32_t t = lane_id(); t < (uint32_t)nw; t += 64) {
+    const int32_t a = (int32_t)(64 * t) - (int32_t)g;  // first image bit of output word t
+    const uint32_t b = a < 0 ? 0u : (uint32_t)a;
+    const uint32_t i = b >> 5, sh = b & 31;
+    const uint64_t hi = ((uint64_t)img[i] << 32) | img[i + 1];
+    uint64_t v = (hi << sh) | ((uint64_t)img[i + 2] >> (32 - sh));
+    if (a < 0) v >>= -a;
+    if (t != 0 && t != (uint32_t)nw - 1) out[w0 + t] = bswap64(v);
+    else if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
     else frag[t == 0 ? 0 : 1] = v;
   }
 }
