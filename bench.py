@@ -35,7 +35,11 @@ def parse():
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--rows", type=int, default=0, help="override image rows (c3/c2/c5)")
     ap.add_argument("--cols", type=int, default=0, help="override image cols")
-    ap.add_argument("--cpu-rows", type=int, default=4096, help="rows per plane in the CPU baseline sample")
+    ap.add_argument("--cpu-rows", type=int, default=16384, help="rows per plane in the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="repeat the CPU baseline sample until this much CPU time has been measured")
+    ap.add_argument("--encoder", default="single-pass", choices=["single-pass", "two-pass", "multipass"],
+                    help="row encoder for rows <= 16384 columns (bic_ctx_set_option)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
@@ -310,22 +314,26 @@ def cpu_baseline(wl, args):
     threads = max(1, min(nplanes, int(os.environ.get("OMP_NUM_THREADS", "8") or 8)))
     do_eg = 1 if isinstance(wl, C3) and type(wl) is C3 else 0
     predict = 0 if isinstance(wl, C2) else 1
-    if have_ref():
-        dt, gb, eb, used = Ref().baseline(planes, rows, wl.cols, predict=predict, do_eg=do_eg, threads=threads)
-        kind = "reference"
-    else:
-        import ctypes as C
-        o = Oracle()
-        used_c = C.c_int(0)
-        t0 = time.perf_counter()
-        o.lib.bo_baseline_planes(planes.ctypes.data_as(C.POINTER(C.c_uint64)), nplanes, rows, wl.cols,
-                                 planes.shape[-1], predict, do_eg, C.byref(used_c))
-        dt, used, kind = time.perf_counter() - t0, used_c.value, "port"
-    px = nplanes * rows * wl.cols
+    reps, dt, used = 0, 0.0, 0
+    while reps == 0 or (dt < args.cpu_seconds and reps < 32):
+        if have_ref():
+            t, _, _, used = Ref().baseline(planes, rows, wl.cols, predict=predict, do_eg=do_eg, threads=threads)
+            kind = "reference"
+        else:
+            import ctypes as C
+            o = Oracle()
+            used_c = C.c_int(0)
+            t0 = time.perf_counter()
+            o.lib.bo_baseline_planes(planes.ctypes.data_as(C.POINTER(C.c_uint64)), nplanes, rows, wl.cols,
+                                     planes.shape[-1], predict, do_eg, C.byref(used_c))
+            t, used, kind = time.perf_counter() - t0, used_c.value, "port"
+        dt += t
+        reps += 1
+    px = reps * nplanes * rows * wl.cols
     return {"value": px / dt / 1e6, "unit": "MPix/s", "cores": int(min(used, nplanes)), "kind": kind,
             "sample": f"{nplanes} planes x {rows} rows x {wl.cols} cols (first {rows} rows of the bench input), "
                       f"{'med+Golomb+EG' if do_eg else ('med+Golomb' if predict else 'Golomb')}, "
-                      f"OpenMP over planes, {dt:.2f} s"}
+                      f"OpenMP over planes, {reps} repetitions, {dt:.2f} s"}
 
 
 def main():
@@ -334,6 +342,8 @@ def main():
     world, rank, local = dist_setup(args)
     import pybic
     ctx = pybic.Context(local)
+    ctx.set_two_pass(args.encoder == "two-pass")
+    ctx.set_multipass(args.encoder == "multipass")
     if args.workload == "c3":
         wl = C3(ctx, args, rank)
     elif args.workload == "c2":

@@ -35,6 +35,7 @@ struct bic_ctx {
   // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
   bool prof_on = false;
   bool force_multipass = false;
+  bool two_pass = false;  // BIC_OPT_TWO_PASS: the two-pass row encoder instead of the single-kernel one
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -261,6 +262,10 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
     ctx->force_multipass = value != 0;
     return BIC_OK;
   }
+  if (option == BIC_OPT_TWO_PASS) {
+    ctx->two_pass = value != 0;
+    return BIC_OK;
+  }
   return BIC_EINVAL;
 }
 
@@ -323,7 +328,7 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
     const bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
     timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg", [&] {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
-                        bits_eg, ctx->flags);
+                        bits_eg, ctx->flags, !ctx->two_pass);
     });
     BIC_HIP(hipGetLastError());
     return BIC_OK;

@@ -133,6 +133,8 @@ __device__ __forceinline__ void tail_put_n(LaneEnc& e, uint64_t cw, uint32_t nb)
   if (nb) tail_put(e, cw, nb);
 }
 
+// STR = false computes only e.len (the length pass of the two-pass encoder).
+template <bool STR = true>
 __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t n, int jp, uint32_t arow,
                                                bool eol, uint32_t cols, ByteTables lut) {
   LaneEnc e{};
@@ -190,19 +192,21 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
             tz = (uint32_t)(en >> 44) & 15u;
           }
           const uint32_t sr = c + t, q = sr >> k, bin = sr & kmask;
-          if (first) {
-            e.head = bin;
-            e.k0 = k;
-            e.z = q;
-            tail_put(e, (1ull << lr) | R, 1 + lr);
-            first = false;
-          } else {
-            const uint32_t nb = k + q + 1;  // sr <= 63 here
-            if (nb + lr <= 64) {
-              tail_put(e, ((((uint64_t)bin << (q + 1)) | 1ull) << lr) | R, nb + lr);
+          if constexpr (STR) {
+            if (first) {
+              e.head = bin;
+              e.k0 = k;
+              e.z = q;
+              tail_put(e, (1ull << lr) | R, 1 + lr);
+              first = false;
             } else {
-              tail_put(e, ((uint64_t)bin << (q + 1)) | 1ull, nb);
-              tail_put_n(e, R, lr);
+              const uint32_t nb = k + q + 1;  // sr <= 63 here
+              if (nb + lr <= 64) {
+                tail_put(e, ((((uint64_t)bin << (q + 1)) | 1ull) << lr) | R, nb + lr);
+              } else {
+                tail_put(e, ((uint64_t)bin << (q + 1)) | 1ull, nb);
+                tail_put_n(e, R, lr);
+              }
             }
           }
           e.len += k + q + 1 + lr;
@@ -213,7 +217,7 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
       }
       if (eol) {  // the row's trailing zeros (pad columns excluded)
         const uint32_t sr = c - (w * 64 + 64 - cols), q = sr >> k;
-        tail_put(e, ((uint64_t)(sr & kmask) << (q + 1)) | 1ull, k + q + 1);
+        if constexpr (STR) tail_put(e, ((uint64_t)(sr & kmask) << (q + 1)) | 1ull, k + q + 1);
         e.len += k + q + 1;
       }
       return e;
@@ -241,14 +245,16 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
     const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
     const uint32_t q = s >> k;
     const uint32_t bin = s & ((1u << k) - 1u);
-    if (first) {
-      e.head = bin;
-      e.k0 = k;
-      e.z = q;
-      tail_put(e, 1, 1);
-      first = false;
-    } else {
-      tail_put(e, ((uint64_t)bin << (q + 1)) | 1ull, k + q + 1);  // s <= 63 here: k + q + 1 <= 64
+    if constexpr (STR) {
+      if (first) {
+        e.head = bin;
+        e.k0 = k;
+        e.z = q;
+        tail_put(e, 1, 1);
+        first = false;
+      } else {
+        tail_put(e, ((uint64_t)bin << (q + 1)) | 1ull, k + q + 1);  // s <= 63 here: k + q + 1 <= 64
+      }
     }
     e.len += k + q + 1;
     ++n;
@@ -388,6 +394,7 @@ struct FusedArgs {
   uint64_t* bits_rec;  // zeroed per launch
   uint64_t *gboff, *glen, *gfrag, *gslow;
   uint64_t *eboff, *elen, *efrag;
+  uint32_t* row_o;     // two-pass encoder: ones of the plane before each row
   uint64_t* out_g;
   uint64_t slot_g;
   uint64_t* bits_g;
@@ -495,10 +502,12 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
   }
 }
 
-// One workgroup = one TILE of 4 consecutive rows of one plane (one wave per row). Tiles are
-// claimed in order through an atomic counter with the planes interleaved (tile t -> plane
-// t % nplanes), so the 8 planes' look-back chains advance side by side; one look-back per tile
-// (by wave 0) serves its 4 rows, which combine their counts through LDS.
+// One workgroup = one TILE of kTileRows consecutive rows of one plane (one wave per row). Tiles
+// are claimed in order through one atomic ticket counter with the planes interleaved (tile t ->
+// plane t % nplanes), so the planes' look-back chains advance side by side and any idle CU takes
+// the oldest pending tile of any plane; one look-back per tile (by wave 0) serves its rows, which
+// combine their counts through LDS. (Per-plane counters bound to blockIdx were measured slower:
+// 793-918 us vs 682 us for C3, the claims themselves are not the limit.)
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * (kGImg + kEImg)];
@@ -510,12 +519,11 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   uint32_t* gimg = lds + wave * (kGImg + kEImg);
   uint32_t* eimg = gimg + kGImg;
   const uint32_t tpp = (g.rows + kTileRows - 1) / kTileRows;  // tiles per plane
-  const uint64_t ntiles = (uint64_t)tpp * g.nplanes;
   if (threadIdx.x == 0) sh_tile = atomicAdd(a.counter, 1u);
   s_lut[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lut + 256)[threadIdx.x];
   __syncthreads();
   const uint64_t tile = sh_tile;
-  if (tile >= ntiles) return;  // uniform over the workgroup
+  if (tile >= (uint64_t)tpp * g.nplanes) return;  // uniform over the workgroup
   const uint32_t plane = (uint32_t)(tile % g.nplanes), trow = (uint32_t)(tile / g.nplanes);
   const uint64_t rbase = (uint64_t)plane * tpp;  // this plane's first tile record
   const uint64_t rid = rbase + trow;             // this tile's record
@@ -528,6 +536,10 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   uint32_t ones = 0;
   int fcol = INT_MAX;
   if (valid) {
+    if constexpr (DO_G) {  // zero the Golomb image while the row loads are in flight
+      uint4* z = reinterpret_cast<uint4*>(gimg);
+      for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+    }
     uint64_t rr[WPL];
     resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
 #pragma unroll
@@ -626,13 +638,8 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
 #endif
         const uint32_t inc = wave_incl_sum_u32(e.len);
         const uint64_t off = loc + inc - e.len;
-        const uint64_t start = loc;
         loc += __shfl(inc, 63);
         if (fits && loc <= kCapBits) {
-          for (uint32_t i = (uint32_t)((start + 31) >> 5) + lane; i < (uint32_t)((loc + 31) >> 5); i += 64)
-            gimg[i] = 0;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
           if (!e.lng) {
             place_small(gimg, (uint32_t)off, e.head, e.k0);
             place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
@@ -687,8 +694,6 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
       if (lane == 0 && row == g.rows - 1) a.bits_g[plane] = Grel + L;
       if (Grel + L <= cap) {
         if (fits) {
-          const uint32_t endw = (uint32_t)((L + 31) >> 5);
-          if (lane < kPad) gimg[endw + lane] = 0;
           __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
           __builtin_amdgcn_wave_barrier();
           write_row(gimg, L, G, -1, a.out_g, a.gfrag + 2 * id);
@@ -706,6 +711,287 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
       }
     }
     STAMP(6);
+  }
+}
+
+// ==========================================================================================
+// Two-pass encoder. Pass 1 (k_len_rows) runs the look-back chains with nothing but lengths:
+// per 8-row tile the ones count, the ones prefix, each row's Golomb length (byte tables, no
+// codeword strings) and the bits prefix; it stores, per row, the ones before it and both
+// streams' bit offsets. Pass 2 (k_emit_rows) then writes every row independently -- no
+// look-back, no workgroup barrier -- streaming each row's codewords through a small LDS window
+// whose complete words go straight to HBM. A row's first and last word (shared with the
+// neighbouring rows) go to the fragment table, as in the single-pass kernel.
+// ==========================================================================================
+constexpr int kWin = 1024;                      // u32 words of one wave's output window (also holds
+                                                // the EG image of a plane's first-1 row)
+constexpr uint32_t kIterCap = (kWin - 8) * 32 - 128;  // bits one 64-word step may emit
+
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+__global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
+  __shared__ uint64_t sh_cnt[kTileRows], sh_pre[2];
+  __shared__ uint32_t sh_tile;
+  __shared__ uint32_t s_lut[512];
+  const Geom& g = a.g;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t tpp = (g.rows + kTileRows - 1) / kTileRows;
+  if (threadIdx.x == 0) sh_tile = atomicAdd(a.counter, 1u);
+  if (DO_G) s_lut[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lut + 256)[threadIdx.x];
+  __syncthreads();
+  const uint64_t tile = sh_tile;
+  if (tile >= (uint64_t)tpp * g.nplanes) return;  // uniform over the workgroup
+  const uint32_t plane = (uint32_t)(tile % g.nplanes), trow = (uint32_t)(tile / g.nplanes);
+  const uint64_t rbase = (uint64_t)plane * tpp, rid = rbase + trow;
+  const uint32_t row = trow * kTileRows + wave;
+  const bool valid = row < g.rows;
+  const uint64_t id = (uint64_t)plane * g.rows + row;
+
+  uint64_t rr[WPL];
+  uint32_t ones = 0;
+  if (valid) {
+    resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) ones += (uint32_t)__popcll(rr[t]);
+    ones = wave_sum_u32(ones);
+  }
+  if (lane == 0) sh_cnt[wave] = ones;
+  __syncthreads();
+  if (wave == 0) {
+    uint64_t tile_ones = 0;
+    for (int q = 0; q < kTileRows; ++q) tile_ones += sh_cnt[q];
+    uint64_t O = 0;
+    if (trow == 0) {
+      if (lane == 0) rec_store(&a.ones_rec[rid], kInc | tile_ones);
+    } else {
+      if (lane == 0) rec_store(&a.ones_rec[rid], kAgg | tile_ones);
+      O = lookback(a.ones_rec, rbase, rid, a.flags);
+      if (lane == 0) rec_store(&a.ones_rec[rid], kInc | (O + tile_ones));
+    }
+    if (lane == 0) sh_pre[0] = O;
+  }
+  __syncthreads();
+  uint64_t O = sh_pre[0];
+  for (int q = 0; q < wave; ++q) O += sh_cnt[q];
+
+  if (DO_E && valid && lane == 0) {  // EG as written: ~R then '1' per row; a '0' after the plane's first 1
+    const uint64_t Le = (uint64_t)g.cols + 1 + ((O == 0 && ones > 0) ? 1 : 0);
+    const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
+    const uint64_t cap = a.slot_e * 64;
+    a.eboff[id] = (uint64_t)plane * cap + Ge_rel;
+    if (Ge_rel + Le <= cap) {
+      a.elen[id] = Le;
+    } else {
+      a.elen[id] = 0;
+      atomicOr(&a.flags[0], 1u);
+    }
+    if (row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
+  }
+  if (valid && lane == 0) a.row_o[id] = (uint32_t)O;
+
+  if constexpr (DO_G) {
+    uint64_t L = 0;
+    uint32_t step_max = 0;
+    if (valid) {
+      StepState st{(uint32_t)(O + row), -1};
+      const uint32_t arow = row * (g.cols + 1);
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        const uint32_t w = t * 64 + lane;
+        if (t * 64 >= (int)g.used) break;
+        uint32_t n;
+        int jp;
+        step_prefix(rr[t], w, st, n, jp);
+        const LaneEnc e = encode_word<false>(rr[t], w, n, jp, arow, w == g.used - 1, g.cols, ByteTables{s_lut, a.lut});
+        const uint32_t tot = wave_sum_u32(e.len);
+        L += tot;
+        step_max = max(step_max, tot);
+      }
+    }
+    if (lane == 0) sh_cnt[wave] = L;
+    __syncthreads();
+    if (wave == 0) {
+      uint64_t tile_bits = 0;
+      for (int q = 0; q < kTileRows; ++q) tile_bits += sh_cnt[q];
+      uint64_t Gt = 0;
+      if (trow == 0) {
+        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | tile_bits);
+      } else {
+        if (lane == 0) rec_store(&a.bits_rec[rid], kAgg | tile_bits);
+        Gt = lookback(a.bits_rec, rbase, rid, a.flags);
+        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | (Gt + tile_bits));
+      }
+      if (lane == 0) sh_pre[1] = Gt;
+    }
+    __syncthreads();
+    if (valid && lane == 0) {
+      uint64_t Grel = sh_pre[1];
+      for (int q = 0; q < wave; ++q) Grel += sh_cnt[q];
+      const uint64_t cap = a.slot_g * 64;
+      a.gboff[id] = (uint64_t)plane * cap + Grel;
+      if (row == g.rows - 1) a.bits_g[plane] = Grel + L;
+      if (Grel + L <= cap) {
+        a.glen[id] = L;
+        a.gslow[id] = step_max > kIterCap ? O + row + 1 : 0;  // k_rows_global writes such rows
+      } else {
+        a.glen[id] = 0;
+        a.gslow[id] = 0;
+        atomicOr(&a.flags[0], 1u);
+      }
+    }
+  }
+}
+
+// EG row from registers: row bit b (b < cols) is ~R, bit cols is the end-of-row '1'; output word
+// j of the row holds row bits [64j - g, 64j - g + 64) with g = Ge % 64. Lane l forms words
+// j = 64t + l from its own row word and its left neighbour's (one shuffle per step).
+template <int WPL>
+__device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geom& g, uint64_t Ge, uint64_t Le,
+                                            uint64_t* out, uint64_t* frag) {
+  const int lane = lane_id();
+  const uint32_t sh = (uint32_t)(Ge & 63);
+  const uint64_t w0 = Ge >> 6, nw = ((Ge + Le - 1) >> 6) - w0 + 1;
+  const uint32_t eolw = g.cols >> 6;
+  const uint64_t eolbit = BIC_MSB >> (g.cols & 63);
+  uint64_t carry = 0;
+#pragma unroll
+  for (int t = 0; t <= WPL; ++t) {
+    const uint32_t j = t * 64 + lane;
+    if (t * 64 >= (int)nw) break;
+    uint64_t X = 0;
+    if (t < WPL && j < g.used) X = ~rr[t] & (j == g.used - 1 ? g.trail : ~0ull);
+    if (j == eolw) X |= eolbit;
+    uint64_t Xl = shfl_up_u64(X, 1);
+    if (lane == 0) Xl = carry;
+    carry = shfl_u64(X, 63);
+    const uint64_t v = sh ? (Xl << (64 - sh)) | (X >> sh) : X;
+    if (j < nw) {
+      const uint64_t wi = w0 + j;
+      if (word_complete(wi, Ge, Le)) out[wi] = bswap64(v);
+      else frag[j == 0 ? 0 : 1] = v;
+    }
+  }
+}
+
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+__global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * kWin];
+  __shared__ uint32_t s_lut[512];
+  const Geom& g = a.g;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t* win = lds + wave * kWin;
+  if (DO_G) s_lut[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lut + 256)[threadIdx.x];
+  __syncthreads();  // the only workgroup barrier
+  const uint64_t id = (uint64_t)blockIdx.x * kTileRows + wave;
+  if (id >= (uint64_t)g.rows * g.nplanes) return;
+  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+  const bool do_g = DO_G && a.glen[id] != 0 && a.gslow[id] == 0;
+  const bool do_e = DO_E && a.elen[id] != 0;
+  if (!do_g && !do_e) return;
+  if (do_g) {
+    uint4* z = reinterpret_cast<uint4*>(win);
+    for (int i = lane; i < kWin / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  uint64_t rr[WPL];
+  resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
+  const uint32_t O = a.row_o[id];
+
+  if (do_e) {
+    const uint64_t Ge = a.eboff[id], Le = a.elen[id];
+    if (Le == (uint64_t)g.cols + 1) {
+      eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
+    } else {
+      // the plane's first 1 is in this row: EG image with the inserted '0' (once per plane)
+      uint32_t* eimg = win;  // reused before the Golomb window is live
+      int fcol = INT_MAX;
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        const uint32_t w = t * 64 + lane;
+        if (rr[t] && fcol == INT_MAX) fcol = (int)(w * 64 + __builtin_clzll(rr[t]));
+        if (w < g.used) {
+          const uint64_t v = ~rr[t] & (w == g.used - 1 ? g.trail : ~0ull);
+          eimg[2 * w] = (uint32_t)(v >> 32);
+          eimg[2 * w + 1] = (uint32_t)v;
+        }
+      }
+      if (lane < kPad + 1) eimg[2 * g.used + lane] = 0;
+      fcol = wave_min(fcol);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) eimg[g.cols >> 5] |= 0x80000000u >> (g.cols & 31);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      write_row(eimg, Le, Ge, (int64_t)fcol + 1, a.out_e, a.efrag + 2 * id);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (do_g) {
+        uint4* z = reinterpret_cast<uint4*>(win);
+        for (int i = lane; i < kWin / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+
+  if constexpr (DO_G) {
+    if (!do_g) return;
+    const uint64_t G = a.gboff[id], L = a.glen[id];
+    uint64_t* out = a.out_g;
+    uint64_t* frag = a.gfrag + 2 * id;
+    uint64_t wbase = G & ~63ull;  // absolute bit of win[0]
+    const uint64_t first_word = G >> 6;
+    StepState st{O + row, -1};
+    const uint32_t arow = row * (g.cols + 1);
+    uint64_t loc = 0;  // row bits placed so far
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = t * 64 + lane;
+      if (t * 64 >= (int)g.used) break;
+      const uint64_t x = rr[t];
+      uint32_t n;
+      int jp;
+      step_prefix(x, w, st, n, jp);
+      const bool eol = w == g.used - 1;
+      const LaneEnc e = encode_word<true>(x, w, n, jp, arow, eol, g.cols, ByteTables{s_lut, a.lut});
+      const uint32_t inc = wave_incl_sum_u32(e.len);
+      const uint32_t p = (uint32_t)(G + loc - wbase) + inc - e.len;  // window bit of this lane's string
+      if (!e.lng) {
+        place_small(win, p, e.head, e.k0);
+        place128(win, p + e.k0 + e.z, e.t0, e.t1, e.tlen);
+      } else {
+        LdsSink ls{win, 0, 0};
+        emit_word(ls, p, x, w, n, jp, arow, eol, g.cols);
+        ls.flush();
+      }
+      loc += __shfl(inc, 63);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // flush the complete 64-bit words; the row's first word, if shared, is a fragment
+      const uint32_t nfull = (uint32_t)((G + loc - wbase) >> 6);
+      for (uint32_t q = lane; q < nfull; q += 64) {
+        const uint64_t v = ((uint64_t)win[2 * q] << 32) | win[2 * q + 1];
+        const uint64_t wi = (wbase >> 6) + q;
+        if (wi == first_word && (G & 63)) frag[0] = v;
+        else out[wi] = bswap64(v);
+      }
+      if (nfull) {  // carry the partial word to the front, clear the rest
+        const uint32_t c0 = win[2 * nfull], c1 = win[2 * nfull + 1];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t q = 2 + lane; q < 2 * nfull + 2; q += 64) win[q] = 0;
+        if (lane == 0) { win[0] = c0; win[1] = c1; }
+        wbase += 64ull * nfull;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    // the row's last word, if it ends inside one
+    if ((G + L) & 63) {
+      if (lane == 0) {
+        const uint64_t v = ((uint64_t)win[0] << 32) | win[1];
+        if ((wbase >> 6) == first_word) frag[0] = v;
+        else frag[1] = v;
+      }
+    }
   }
 }
 
@@ -734,7 +1020,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 9 + 1024;
+  return 256 + n * 8 * 2 + n * 8 * 9 + n * 4 + 1024;
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -752,7 +1038,8 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
   fs.gslow = q; q += n;
   fs.eboff = q; q += n;
   fs.elen = q; q += n;
-  fs.efrag = q;
+  fs.efrag = q; q += 2 * n;
+  fs.row_o = reinterpret_cast<uint32_t*>(q);
   return fs;
 }
 
@@ -767,27 +1054,37 @@ int read_stamps(uint64_t* host, size_t n) {
 void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
                   const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
-                  uint64_t* bits_e, uint32_t* flags) {
+                  uint64_t* bits_e, uint32_t* flags, bool single_pass) {
   (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
   FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
-              fs.eboff, fs.elen, fs.efrag, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
+              fs.eboff, fs.elen, fs.efrag, fs.row_o, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
 #endif
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t grid = (uint32_t)((g.rows + kTileRows - 1) / kTileRows * (uint64_t)g.nplanes);  // one per tile
+  const uint32_t egrid = (uint32_t)((nrows + kTileRows - 1) / kTileRows);                       // one per 8 rows
   const bool dg = out_g != nullptr, de = out_e != nullptr;
-#define BIC_FUSED(W, P)                                                               \
-  if (dg && de) k_encode_rows<W, P, true, true><<<grid, 64 * kTileRows, 0, s>>>(a);   \
-  else if (dg) k_encode_rows<W, P, true, false><<<grid, 64 * kTileRows, 0, s>>>(a);   \
-  else k_encode_rows<W, P, false, true><<<grid, 64 * kTileRows, 0, s>>>(a);
+  const dim3 blk(64 * kTileRows);
+#define BIC_PASSES(W, P, DG, DE)                                                        \
+  if (single_pass) {                                                                    \
+    k_encode_rows<W, P, DG, DE><<<grid, blk, 0, s>>>(a);                                \
+  } else {                                                                              \
+    k_len_rows<W, P, DG, DE><<<grid, blk, 0, s>>>(a);                                   \
+    k_emit_rows<W, P, DG, DE><<<egrid, blk, 0, s>>>(a);                                 \
+  }
+#define BIC_CODERS(W, P)                                                                \
+  if (dg && de) { BIC_PASSES(W, P, true, true) }                                        \
+  else if (dg) { BIC_PASSES(W, P, true, false) }                                        \
+  else { BIC_PASSES(W, P, false, true) }
   const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
   if (predict) {
-    if (wpl == 1) { BIC_FUSED(1, true) } else if (wpl == 2) { BIC_FUSED(2, true) } else { BIC_FUSED(4, true) }
+    if (wpl == 1) { BIC_CODERS(1, true) } else if (wpl == 2) { BIC_CODERS(2, true) } else { BIC_CODERS(4, true) }
   } else {
-    if (wpl == 1) { BIC_FUSED(1, false) } else if (wpl == 2) { BIC_FUSED(2, false) } else { BIC_FUSED(4, false) }
+    if (wpl == 1) { BIC_CODERS(1, false) } else if (wpl == 2) { BIC_CODERS(2, false) } else { BIC_CODERS(4, false) }
   }
-#undef BIC_FUSED
+#undef BIC_CODERS
+#undef BIC_PASSES
   const uint32_t fgrid = (uint32_t)((nrows + 255) / 256);
   if (dg) {
     const uint32_t rgrid = (uint32_t)((nrows + 3) / 4);

@@ -83,6 +83,7 @@ struct FusedScratch {
   uint64_t *ones_rec, *bits_rec;
   size_t zero_bytes;  // counter + records, zeroed per launch
   uint64_t *gboff, *glen, *gfrag, *gslow, *eboff, *elen, *efrag;
+  uint32_t* row_o;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
@@ -93,7 +94,7 @@ void build_byte_lut(uint64_t* lut);
 void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
                   const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
-                  uint64_t* bits_e, uint32_t* flags);
+                  uint64_t* bits_e, uint32_t* flags, bool single_pass);
 
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);

@@ -236,6 +236,10 @@ class Context:
     def set_multipass(self, on=True):
         self._chk(self.lib.bic_ctx_set_option(self.h, 1, int(on)), "bic_ctx_set_option")
 
+    def set_two_pass(self, on=True):
+        """the two-pass row encoder instead of the default single-kernel one"""
+        self._chk(self.lib.bic_ctx_set_option(self.h, 2, int(on)), "bic_ctx_set_option")
+
     def golomb_encode_samples(self, samples, n0=0, a0=0, bit0=0, cap_words=None, out=None):
         """samples: int32 device tensor (uint32 values) -> (stream int64 [cap], bits int64[2])."""
         n = samples.numel()

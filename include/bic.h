@@ -68,8 +68,12 @@ int bic_memset(bic_ctx* ctx, void* dst, int value, size_t bytes);
 /* Pre-grow the ctx scratch so later calls do not allocate (needed before stream capture). */
 int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
 /* Options: BIC_OPT_MULTIPASS = 1 forces the multi-pass chunk kernels for every geometry
- * (cross-checking the fused encoder); 0 (default) picks the fused encoder where it applies. */
+ * (cross-checking the row encoders); 0 (default) picks a row encoder where it applies. */
 #define BIC_OPT_MULTIPASS 1
+/* BIC_OPT_TWO_PASS = 1 selects the two-pass row encoder (lengths and offsets first, then every
+ * row written independently) instead of the default single-kernel one (rows stage in LDS until
+ * their offset is known). Same output; kept as a cross-check and for comparison. */
+#define BIC_OPT_TWO_PASS 2
 int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
 
 /* ---- a2: bitplane extraction (bitplane_tool.cpp:24-30) -----------------------------------

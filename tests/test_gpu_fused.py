@@ -1,7 +1,8 @@
-"""The single-pass row encoder (bic_fused.hip) against the oracle and against the multi-pass
-chunk kernels, with inputs built to reach each of its paths: k = 0 copy mode, lanes whose
-codewords exceed the 128-bit register string, rows whose output exceeds the LDS window
-(global fallback), many short rows sharing one output word (fixup chains)."""
+"""The row encoders (bic_fused.hip: the default two-pass one and the single-kernel one) against the
+oracle and against the multi-pass chunk kernels, with inputs built to reach each of their paths:
+k = 0 copy mode, byte tables, lanes whose codewords exceed the 128-bit register string, rows whose
+output exceeds the LDS window (global fallback), many short rows sharing one output word (fixup
+chains), the plane's first 1 (EG's inserted bit)."""
 import numpy as np
 import pytest
 
@@ -28,12 +29,29 @@ def check(ctx, oracle, P, cols, pred, both=True):
             assert stream_bytes(out[k], nb) == est.tobytes(), (k, coder)
 
 
+@pytest.fixture(params=["single_pass", "two_pass"])
+def encoder(request, ctx):
+    ctx.set_two_pass(request.param == "two_pass")
+    yield request.param
+    ctx.set_two_pass(False)
+
+
 @pytest.mark.parametrize("rows,cols", [(1, 1), (3, 64), (7, 65), (64, 100), (50, 1000), (40, 4096), (20, 8191),
                                        (16, 16384), (130, 640)])
 @pytest.mark.parametrize("p", [0.5, 0.25, 0.03, 0.0, 1.0])
-def test_fused_random(ctx, oracle, rows, cols, p):
+def test_fused_random(ctx, oracle, encoder, rows, cols, p):
     P = np.stack([oracle.gen_plane(1000 * rows + cols + k + int(p * 97), p, rows, cols) for k in range(2)])
     for pred in (1, 0):
+        check(ctx, oracle, P, cols, pred)
+
+
+def test_first_one_late_in_plane(ctx, oracle, encoder):
+    """EG's extra bit sits after the plane's first 1: put it deep inside the plane"""
+    rows, cols = 40, 3000
+    P = np.zeros((rows, (cols + 63) // 64), np.uint64)
+    P[23, 17] = np.uint64(1 << 40)
+    P[30:] = oracle.gen_plane(4, 0.3, 10, cols)
+    for pred in (0, 1):
         check(ctx, oracle, P, cols, pred)
 
 
@@ -42,19 +60,22 @@ def test_fused_vs_multipass(ctx, oracle):
     P = np.stack([oracle.gen_plane(77 + k, p, rows, cols) for k, p in enumerate([0.5, 0.1, 0.01])])
     d = ctx.to_dev(P)
     res = {}
-    for mp in (False, True):
-        ctx.set_multipass(mp)
+    for mode in ("single_pass", "two_pass", "multipass"):
+        ctx.set_multipass(mode == "multipass")
+        ctx.set_two_pass(mode == "two_pass")
         (og, bg), (oe, be) = ctx.encode_planes2(d, cols, True)
         ctx.sync()
-        res[mp] = [(as_u64(bg), [stream_bytes(og[k], as_u64(bg)[k]) for k in range(3)]),
-                   (as_u64(be), [stream_bytes(oe[k], as_u64(be)[k]) for k in range(3)])]
+        res[mode] = [(as_u64(bg), [stream_bytes(og[k], as_u64(bg)[k]) for k in range(3)]),
+                     (as_u64(be), [stream_bytes(oe[k], as_u64(be)[k]) for k in range(3)])]
     ctx.set_multipass(False)
-    for c in range(2):
-        assert np.array_equal(res[False][c][0], res[True][c][0])
-        assert res[False][c][1] == res[True][c][1]
+    ctx.set_two_pass(False)
+    for mode in ("two_pass", "multipass"):
+        for c in range(2):
+            assert np.array_equal(res["single_pass"][c][0], res[mode][c][0])
+            assert res["single_pass"][c][1] == res[mode][c][1]
 
 
-def test_long_lane_and_global_fallback(ctx, oracle):
+def test_long_lane_and_global_fallback(ctx, oracle, encoder):
     """zero rows drive k up (A grows, n grows by one EOL per row); then a dense word yields a
     lane string > 128 bits, and a dense row yields a row longer than the LDS window."""
     rows, cols = 160, 16384
@@ -68,7 +89,7 @@ def test_long_lane_and_global_fallback(ctx, oracle):
         check(ctx, oracle, P, cols, pred)
 
 
-def test_many_short_rows_share_words(ctx, oracle):
+def test_many_short_rows_share_words(ctx, oracle, encoder):
     """sparse rows of a few bits each: dozens of rows end inside one output word."""
     rows, cols = 3000, 64
     P = np.zeros((rows, 1), np.uint64)
@@ -77,7 +98,7 @@ def test_many_short_rows_share_words(ctx, oracle):
         check(ctx, oracle, P, cols, pred)
 
 
-def test_copy_mode_runs_across_words(ctx, oracle):
+def test_copy_mode_runs_across_words(ctx, oracle, encoder):
     """p = 0.5 keeps k in {0, 1}; long stretches of k = 0 take the copy path, including runs
     that start in an earlier word."""
     rows, cols = 64, 16384
@@ -87,7 +108,7 @@ def test_copy_mode_runs_across_words(ctx, oracle):
     check(ctx, oracle, P, cols, 1)
 
 
-def test_single_stream_calls_match_dual(ctx, oracle):
+def test_single_stream_calls_match_dual(ctx, oracle, encoder):
     rows, cols = 33, 2000
     P = oracle.gen_plane(3, 0.2, rows, cols)[None]
     d = ctx.to_dev(P)
@@ -100,7 +121,7 @@ def test_single_stream_calls_match_dual(ctx, oracle):
     assert stream_bytes(oe[0], as_u64(be)[0]) == stream_bytes(oe2[0], as_u64(be2)[0])
 
 
-def test_fused_overflow(ctx, oracle):
+def test_fused_overflow(ctx, oracle, encoder):
     rows, cols = 64, 1024
     P = oracle.gen_plane(8, 0.5, rows, cols)
     t = ctx.torch
