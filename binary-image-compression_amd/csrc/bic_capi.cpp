@@ -32,6 +32,7 @@ struct bic_ctx {
   size_t lentab_cap = 0;          // entries
   uint64_t* staging = nullptr;    // pinned host staging for lentab
   size_t staging_cap = 0;         // entries
+  std::vector<uint64_t> lentab_host;  // what ctx->lentab holds
   // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
   bool prof_on = false;
   bool force_multipass = false;
@@ -395,23 +396,29 @@ int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
   const size_t M = (size_t)W * W;
   const size_t ntiles = (rows / W) * (cols / W);
   if (ntiles >= 0x80000000ull || (unsigned long long)ntiles * M >= 0x80000000ull) return BIC_EINVAL;
-  // length table -> device (pinned staging; the previous copy must be done before reuse)
-  if (ctx->staging_cap < M + 1) {
-    BIC_HIP(hipStreamSynchronize(ctx->cur));
-    if (ctx->staging) (void)hipHostFree(ctx->staging);
-    if (ctx->lentab) (void)hipFree(ctx->lentab);
-    ctx->staging = nullptr;
-    ctx->lentab = nullptr;
-    ctx->staging_cap = ctx->lentab_cap = 0;
-    if (hipHostMalloc(&ctx->staging, (M + 1) * sizeof(uint64_t)) != hipSuccess) return BIC_ENOMEM;
-    if (hipMalloc(&ctx->lentab, (M + 1) * sizeof(uint64_t)) != hipSuccess) return BIC_ENOMEM;
-    ctx->staging_cap = ctx->lentab_cap = M + 1;
-  } else {
-    BIC_HIP(hipStreamSynchronize(ctx->cur));
+  // length table -> device (pinned staging; the previous copy must be done before reuse). A table
+  // equal to the one already on the device (the usual case: one W per run) is not re-sent, so
+  // repeated calls do not synchronise the host with the stream.
+  if (ctx->lentab_host.size() != M + 1 ||
+      std::memcmp(ctx->lentab_host.data(), lentab, (M + 1) * sizeof(uint64_t)) != 0) {
+    if (ctx->staging_cap < M + 1) {
+      BIC_HIP(hipStreamSynchronize(ctx->cur));
+      if (ctx->staging) (void)hipHostFree(ctx->staging);
+      if (ctx->lentab) (void)hipFree(ctx->lentab);
+      ctx->staging = nullptr;
+      ctx->lentab = nullptr;
+      ctx->staging_cap = ctx->lentab_cap = 0;
+      if (hipHostMalloc(&ctx->staging, (M + 1) * sizeof(uint64_t)) != hipSuccess) return BIC_ENOMEM;
+      if (hipMalloc(&ctx->lentab, (M + 1) * sizeof(uint64_t)) != hipSuccess) return BIC_ENOMEM;
+      ctx->staging_cap = ctx->lentab_cap = M + 1;
+    } else {
+      BIC_HIP(hipStreamSynchronize(ctx->cur));
+    }
+    std::memcpy(ctx->staging, lentab, (M + 1) * sizeof(uint64_t));
+    BIC_HIP(hipMemcpyAsync(ctx->lentab, ctx->staging, (M + 1) * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, ctx->cur));
+    ctx->lentab_host.assign(lentab, lentab + M + 1);
   }
-  std::memcpy(ctx->staging, lentab, (M + 1) * sizeof(uint64_t));
-  BIC_HIP(hipMemcpyAsync(ctx->lentab, ctx->staging, (M + 1) * sizeof(uint64_t),
-                         hipMemcpyHostToDevice, ctx->cur));
   // per-tile chosen weights feed the sample coder: use the caller's array or scratch
   const size_t wbytes = ((ntiles * sizeof(uint32_t)) + 255) & ~(size_t)255;
   if ((rc = ensure_scratch(ctx, wbytes + bic::sample_scratch_bytes(ntiles)))) return rc;
@@ -419,7 +426,6 @@ int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
   const bic::SampleScratch ss =
       bic::carve_sample_scratch(reinterpret_cast<char*>(ctx->scratch) + wbytes, ntiles);
   BIC_HIP(hipMemsetAsync(stats, 0, 3 * sizeof(uint64_t), ctx->cur));
-  if (resid) BIC_HIP(hipMemsetAsync(resid, 0, rows * wpr * sizeof(uint64_t), ctx->cur));
   timed(ctx, "tiles", [&] {
     bic::launch_tiles(ctx->cur, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, W, ctx->lentab, wts,
                       w_nonpred, w_pred, modes, resid, stats);

@@ -736,17 +736,108 @@ __global__ __launch_bounds__(kBlock) void k_tiles(const uint64_t* __restrict__ p
   }
 }
 
+// K8a: W x W tiles for W in {8, 16, 32, 64} (W divides 64, so no tile straddles a word). One
+// wave covers a strip of W rows x 64 words: lane l owns word column l, i.e. 64/W tiles side by
+// side, and walks the W rows with coalesced 512-byte loads (the row above stays in a register).
+// The med inside a tile (out-of-tile neighbours 0, R(0,0) = 0) is R = D ^ (D >> 1 & ~F) with
+// D = row ^ row-above and F the tiles' first-column bits. A second walk (cache-resident) writes
+// the residual image word by word -- every word exactly once: no pre-zeroing, no atomics.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_tiles_aligned(const uint64_t* __restrict__ plane, uint32_t rows,
+                                                          uint32_t cols, uint32_t wpr, uint32_t used, uint32_t nx,
+                                                          const uint64_t* __restrict__ lentab, uint32_t* weights,
+                                                          uint32_t* w_nonpred, uint32_t* w_pred, uint8_t* modes,
+                                                          uint64_t* resid, unsigned long long* stats) {
+  constexpr int T = 64 / W;
+  const int lane = lane_id();
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint32_t groups = (used + 63) / 64;
+  const uint32_t ty = (uint32_t)(gw / groups), w = (uint32_t)(gw % groups) * 64 + lane;
+  if (ty >= rows / W) return;  // wave-uniform
+  const bool act = w < used;
+  uint64_t F = 0;  // first column of every tile in the word
+#pragma unroll
+  for (int j = 0; j < T; ++j) F |= BIC_MSB >> (j * W);
+  const uint64_t* src = plane + (uint64_t)ty * W * wpr + (act ? w : 0);
+  uint32_t co[T], cO[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) co[j] = cO[j] = 0;
+  uint64_t up = 0;
+#pragma unroll 8
+  for (int r = 0; r < W; ++r) {
+    const uint64_t x = act ? src[(uint64_t)r * wpr] : 0;
+    const uint64_t d = x ^ up;
+    uint64_t R = d ^ ((d >> 1) & ~F);
+    if (r == 0) R &= ~F;  // compress7's med never writes a tile's R(0,0)
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const uint64_t m = (W == 64) ? ~0ull : (((1ull << W) - 1) << (64 - W * (j + 1)));
+      co[j] += (uint32_t)__popcll(x & m);
+      cO[j] += (uint32_t)__popcll(R & m);
+    }
+    up = x;
+  }
+  uint64_t L = 0, keepR = 0;  // keepR: word mask of the tiles coded as residuals ('O')
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const uint32_t col0 = w * 64 + j * W;
+    if (!act || col0 >= cols) continue;
+    const uint64_t tile = (uint64_t)ty * nx + col0 / W;
+    const bool pred = lentab[co[j]] > lentab[cO[j]];  // compress7_test.cpp:248
+    const uint32_t wc = pred ? cO[j] : co[j];
+    if (weights) weights[tile] = wc;
+    if (w_nonpred) w_nonpred[tile] = co[j];
+    if (w_pred) w_pred[tile] = cO[j];
+    if (modes) modes[tile] = pred ? 'O' : 'o';
+    L += lentab[wc];
+    if (pred) keepR |= (W == 64) ? ~0ull : (((1ull << W) - 1) << (64 - W * (j + 1)));
+  }
+  if (resid && act) {
+    uint64_t* dst = resid + (uint64_t)ty * W * wpr + w;
+    const uint64_t valid = w == used - 1 && (cols & 63) ? ~(~0ull >> (cols & 63)) : ~0ull;
+    up = 0;
+#pragma unroll 8
+    for (int r = 0; r < W; ++r) {
+      const uint64_t x = src[(uint64_t)r * wpr];
+      const uint64_t d = x ^ up;
+      uint64_t R = d ^ ((d >> 1) & ~F);
+      if (r == 0) R &= ~F;
+      dst[(uint64_t)r * wpr] = ((R & keepR) | (x & ~keepR)) & valid;
+      up = x;
+    }
+  }
+  L = wave_sum_u64(L);
+  if (lane == 0 && L) atomicAdd(&stats[2], (unsigned long long)L);
+}
+
 void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
                   uint32_t W, const uint64_t* lentab_dev, uint32_t* weights, uint32_t* w_nonpred,
                   uint32_t* w_pred, uint8_t* modes, uint64_t* resid, uint64_t* stats) {
   const uint32_t nx = cols / W, ny = rows / W;
   const uint32_t ntiles = nx * ny;
+  const uint32_t used = (cols + 63) / 64;
+  unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
+  if (W == 8 || W == 16 || W == 32 || W == 64) {
+    // words past `used` in a row (wpr > used) are the only ones the kernel does not write
+    if (resid && wpr > used) (void)hipMemsetAsync(resid, 0, (size_t)rows * wpr * sizeof(uint64_t), s);
+    const uint64_t waves = (uint64_t)ny * ((used + 63) / 64);
+    const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
+#define BIC_TILES(WW) \
+    k_tiles_aligned<WW><<<grid, kBlock, 0, s>>>(plane, rows, cols, wpr, used, nx, lentab_dev, weights, w_nonpred, \
+                                               w_pred, modes, resid, st)
+    if (W == 8) BIC_TILES(8);
+    else if (W == 16) BIC_TILES(16);
+    else if (W == 32) BIC_TILES(32);
+    else BIC_TILES(64);
+#undef BIC_TILES
+    return;
+  }
+  if (resid) (void)hipMemsetAsync(resid, 0, (size_t)rows * wpr * sizeof(uint64_t), s);
   const uint32_t tpw = 64 / W;
   const uint64_t waves = (ntiles + tpw - 1) / tpw;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
   k_tiles<<<grid, kBlock, 0, s>>>(plane, rows, cols, wpr, W, nx, ntiles, lentab_dev, weights, w_nonpred,
-                                  w_pred, modes, reinterpret_cast<unsigned long long*>(resid),
-                                  reinterpret_cast<unsigned long long*>(stats));
+                                  w_pred, modes, reinterpret_cast<unsigned long long*>(resid), st);
 }
 
 // ------------------------------------------------------------------------------------

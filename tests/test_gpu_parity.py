@@ -242,10 +242,14 @@ def test_tiles_golden(ctx, golden):
         assert np.array_equal(as_u64(res["resid"]), mask_pixels(A[k + "_resid"], cols)), k
 
 
-@pytest.mark.parametrize("W,rows,cols,p", [(32, 1024, 1024, 0.5), (32, 512, 2048, 0.02), (8, 256, 512, 0.1),
-                                           (5, 100, 200, 0.3), (64, 256, 320, 0.01)])
-def test_tiles_stream(ctx, oracle, W, rows, cols, p):
-    I = oracle.gen_plane(31 + W, p, rows, cols)
+@pytest.mark.parametrize("W,rows,cols,p,wpr", [(32, 1024, 1024, 0.5, None), (32, 512, 2048, 0.02, None),
+                                               (8, 256, 512, 0.1, None), (5, 100, 200, 0.3, None),
+                                               (64, 256, 320, 0.01, None), (16, 96, 208, 0.4, None),
+                                               (8, 64, 72, 0.5, None), (32, 64, 96, 0.3, 4), (16, 48, 4160, 0.2, None)])
+def test_tiles_stream(ctx, oracle, W, rows, cols, p, wpr):
+    """aligned tiles (W in 8..64, one word holds 64/W tiles) and the generic path (W = 5); partial
+    last words, rows with words past the pixels (wpr > ceil(cols/64))"""
+    I = oracle.gen_plane(31 + W, p, rows, cols, wpr=wpr)
     lt = oracle.lentab(W)
     exp = oracle.patch_encode(I, cols, W, lt)
     res = ctx.patch_encode(ctx.to_dev(I), cols, W, lt)
@@ -255,6 +259,11 @@ def test_tiles_stream(ctx, oracle, W, rows, cols, p):
     assert int(stats[2]) == exp["L"]
     assert stream_bytes(res["stream"], exp["bits"]) == exp["stream"].tobytes()
     assert np.array_equal(as_u64(res["resid"]), mask_pixels(exp["residual"], cols))
+    for key in ("w_nonpred", "w_pred", "weights"):
+        if key in exp:
+            assert np.array_equal(res[key].cpu().numpy().view(np.uint32), np.asarray(exp[key], np.uint32)), key
+    if "modes" in exp:
+        assert bytes(res["modes"].cpu().numpy()).decode() == exp["modes"], "modes"
 
 
 def test_pack_streams(ctx, oracle):
