@@ -100,6 +100,66 @@ __device__ __forceinline__ T block_excl_scan(T x, T* tmp, T& total) {
   return res;
 }
 
+// ------------------------------------------------------------------------------------
+// Decoupled look-back records (row encoder tiles, sample coder blocks): 8-byte {flag, value}
+// granules written and polled with agent-scope relaxed atomics (cdna_hip_programming.md §6
+// Guideline 16, R2). flag 0 = not yet published, kAgg = the unit's own total, kInc = inclusive
+// prefix. A unit takes its index from a ticket counter, so every unit it waits on holds an earlier
+// ticket and is already running or done.
+// ------------------------------------------------------------------------------------
+constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+__device__ __forceinline__ void rec_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t rec_load(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix of the record values [base, me): decoupled look-back by one wave. Each probe
+// reads 256 predecessors (4 per lane; position p = 4*lane + q counts back from me-1) and stops
+// at the nearest inclusive record, so the inclusive front advances 256 tiles per round trip.
+// Bounded spin.
+__device__ __forceinline__ uint64_t lookback(uint64_t* recs, uint64_t base, uint64_t me, uint32_t* flags) {
+  uint64_t excl = 0;
+  int64_t pos = (int64_t)me - 1;
+  const int lane = lane_id();
+  uint32_t spins = 0;
+  while (pos >= (int64_t)base) {
+    uint64_t r[4];
+    int stop = 256;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // all four loads in flight before any is used
+      const int64_t idx = pos - (4 * lane + q);
+      r[q] = rec_load(&recs[idx >= (int64_t)base ? idx : (int64_t)base]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (pos - (4 * lane + q) < (int64_t)base) r[q] = kInc;
+      const uint64_t inc = __ballot((r[q] >> 62) == 2);
+      if (inc) stop = min(stop, 4 * (int)__builtin_ctzll(inc) + q);
+    }
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bad |= (4 * lane + q <= stop) && (r[q] >> 62) == 0;
+    if (__ballot(bad)) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {  // ~seconds: a record never arrived
+        if (lane == 0) atomicOr(&flags[2], 1u);
+        return excl;
+      }
+      continue;
+    }
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v += (4 * lane + q <= stop) ? (r[q] & kValMask) : 0;
+    excl += wave_sum_u64(v);
+    if (stop < 256) break;
+    pos -= 256;
+  }
+  return excl;
+}
+
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks that share an XCD (b % 8 equal) get a contiguous range of logical ids, so the
 // chunks of consecutive rows -- which re-read each other as the row above -- share an L2.

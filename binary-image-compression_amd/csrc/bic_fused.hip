@@ -42,59 +42,6 @@ constexpr int kGImg = 684;    // u32 words of Golomb row image per wave (21760 b
                               // the k = 1, 2 byte tables 4 workgroups (32 waves) fit one CU's LDS)
 constexpr int kEImg = 520;    // u32 words of EG row image per wave (cols <= 16384)
 constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads ahead)
-constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
-
-__device__ __forceinline__ void rec_store(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t rec_load(uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Exclusive prefix of the record values [base, me): decoupled look-back by one wave. Each probe
-// reads 256 predecessors (4 per lane; position p = 4*lane + q counts back from me-1) and stops
-// at the nearest inclusive record, so the inclusive front advances 256 tiles per round trip.
-// Bounded spin.
-__device__ __forceinline__ uint64_t lookback(uint64_t* recs, uint64_t base, uint64_t me, uint32_t* flags) {
-  uint64_t excl = 0;
-  int64_t pos = (int64_t)me - 1;
-  const int lane = lane_id();
-  uint32_t spins = 0;
-  while (pos >= (int64_t)base) {
-    uint64_t r[4];
-    int stop = 256;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {  // all four loads in flight before any is used
-      const int64_t idx = pos - (4 * lane + q);
-      r[q] = rec_load(&recs[idx >= (int64_t)base ? idx : (int64_t)base]);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (pos - (4 * lane + q) < (int64_t)base) r[q] = kInc;
-      const uint64_t inc = __ballot((r[q] >> 62) == 2);
-      if (inc) stop = min(stop, 4 * (int)__builtin_ctzll(inc) + q);
-    }
-    bool bad = false;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bad |= (4 * lane + q <= stop) && (r[q] >> 62) == 0;
-    if (__ballot(bad)) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {  // ~seconds: a record never arrived
-        if (lane == 0) atomicOr(&flags[2], 1u);
-        return excl;
-      }
-      continue;
-    }
-    uint64_t v = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v += (4 * lane + q <= stop) ? (r[q] & kValMask) : 0;
-    excl += wave_sum_u64(v);
-    if (stop < 256) break;
-    pos -= 256;
-  }
-  return excl;
-}
-
 // One lane's codewords for one residual word.
 struct LaneEnc {
   uint32_t head, k0, z;  // first codeword: k0-bit binary part, then z unary zeros

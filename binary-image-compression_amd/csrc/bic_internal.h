@@ -60,10 +60,12 @@ void launch_eg_emit(hipStream_t s, const Geom& g, const uint64_t* planes, int pr
 
 // Sample coder (GolombCoder::codeSample over an array).
 struct SampleScratch {
-  uint64_t* blk_sum;   // [nblk]
-  uint64_t* blk_A;     // [nblk]
-  uint64_t* blk_bits;  // [nblk]
-  uint64_t* blk_off;   // [nblk]
+  uint32_t* counter;   // block tickets
+  uint64_t* a_rec;     // [nblk] look-back records: sums of samples
+  uint64_t* b_rec;     // [nblk] look-back records: codeword bits
+  uint64_t* blk_A;     // [nblk] accumulated error before the block
+  uint64_t* blk_off;   // [nblk] absolute bit offset of the block
+  size_t zero_bytes;   // counter + records, zeroed per launch
 };
 size_t sample_scratch_bytes(size_t n);
 SampleScratch carve_sample_scratch(void* base, size_t n);

@@ -529,52 +529,95 @@ void launch_eg_emit(hipStream_t s, const Geom& g, const uint64_t* planes, int pr
 }
 
 // ------------------------------------------------------------------------------------
-// Sample coder: GolombCoder::codeSample over an array (reduce -> scan -> lengths ->
-// scan -> emit). ITEMS consecutive samples per thread.
+// Sample coder: GolombCoder::codeSample over an array. Blocks of kSampPerBlk samples take a
+// ticket; a first kernel runs two decoupled look-backs per block -- the sum of the samples
+// before it (the coder's accumulated error A) and, once its lengths are known, its bit offset
+// -- and zeroes the block's output words; a second kernel writes the codewords.
 // ------------------------------------------------------------------------------------
 constexpr int kItems = 8;
 constexpr uint32_t kSampPerBlk = kBlock * kItems;
 
-__global__ __launch_bounds__(kBlock) void k_samp_sum(const uint32_t* __restrict__ s, size_t n,
-                                                     uint64_t* blk_sum) {
+__global__ __launch_bounds__(kBlock) void k_samp_scan(const uint32_t* __restrict__ s, size_t n, uint64_t n0,
+                                                      uint64_t a0, unsigned bit0, SampleScratch ss,
+                                                      uint64_t* out, size_t cap_words, uint64_t* bits_out,
+                                                      uint32_t* flags, uint32_t nblk) {
   __shared__ uint64_t tmp[17];
-  const uint64_t base = (uint64_t)blockIdx.x * kSampPerBlk + (uint64_t)threadIdx.x * kItems;
+  __shared__ uint64_t sh[2];
+  __shared__ uint32_t sh_blk;
+  if (threadIdx.x == 0) sh_blk = atomicAdd(ss.counter, 1u);
+  __syncthreads();
+  const uint32_t blk = sh_blk;
+  const uint64_t base = (uint64_t)blk * kSampPerBlk + (uint64_t)threadIdx.x * kItems;
+  uint32_t v[kItems];
   uint64_t a = 0;
 #pragma unroll
-  for (int i = 0; i < kItems; ++i)
-    if (base + i < n) a += s[base + i];
-  uint64_t tot;
-  block_excl_scan<uint64_t>(a, tmp, tot);
-  if (threadIdx.x == 0) blk_sum[blockIdx.x] = tot;
-}
-
-// single workgroup: exclusive scan of per-block values (+ init) -> dst, total -> *total_out
-__global__ __launch_bounds__(1024) void k_scan_blocks(const uint64_t* src, uint64_t* dst, uint32_t nblk,
-                                                      uint64_t init, uint64_t* total_out) {
-  __shared__ uint64_t tmp[17];
-  uint64_t carry = init;
-  for (uint32_t i0 = 0; i0 < nblk; i0 += blockDim.x) {
-    const uint32_t i = i0 + threadIdx.x;
-    const uint64_t v = i < nblk ? src[i] : 0;
-    uint64_t tot;
-    const uint64_t e = block_excl_scan<uint64_t>(v, tmp, tot);
-    if (i < nblk) dst[i] = carry + e;
-    carry += tot;
+  for (int i = 0; i < kItems; ++i) {
+    v[i] = base + i < n ? s[base + i] : 0;
+    a += v[i];
   }
-  if (threadIdx.x == 0 && total_out) *total_out = carry - init;
+  uint64_t tot_a;
+  const uint64_t ea = block_excl_scan<uint64_t>(a, tmp, tot_a);
+  if (threadIdx.x < 64) {  // A before this block
+    uint64_t A0 = a0;
+    if (blk == 0) {
+      if (threadIdx.x == 0) rec_store(&ss.a_rec[0], kInc | (a0 + tot_a));
+    } else {
+      if (threadIdx.x == 0) rec_store(&ss.a_rec[blk], kAgg | tot_a);
+      A0 = lookback(ss.a_rec, 0, blk, flags);  // inclusive records carry a0
+      if (threadIdx.x == 0) rec_store(&ss.a_rec[blk], kInc | (A0 + tot_a));
+    }
+    if (threadIdx.x == 0) sh[0] = A0;
+  }
+  __syncthreads();
+  const uint64_t Ablk = sh[0];
+  uint64_t AA = Ablk + ea, bits = 0;
+#pragma unroll
+  for (int i = 0; i < kItems; ++i) {
+    if (base + i < n) {
+      const uint64_t nn = n0 + base + i;
+      if (nn >= 0x80000000ull || AA >= 0x80000000ull) atomicOr(&flags[1], 1u);
+      const uint32_t k = golomb_k_state((uint32_t)nn, (uint32_t)AA);
+      bits += k + (v[i] >> k) + 1;
+      AA += v[i];
+    }
+  }
+  uint64_t tot_b;
+  block_excl_scan<uint64_t>(bits, tmp, tot_b);
+  if (threadIdx.x < 64) {  // bit offset of this block (the stream starts at bit0)
+    uint64_t B0 = bit0;
+    if (blk == 0) {
+      if (threadIdx.x == 0) rec_store(&ss.b_rec[0], kInc | (bit0 + tot_b));
+    } else {
+      if (threadIdx.x == 0) rec_store(&ss.b_rec[blk], kAgg | tot_b);
+      B0 = lookback(ss.b_rec, 0, blk, flags);  // inclusive records carry bit0
+      if (threadIdx.x == 0) rec_store(&ss.b_rec[blk], kInc | (B0 + tot_b));
+    }
+    if (threadIdx.x == 0) {
+      sh[1] = B0;
+      ss.blk_A[blk] = Ablk;
+      ss.blk_off[blk] = B0;
+      if (blk == nblk - 1) {
+        bits_out[0] = B0 + tot_b - bit0;
+        bits_out[1] = Ablk + tot_a - a0;
+      }
+    }
+  }
+  __syncthreads();
+  // zero the words this block's codewords touch (within the caller's capacity); the words it
+  // shares with its neighbours may be zeroed by either -- all of it before any codeword is OR'd
+  const uint64_t B0 = sh[1];
+  const uint64_t w_lo = blk == 0 ? 0 : B0 / 64, w_hi = (B0 + tot_b + 63) / 64;
+  if (w_hi > cap_words && threadIdx.x == 0) atomicOr(&flags[0], 1u);
+  for (uint64_t w = w_lo + threadIdx.x; w < w_hi && w < cap_words; w += kBlock) out[w] = 0;
 }
 
-template <bool EMIT>
-__global__ __launch_bounds__(kBlock) void k_samp_code(const uint32_t* __restrict__ s, size_t n, uint64_t n0,
-                                                      const uint64_t* blk_A, uint64_t* blk_bits,
-                                                      const uint64_t* blk_off, uint64_t* out,
-                                                      uint32_t* flags, const uint64_t* total_bits,
+__global__ __launch_bounds__(kBlock) void k_samp_emit(const uint32_t* __restrict__ s, size_t n, uint64_t n0,
+                                                      SampleScratch ss, uint64_t* out, const uint64_t* total_bits,
                                                       unsigned bit0, size_t cap_words) {
   __shared__ uint64_t tmp[17];
-  if constexpr (EMIT) {
-    if ((bit0 + *total_bits + 63) / 64 > cap_words) return;  // block-uniform
-  }
-  const uint64_t base = (uint64_t)blockIdx.x * kSampPerBlk + (uint64_t)threadIdx.x * kItems;
+  if ((bit0 + *total_bits + 63) / 64 > cap_words) return;  // overflow: write nothing (flagged)
+  const uint32_t blk = blockIdx.x;
+  const uint64_t base = (uint64_t)blk * kSampPerBlk + (uint64_t)threadIdx.x * kItems;
   uint32_t v[kItems];
   uint64_t a = 0;
 #pragma unroll
@@ -583,61 +626,49 @@ __global__ __launch_bounds__(kBlock) void k_samp_code(const uint32_t* __restrict
     a += v[i];
   }
   uint64_t tot;
-  uint64_t A = blk_A[blockIdx.x] + block_excl_scan<uint64_t>(a, tmp, tot);
-  // lengths
+  uint64_t A = ss.blk_A[blk] + block_excl_scan<uint64_t>(a, tmp, tot);
   uint64_t bits = 0;
   {
     uint64_t AA = A;
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
       if (base + i < n) {
-        const uint64_t nn = n0 + base + i;
-        if (nn >= 0x80000000ull || AA >= 0x80000000ull) atomicOr(&flags[1], 1u);
-        const uint32_t k = golomb_k_state((uint32_t)nn, (uint32_t)AA);
+        const uint32_t k = golomb_k_state((uint32_t)(n0 + base + i), (uint32_t)AA);
         bits += k + (v[i] >> k) + 1;
         AA += v[i];
       }
     }
   }
-  if constexpr (!EMIT) {
-    uint64_t bt;
-    block_excl_scan<uint64_t>(bits, tmp, bt);
-    if (threadIdx.x == 0) blk_bits[blockIdx.x] = bt;
-  } else {
-    uint64_t bt;
-    uint64_t off = blk_off[blockIdx.x] + block_excl_scan<uint64_t>(bits, tmp, bt);
-    GlobalSink gs{reinterpret_cast<unsigned long long*>(out), 0, 0};
+  uint64_t off = ss.blk_off[blk] + block_excl_scan<uint64_t>(bits, tmp, tot);
+  GlobalSink gs{reinterpret_cast<unsigned long long*>(out), 0, 0};
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-      if (base + i < n) {
-        const uint32_t k = golomb_k_state((uint32_t)(n0 + base + i), (uint32_t)A);
-        emit_codeword(gs, off, v[i], k);
-        off += k + (v[i] >> k) + 1;
-        A += v[i];
-      }
+  for (int i = 0; i < kItems; ++i) {
+    if (base + i < n) {
+      const uint32_t k = golomb_k_state((uint32_t)(n0 + base + i), (uint32_t)A);
+      emit_codeword(gs, off, v[i], k);
+      off += k + (v[i] >> k) + 1;
+      A += v[i];
     }
-    gs.flush();
   }
-}
-
-__global__ __launch_bounds__(1024) void k_samp_zero(uint64_t* out, const uint64_t* total_bits,
-                                                    unsigned bit0, size_t cap_words, uint32_t* flags) {
-  const uint64_t words = (bit0 + *total_bits + 63) / 64;
-  if (words > cap_words) {
-    if (threadIdx.x == 0) atomicOr(&flags[0], 1u);
-    return;
-  }
-  for (uint64_t i = threadIdx.x; i < words; i += blockDim.x) out[i] = 0;
+  gs.flush();
 }
 
 size_t sample_scratch_bytes(size_t n) {
   const size_t nblk = (n + kSampPerBlk - 1) / kSampPerBlk + 1;
-  return 4 * nblk * sizeof(uint64_t) + 256;
+  return 256 + 4 * nblk * sizeof(uint64_t) + 256;
 }
 SampleScratch carve_sample_scratch(void* base, size_t n) {
   const size_t nblk = (n + kSampPerBlk - 1) / kSampPerBlk + 1;
-  uint64_t* p = reinterpret_cast<uint64_t*>(base);
-  return SampleScratch{p, p + nblk, p + 2 * nblk, p + 3 * nblk};
+  char* c = reinterpret_cast<char*>(base);
+  uint64_t* p = reinterpret_cast<uint64_t*>(c + 256);
+  SampleScratch ss;
+  ss.counter = reinterpret_cast<uint32_t*>(c);
+  ss.a_rec = p;
+  ss.b_rec = p + nblk;
+  ss.blk_A = p + 2 * nblk;
+  ss.blk_off = p + 3 * nblk;
+  ss.zero_bytes = 256 + 2 * nblk * sizeof(uint64_t);
+  return ss;
 }
 
 void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uint64_t n0,
@@ -648,14 +679,9 @@ void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uin
     (void)hipMemsetAsync(bits_out, 0, 2 * sizeof(uint64_t), s);
     return;
   }
-  k_samp_sum<<<nblk, kBlock, 0, s>>>(samples, n, ss.blk_sum);
-  k_scan_blocks<<<1, 1024, 0, s>>>(ss.blk_sum, ss.blk_A, nblk, a0, bits_out + 1);
-  k_samp_code<false><<<nblk, kBlock, 0, s>>>(samples, n, n0, ss.blk_A, ss.blk_bits, nullptr, nullptr, flags,
-                                              nullptr, 0, 0);
-  k_scan_blocks<<<1, 1024, 0, s>>>(ss.blk_bits, ss.blk_off, nblk, bit0, bits_out);
-  k_samp_zero<<<1, 1024, 0, s>>>(out, bits_out, bit0, cap_words, flags);
-  k_samp_code<true><<<nblk, kBlock, 0, s>>>(samples, n, n0, ss.blk_A, nullptr, ss.blk_off, out, flags,
-                                             bits_out, bit0, cap_words);
+  (void)hipMemsetAsync(ss.counter, 0, ss.zero_bytes, s);
+  k_samp_scan<<<nblk, kBlock, 0, s>>>(samples, n, n0, a0, bit0, ss, out, cap_words, bits_out, flags, nblk);
+  k_samp_emit<<<nblk, kBlock, 0, s>>>(samples, n, n0, ss, out, bits_out, bit0, cap_words);
 }
 
 // ------------------------------------------------------------------------------------
