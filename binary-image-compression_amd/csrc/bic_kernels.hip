@@ -872,23 +872,34 @@ void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t 
 __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ slots, int nplanes,
                                                  uint64_t slot_words, const uint64_t* __restrict__ plane_bits,
                                                  uint64_t* __restrict__ dst, uint64_t* word_off) {
+  __shared__ uint64_t sh_off, sh_nw;
   const int p = blockIdx.y;
-  uint64_t off = 0;
-  for (int q = 0; q < p; ++q) off += (plane_bits[q] + 63) / 64;
-  const uint64_t nw = (plane_bits[p] + 63) / 64;
+  if (threadIdx.x < 64) {  // this plane's start word: one wave sums the earlier planes' sizes
+    uint64_t part = 0;
+    for (int q = threadIdx.x; q < p; q += 64) part += (plane_bits[q] + 63) / 64;
+    part = wave_sum_u64(part);
+    if (threadIdx.x == 0) {
+      sh_off = part;
+      sh_nw = (plane_bits[p] + 63) / 64;
+    }
+  }
+  __syncthreads();
+  const uint64_t off = sh_off, nw = sh_nw;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     word_off[p] = off;
     if (p == nplanes - 1) word_off[nplanes] = off + nw;
   }
   if (nw > slot_words) return;
+  const uint64_t* src = slots + (uint64_t)p * slot_words;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * kBlock)
-    dst[off + i] = slots[(uint64_t)p * slot_words + i];
+    dst[off + i] = src[i];
 }
 
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off) {
-  uint32_t gx = (uint32_t)((slot_words + kBlock - 1) / kBlock);
-  if (gx > 1024) gx = 1024;
+  // ~4 words per thread per plane: enough blocks in flight without re-summing the prefix often
+  uint32_t gx = (uint32_t)((slot_words / 2 + 4 * kBlock - 1) / (4 * kBlock));
+  if (gx > 256) gx = 256;
   if (gx == 0) gx = 1;
   k_pack<<<dim3(gx, nplanes), kBlock, 0, s>>>(slots, nplanes, slot_words, plane_bits, dst, word_off);
 }
