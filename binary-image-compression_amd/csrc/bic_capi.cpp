@@ -295,7 +295,13 @@ int bic_med_residual(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t r
   const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
   if ((rc = ensure_scratch(ctx, bic::chunk_scratch_bytes(g)))) return rc;
   const bic::ChunkScratch cs = bic::carve_chunk_scratch(ctx->scratch, g);
-  timed(ctx, "med_count", [&] { bic::launch_count(ctx->cur, g, planes, predict ? 1 : 0, cs, resid, weight_out); });
+  if (bic::med_rows_supported(g, planes, resid)) {
+    timed(ctx, "med_count", [&] {
+      bic::launch_med_rows(ctx->cur, g, planes, predict ? 1 : 0, resid, cs.ones, weight_out);
+    });
+  } else {
+    timed(ctx, "med_count", [&] { bic::launch_count(ctx->cur, g, planes, predict ? 1 : 0, cs, resid, weight_out); });
+  }
   BIC_HIP(hipGetLastError());
   return BIC_OK;
 }

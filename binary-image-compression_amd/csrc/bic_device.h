@@ -227,22 +227,23 @@ __device__ __forceinline__ uint64_t resid_word(RowCtx& rc, const Geom& g, uint32
 // (shifts distribute over XOR), one cross-lane shuffle per word.
 template <int WPL, bool PREDICT>
 __device__ __forceinline__ void resid_row(const uint64_t* planes, const Geom& g, uint32_t plane, uint32_t row,
-                                          uint64_t (&r)[WPL]) {
+                                          uint64_t (&r)[WPL], uint32_t c0 = 0) {
   const int lane = lane_id();
   const uint64_t* cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
   const uint64_t* up = row ? cur - g.wpr : cur;
   uint64_t p[WPL], u[WPL];
 #pragma unroll
   for (int t = 0; t < WPL; ++t) {
-    const uint32_t w = t * 64 + lane;
+    const uint32_t w = c0 + t * 64 + lane;
     const uint32_t wc = w < g.used ? w : g.used - 1;
     p[t] = cur[wc];
     if constexpr (PREDICT) u[t] = up[wc];
   }
-  uint64_t carry = 0;
+  uint64_t carry = 0;  // D of the word left of the chunk (chunks after the first of a row)
+  if (PREDICT && c0) carry = cur[c0 - 1] ^ (row ? up[c0 - 1] : 0);
 #pragma unroll
   for (int t = 0; t < WPL; ++t) {
-    const uint32_t w = t * 64 + lane;
+    const uint32_t w = c0 + t * 64 + lane;
     uint64_t d = p[t];
     if constexpr (PREDICT) {
       if (row) d ^= u[t];

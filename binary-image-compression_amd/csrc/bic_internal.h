@@ -48,6 +48,11 @@ void launch_bitplanes_u8(hipStream_t s, const uint8_t* gray, size_t pitch, uint3
 void launch_count(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
                   const ChunkScratch& cs, uint64_t* resid, uint64_t* weight_out);
 void launch_scan_rows(hipStream_t s, const Geom& g, const ChunkScratch& cs);
+// bic_med_residual for rows of <= 256 words: RPW rows per wave, 16-byte loads; part = one u32 per
+// wave (scratch, ceil(rows/8) per plane)
+bool med_rows_supported(const Geom& g, const void* planes, const void* resid);
+void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,
+                     uint32_t* part, uint64_t* weight_out);
 void launch_golomb_bits(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
                         const ChunkScratch& cs);
 void launch_golomb_offsets(hipStream_t s, const Geom& g, const ChunkScratch& cs, uint64_t* out,

@@ -101,20 +101,20 @@ void launch_bitplanes_u8(hipStream_t s, const uint8_t* gray, size_t pitch, uint3
 // ------------------------------------------------------------------------------------
 template <int WPL, bool PREDICT>
 __global__ __launch_bounds__(kBlock) void k_count(Geom g, const uint64_t* __restrict__ planes,
-                                                  ChunkScratch cs, uint64_t* __restrict__ resid,
-                                                  unsigned long long* __restrict__ weight_out) {
+                                                  ChunkScratch cs, uint64_t* __restrict__ resid) {
   const ChunkId ci = chunk_id(g);
   if (!ci.ok) return;  // whole wave uniform
   const uint32_t c0 = ci.c * g.wpc;
-  RowCtx rc = row_ctx(planes, g, ci.plane, ci.row, c0);
   const int lane = lane_id();
+  uint64_t rr[WPL];
+  resid_row<WPL, PREDICT>(planes, g, ci.plane, ci.row, rr, c0);
   uint32_t ones = 0;
   int last = -1, first = INT_MAX;
 #pragma unroll
   for (int t = 0; t < WPL; ++t) {
     const uint32_t w = c0 + t * 64 + lane;
-    const uint64_t r = resid_word<PREDICT>(rc, g, ci.row, w);
-    if (resid && w < g.wpr)
+    const uint64_t r = rr[t];
+    if (resid && w < g.wpr && w < c0 + g.wpc)
       resid[(uint64_t)ci.plane * g.plane_words + (uint64_t)ci.row * g.wpr + w] = r;
     ones += (uint32_t)__popcll(r);
     if (r) {
@@ -129,17 +129,124 @@ __global__ __launch_bounds__(kBlock) void k_count(Geom g, const uint64_t* __rest
     cs.ones[ci.id] = ones;
     cs.last[ci.id] = last;
     cs.first[ci.id] = first;
-    if (weight_out && ones) atomicAdd(&weight_out[ci.plane], (unsigned long long)ones);
   }
+}
+
+// per-plane weight (binmat.cpp:57-67) from the chunks' 1-counts: one workgroup per plane
+__global__ __launch_bounds__(1024) void k_plane_weight(const uint32_t* __restrict__ ones, uint64_t chunks_per_plane,
+                                                       uint64_t* weight_out) {
+  __shared__ uint64_t tmp[17];
+  const uint32_t* o = ones + (uint64_t)blockIdx.x * chunks_per_plane;
+  uint64_t a = 0;
+  for (uint64_t i = threadIdx.x; i < chunks_per_plane; i += 1024) a += o[i];
+  uint64_t tot;
+  block_excl_scan<uint64_t>(a, tmp, tot);
+  if (threadIdx.x == 0) weight_out[blockIdx.x] = tot;
+}
+
+// K2b: bic_med_residual for rows of up to 256 words (even row pitch, 16-byte aligned planes):
+// one wave walks RPW consecutive rows of a plane, keeping the row above in registers, with
+// 16-byte loads (lane l holds words 2l, 2l+1 of each 128-word half). Writes the residual if
+// asked and one 1-count per wave; k_plane_weight adds those up per plane.
+template <int NP, int RPW, bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_med_rows(Geom g, const uint64_t* __restrict__ planes,
+                                                     uint64_t* __restrict__ resid, uint32_t* __restrict__ part) {
+  const int lane = lane_id();
+  const uint32_t wpp = (g.rows + RPW - 1) / RPW;  // waves per plane
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  if (gw >= (uint64_t)wpp * g.nplanes) return;
+  const uint32_t plane = (uint32_t)(gw / wpp), r0 = (uint32_t)(gw % wpp) * RPW;
+  const uint64_t* pl = planes + (uint64_t)plane * g.plane_words;
+  uint64_t up0[NP], up1[NP];
+#pragma unroll
+  for (int t = 0; t < NP; ++t) {
+    up0[t] = up1[t] = 0;
+    if (PREDICT && r0) {
+      const uint32_t w = t * 128 + 2 * lane;
+      if (w < g.used) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(pl + (uint64_t)(r0 - 1) * g.wpr + w);
+        up0[t] = v.x;
+        up1[t] = v.y;
+      }
+    }
+  }
+  uint32_t ones = 0;
+  const uint32_t nr = min((uint32_t)RPW, g.rows - r0);
+  uint64_t p0[NP], p1[NP];  // current row; the next one is loaded before this one is used
+  auto load_row = [&](uint32_t row, uint64_t (&a)[NP], uint64_t (&b)[NP]) {
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const uint32_t w = t * 128 + 2 * lane;
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(pl + (uint64_t)row * g.wpr + (w < g.used ? w : 0));
+      a[t] = v.x;
+      b[t] = v.y;
+    }
+  };
+  load_row(r0, p0, p1);
+  for (uint32_t i = 0; i < nr; ++i) {
+    const uint32_t row = r0 + i;
+    uint64_t q0[NP], q1[NP];
+    if (i + 1 < nr) load_row(row + 1, q0, q1);
+    uint64_t carry = 0;
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const uint32_t w = t * 128 + 2 * lane;
+      uint64_t R0 = p0[t], R1 = p1[t];
+      if constexpr (PREDICT) {
+        const uint64_t D0 = p0[t] ^ up0[t], D1 = p1[t] ^ up1[t];
+        uint64_t Dl = shfl_up_u64(D1, 1);
+        if (lane == 0) Dl = carry;
+        carry = shfl_u64(D1, 63);
+        R0 = D0 ^ ((D0 >> 1) | (Dl << 63));
+        R1 = D1 ^ ((D1 >> 1) | (D0 << 63));
+        if (row == 0 && w == 0) R0 &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+        up0[t] = p0[t];
+        up1[t] = p1[t];
+      }
+      if (w >= g.used) R0 = 0;
+      if (w + 1 >= g.used) R1 = 0;
+      if (w == g.used - 1) R0 &= g.trail;
+      if (w + 1 == g.used - 1) R1 &= g.trail;
+      ones += (uint32_t)(__popcll(R0) + __popcll(R1));
+      if (resid && w < g.wpr) {
+        uint64_t* dst = resid + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr + w;
+        *reinterpret_cast<ulonglong2*>(dst) = make_ulonglong2(R0, R1);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      p0[t] = q0[t];
+      p1[t] = q1[t];
+    }
+  }
+  ones = wave_sum_u32(ones);
+  if (lane == 0) part[gw] = ones;
+}
+
+void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,
+                     uint32_t* part, uint64_t* weight_out) {
+  constexpr int RPW = 8;
+  const uint32_t wpp = (g.rows + RPW - 1) / RPW;
+  const uint32_t grid = (uint32_t)(((uint64_t)wpp * g.nplanes + kWaves - 1) / kWaves);
+#define BIC_MED(NP, P) k_med_rows<NP, RPW, P><<<grid, kBlock, 0, s>>>(g, planes, resid, part)
+  if (g.used <= 128) { if (predict) BIC_MED(1, true); else BIC_MED(1, false); }
+  else { if (predict) BIC_MED(2, true); else BIC_MED(2, false); }
+#undef BIC_MED
+  if (weight_out) k_plane_weight<<<g.nplanes, 1024, 0, s>>>(part, wpp, weight_out);
+}
+
+bool med_rows_supported(const Geom& g, const void* planes, const void* resid) {
+  return g.used <= 256 && (g.wpr % 2) == 0 && (reinterpret_cast<uintptr_t>(planes) % 16) == 0 &&
+         (reinterpret_cast<uintptr_t>(resid) % 16) == 0;
 }
 
 template <int WPL>
 static void launch_count_t(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
                            const ChunkScratch& cs, uint64_t* resid, uint64_t* weight_out) {
   const uint32_t grid = (uint32_t)((g.nchunks + kWaves - 1) / kWaves);
-  auto* wo = reinterpret_cast<unsigned long long*>(weight_out);
-  if (predict) k_count<WPL, true><<<grid, kBlock, 0, s>>>(g, planes, cs, resid, wo);
-  else k_count<WPL, false><<<grid, kBlock, 0, s>>>(g, planes, cs, resid, wo);
+  if (predict) k_count<WPL, true><<<grid, kBlock, 0, s>>>(g, planes, cs, resid);
+  else k_count<WPL, false><<<grid, kBlock, 0, s>>>(g, planes, cs, resid);
+  if (weight_out) k_plane_weight<<<g.nplanes, 1024, 0, s>>>(cs.ones, g.chunks_per_plane, weight_out);
 }
 
 void launch_count(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,

@@ -58,3 +58,38 @@ def shard_offsets(bits, device):
     rows = _allgather_i64([int(bits)], device)
     r = dist.get_rank()
     return sum(x[0] for x in rows[:r]), sum(x[0] for x in rows)
+
+
+def merge_bit_streams(parts, bit_offsets, total_bits, device):
+    """parts[r]: int64 words of rank r's stream, written at bit alignment bit_offsets[r] % 64 so its
+    word 0 is global word bit_offsets[r] // 64. A word two neighbours share is the OR of both."""
+    out = torch.zeros((int(total_bits) + 63) // 64, dtype=torch.int64, device=device)
+    for p, b0 in zip(parts, bit_offsets):
+        w0 = int(b0) // 64
+        n = min(p.numel(), out.numel() - w0)
+        if n > 0:
+            out[w0:w0 + n] |= p[:n]
+    return out
+
+
+def sharded_golomb(encode, count, total, device, dst=0):
+    """One adaptive Golomb coder over a sample sequence split across the ranks in rank order
+    (C5: each rank holds a band of tile rows). encode(n0, a0, bit0) -> (words, bits) codes this
+    rank's samples from coder state (n0 samples, accumulated error a0) with its first codeword at
+    bit bit0 of words[0]. Exchanges: all-gather of (count, total), all-gather of the bit lengths,
+    point-to-point gather of the words. Returns (words, total_bits) on `dst`, (None, total_bits)
+    elsewhere."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n0, a0 = shard_state(count, total, device)
+    words, bits = encode(n0, a0, 0)
+    lens = [x[0] for x in _allgather_i64([int(bits)], device)]
+    b0s = [sum(lens[:r]) for r in range(world)]
+    total_bits = sum(lens)
+    if b0s[rank] % 64:
+        words, _ = encode(n0, a0, b0s[rank] % 64)
+    nwords = (b0s[rank] % 64 + int(bits) + 63) // 64
+    gathered, offs = gather_streams(words, nwords, world, rank, dst)
+    if rank != dst:
+        return None, total_bits
+    parts = [gathered[offs[r]:offs[r + 1]] for r in range(world)]
+    return merge_bit_streams(parts, b0s, total_bits, device), total_bits
