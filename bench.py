@@ -50,10 +50,18 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BIC_BENCH_BACKEND=gloo rehearses the N-rank path with several ranks on one GPU (functional
+    # check only); the real run is one rank per GPU over RCCL (backend "nccl")
+    backend = os.environ.get("BIC_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -280,41 +288,65 @@ class C4(C3):
 
 
 class C5(C3):
-    """8192x8192 plane, 32x32 tiles (compress7 R = 0 path): weights, mode, Golomb over tiles."""
+    """8192x8192 plane, 32x32 tiles (compress7 R = 0 path): weights, mode, Golomb over tiles. On N
+    GPUs the plane is split into bands of tile rows (strong scaling); the one adaptive coder over the
+    tile sequence is continued across ranks by exchanging its state and bit offsets
+    (pybic.parallel.sharded_golomb) and the stream is reassembled on rank 0."""
 
-    def __init__(self, ctx, args, rank):
+    def __init__(self, ctx, args, rank, world=1):
         import pybic
         t = ctx.torch
-        self.ctx, self.pybic = ctx, pybic
+        self.ctx, self.pybic, self.rank, self.world = ctx, pybic, rank, world
         self.rows = args.rows or 8192
         self.cols = args.cols or 8192
         self.W = 32
         self.nplanes = 1
         self.wpr = (self.cols + 63) // 64
+        ny = self.rows // self.W
+        lo, hi = rank * ny // world, (rank + 1) * ny // world
+        self.band_rows = (hi - lo) * self.W
         g = t.Generator(device=ctx.dev)
         g.manual_seed(0x5EED0000 + rank)
-        self.planes = rand_words(t, (1, self.rows, self.wpr), ctx.dev, g)
+        self.planes = rand_words(t, (1, self.band_rows, self.wpr), ctx.dev, g)
         self.lt = pybic.lentab(self.W)
         self.res = None
+        self.own_bits = 0
+        self.merged = None
         self.k = 0
-        self.pixels = self.rows * self.cols
+        self.pixels = self.band_rows * self.cols
         self.bits_e = ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
-        self.workload = f"c5: {self.rows}x{self.cols} plane, 32x32 tiles, per-tile med/mode + Golomb over weights"
+        self.workload = (f"c5: {self.rows}x{self.cols} plane, 32x32 tiles, per-tile med/mode + Golomb over weights"
+                         + (f", tile-row bands over {world} GPUs" if world > 1 else ""))
 
     def step(self):
-        self.res = self.ctx.patch_encode(self.planes[0], self.cols, self.W, self.lt, want_resid=True)
+        c = self.ctx
+        self.res = c.patch_encode(self.planes[0], self.cols, self.W, self.lt, want_resid=True)
+        if self.world > 1:
+            from pybic.parallel import sharded_golomb
+            wts = self.res["weights"]
+            total = int(self.pybic.as_u64(self.res["stats"])[1])
+
+            def enc(n0, a0, bit0):
+                out, bits = c.golomb_encode_samples(wts, n0=n0, a0=a0, bit0=bit0)
+                nb = int(self.pybic.as_u64(bits)[0])
+                self.own_bits = nb
+                return out, nb
+            self.merged, _ = sharded_golomb(enc, wts.numel(), total, c.dev)
         self.k += 1
 
     def out_bytes(self):
+        if self.world > 1:
+            return self.own_bits / 8.0
         return int(self.pybic.as_u64(self.res["stats"])[0]) / 8.0
 
     def kernel_bytes(self):
-        return {"tiles": 2 * self.rows * self.wpr * 8}
+        return {"tiles": 2 * self.band_rows * self.wpr * 8}
 
     def check(self, oracle):
         P = self.pybic.as_u64(self.planes[0])
         exp = oracle.patch_encode(P, self.cols, self.W, self.lt, want_stream=True)
         st = self.pybic.as_u64(self.res["stats"])
+        # on N > 1 ranks this checks rank 0's band (its tiles, L and its own fresh-state stream)
         return int(st[0]) == exp["bits"] and int(st[2]) == exp["L"]
 
 
@@ -369,7 +401,7 @@ def main():
     elif args.workload == "c4":
         wl = C4(ctx, args, rank, world)
     else:
-        wl = C5(ctx, args, rank)
+        wl = C5(ctx, args, rank, world)
     dev = ctx.dev
     for _ in range(args.warmup):
         wl.step()
@@ -414,11 +446,12 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong" if args.workload == "c4" else "weak", "vs_baseline": None, "dtype": "u64",
+            "scaling": "strong" if args.workload in ("c4", "c5") else "weak", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (seeded uniform bytes / Bernoulli(0.5) words, device-resident)",
             "config": {"workload": wl.workload, "rows": wl.rows, "cols": wl.cols, "planes_per_gpu": wl.nplanes,
-                       "parallelism": f"dp{world} (independent images per GPU)" if args.workload != "c4"
-                       else f"dp{world} (64 frames sharded)"},
+                       "parallelism": {"c4": f"dp{world} (64 frames sharded)",
+                                       "c5": f"dp{world} (tile-row bands, coder state exchanged)"}.get(
+                                           args.workload, f"dp{world} (independent images per GPU)")},
             "mb_per_s_out": round(out_all / dt_max / 1e6, 1),
             "gray_mpix_per_s": round(value / 8, 1) if args.workload == "c3" else None,
             "roofline": roof, "predictor_pass": pred_pass, "kernels": per_kernel,

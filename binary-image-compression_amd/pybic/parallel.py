@@ -12,8 +12,13 @@ import torch
 import torch.distributed as dist
 
 
+def _host_only():
+    """gloo (CPU tests, one-GPU rehearsals) moves host tensors only"""
+    return dist.get_backend() == "gloo"
+
+
 def _allgather_i64(vals, device):
-    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    t = torch.tensor(vals, dtype=torch.int64, device="cpu" if _host_only() else device)
     outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(outs, t)
     return [o.tolist() for o in outs]
@@ -27,6 +32,9 @@ def gather_streams(packed, nwords, world=None, rank=None, dst=0):
     rank = dist.get_rank() if rank is None else rank
     n = int(nwords.reshape(-1)[0].item()) if torch.is_tensor(nwords) else int(nwords)
     sizes = [s[0] for s in _allgather_i64([n], packed.device)]
+    dev = packed.device
+    if _host_only():
+        packed = packed.cpu()
     if rank == dst:
         offs = [0]
         for s in sizes:
@@ -36,7 +44,7 @@ def gather_streams(packed, nwords, world=None, rank=None, dst=0):
         ops = [dist.P2POp(dist.irecv, out[offs[r]:offs[r + 1]], r) for r in range(world) if r != dst and sizes[r]]
         for req in (dist.batch_isend_irecv(ops) if ops else []):
             req.wait()
-        return out, offs
+        return out.to(dev), offs
     if n:
         for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed[:n].contiguous(), dst)]):
             req.wait()
