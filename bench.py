@@ -100,7 +100,11 @@ def load_pmc(workload, kernel):
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        for sec in ("timers", "kernels"):
+            v = d.get(sec, {}).get(kernel, {}).get("hbm_bytes_per_launch")
+            if v is not None:
+                return v
+        return None
     except (OSError, ValueError):
         return None
 

@@ -53,6 +53,23 @@ def main():
         res["kernels"][k] = {"calls": s["calls"], "avg_us": round(s["total_ns"] / s["calls"] / 1e3, 2),
                              "fetch_kib": fk, "write_kib": wk,
                              "hbm_bytes_per_launch": int(hbm) if hbm is not None else None}
+    # bench.py times launch sequences (bic_prof_* names); their HBM bytes per launch are the sums
+    # over the kernels each sequence runs, per launch of its main kernel
+    timers = {"encode_rows_golomb_eg": ["k_encode_rows", "k_rows_global", "k_fixup"],
+              "encode_rows_golomb": ["k_encode_rows", "k_rows_global", "k_fixup"],
+              "encode_rows_eg": ["k_encode_rows", "k_fixup"],
+              "bitplanes_u8": ["k_bitplanes_u8"], "med_count": ["k_med_rows", "k_count", "k_plane_weight"],
+              "tiles": ["k_tiles_aligned", "k_tiles"], "golomb_samples": ["k_samp_scan", "k_samp_emit"],
+              "pack": ["k_pack"]}
+    res["timers"] = {}
+    K = res["kernels"]
+    for t, ks in timers.items():
+        present = [k for k in ks if k in K and K[k]["hbm_bytes_per_launch"] is not None]
+        if not present:
+            continue
+        launches = K[present[0]]["calls"]
+        tot = sum(K[k]["hbm_bytes_per_launch"] * K[k]["calls"] for k in present)
+        res["timers"][t] = {"kernels": present, "launches": launches, "hbm_bytes_per_launch": int(tot / launches)}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     for k, v in res["kernels"].items():
