@@ -333,10 +333,15 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
     // one pass: residual -> runs -> both streams (bic_fused.hip)
     if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
     const bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
-    timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg", [&] {
+    auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
-                        bits_eg, ctx->flags, !ctx->two_pass);
-    });
+                        bits_eg, ctx->flags, !ctx->two_pass, st);
+    };
+    stage(bic::kFusedPrep);
+    // the row kernel alone is timed under the encoder's name (bench.py's roofline kernel)
+    timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
+          [&] { stage(bic::kFusedRows); });
+    timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
     BIC_HIP(hipGetLastError());
     return BIC_OK;
   }

@@ -342,6 +342,8 @@ struct FusedArgs {
   uint64_t *gboff, *glen, *gfrag, *gslow;
   uint64_t *eboff, *elen, *efrag;
   uint32_t* row_o;     // two-pass encoder: ones of the plane before each row
+  uint32_t* slow_n;    // number of rows k_rows_global must write (zeroed per launch)
+  uint64_t* slow_ids;  // their row ids
   uint64_t* out_g;
   uint64_t slot_g;
   uint64_t* bits_g;
@@ -396,18 +398,14 @@ __device__ __forceinline__ uint64_t img_resid(const uint32_t* eimg, const Geom& 
 }
 
 // Rows whose Golomb output exceeds the LDS window (a long dense stretch at large k): the main
-// kernel records their offset and sample base; this kernel (one wave per row, idle waves exit
-// at once) recomputes the row and writes it straight to global memory -- its inner words are
-// zeroed and OR'd, the bits landing in its first/last (shared) word go to the fragment table.
+// kernel records their offset and sample base and appends them to a list; k_rows_global (a small
+// grid walking that list, one wave per row) recomputes each and writes it straight to global
+// memory -- its inner words are zeroed and OR'd, the bits landing in its first/last (shared) word
+// go to the fragment table.
 template <bool PREDICT>
-__global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
+__device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int lane) {
   const Geom& g = a.g;
-  const int lane = lane_id();
-  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  if (id >= nrows) return;
   const uint64_t slow = a.gslow[id];
-  if (!slow) return;
   const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
   const uint64_t G = a.gboff[id], L = a.glen[id];
   uint64_t* frag = a.gfrag + 2 * id;
@@ -429,8 +427,8 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
     int jp;
     step_prefix(x, w, st, n, jp);
     const bool eol = w == g.used - 1;
-    const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols,
-                                  ByteTables{reinterpret_cast<const uint32_t*>(a.lut + 256), a.lut});
+    const LaneEnc e = encode_word<false>(x, w, n, jp, arow, eol, g.cols,
+                                         ByteTables{reinterpret_cast<const uint32_t*>(a.lut + 256), a.lut});
     const uint32_t inc = wave_incl_sum_u32(e.len);
     const uint64_t off = carry + inc - e.len;
     carry += __shfl(inc, 63);
@@ -447,6 +445,14 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
     if (hpart) frag[0] = h | (wh == wt ? tl : 0);
     if (tpart && wt != wh) frag[1] = tl;
   }
+}
+
+template <bool PREDICT>
+__global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
+  const int lane = lane_id();
+  const uint32_t nslow = *a.slow_n;
+  for (uint32_t li = blockIdx.x * 4 + (threadIdx.x >> 6); li < nslow; li += gridDim.x * 4)
+    row_global<PREDICT>(a, a.slow_ids[li], lane);
 }
 
 // One workgroup = one TILE of kTileRows consecutive rows of one plane (one wave per row). Tiles
@@ -649,6 +655,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
           a.gboff[id] = G;
           a.glen[id] = L;
           a.gslow[id] = fits ? 0 : O + row + 1;  // k_rows_global writes the row
+          if (!fits) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
         }
       } else if (lane == 0) {
         a.gboff[id] = G;
@@ -779,6 +786,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
       if (Grel + L <= cap) {
         a.glen[id] = L;
         a.gslow[id] = step_max > kIterCap ? O + row + 1 : 0;  // k_rows_global writes such rows
+        if (step_max > kIterCap) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
       } else {
         a.glen[id] = 0;
         a.gslow[id] = 0;
@@ -946,8 +954,17 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
 // owns it and ORs in the head fragments of the following rows that start inside that word.
 __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff, const uint64_t* __restrict__ len,
                                                const uint64_t* __restrict__ frag, uint64_t* __restrict__ out,
-                                               uint32_t rows, uint64_t nrows) {
-  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+                                               const uint64_t* __restrict__ boff2, const uint64_t* __restrict__ len2,
+                                               const uint64_t* __restrict__ frag2, uint64_t* __restrict__ out2,
+                                               uint32_t rows, uint64_t nrows, uint32_t second) {
+  // blocks [second, ...) serve the second stream (EG) when both streams are written
+  if (blockIdx.x >= second) {
+    boff = boff2;
+    len = len2;
+    frag = frag2;
+    out = out2;
+  }
+  const uint64_t id = (uint64_t)(blockIdx.x >= second ? blockIdx.x - second : blockIdx.x) * 256 + threadIdx.x;
   if (id >= nrows) return;
   const uint64_t G = boff[id], L = len[id];
   if (L == 0) return;
@@ -967,7 +984,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 9 + n * 4 + 1024;
+  return 256 + n * 8 * 2 + n * 8 * 10 + n * 4 + 1024;
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -986,7 +1003,9 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
   fs.eboff = q; q += n;
   fs.elen = q; q += n;
   fs.efrag = q; q += 2 * n;
+  fs.slow_ids = q; q += n;
   fs.row_o = reinterpret_cast<uint32_t*>(q);
+  fs.slow_n = fs.counter + 1;  // zeroed with the counter
   return fs;
 }
 
@@ -1001,10 +1020,14 @@ int read_stamps(uint64_t* host, size_t n) {
 void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
                   const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
-                  uint64_t* bits_e, uint32_t* flags, bool single_pass) {
-  (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
+                  uint64_t* bits_e, uint32_t* flags, bool single_pass, int stage) {
+  if (stage == kFusedPrep) {
+    (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
+    return;
+  }
   FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
-              fs.eboff, fs.elen, fs.efrag, fs.row_o, out_g, slot_g, bits_g, out_e, slot_e, bits_e, flags};
+              fs.eboff, fs.elen, fs.efrag, fs.row_o, fs.slow_n, fs.slow_ids, out_g, slot_g, bits_g, out_e, slot_e,
+              bits_e, flags};
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
 #endif
@@ -1012,6 +1035,18 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   const uint32_t grid = (uint32_t)((g.rows + kTileRows - 1) / kTileRows * (uint64_t)g.nplanes);  // one per tile
   const uint32_t egrid = (uint32_t)((nrows + kTileRows - 1) / kTileRows);                       // one per 8 rows
   const bool dg = out_g != nullptr, de = out_e != nullptr;
+  const uint32_t fgrid = (uint32_t)((nrows + 255) / 256);
+  if (stage == kFusedFinish) {
+    if (dg) {  // a fixed small grid walks the list of LDS-overflow rows (usually empty)
+      if (predict) k_rows_global<true><<<256, 256, 0, s>>>(a);
+      else k_rows_global<false><<<256, 256, 0, s>>>(a);
+    }
+    k_fixup<<<dg && de ? 2 * fgrid : fgrid, 256, 0, s>>>(dg ? fs.gboff : fs.eboff, dg ? fs.glen : fs.elen,
+                                                        dg ? fs.gfrag : fs.efrag, dg ? out_g : out_e,
+                                                        fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows,
+                                                        dg && de ? fgrid : 0xffffffffu);
+    return;
+  }
   const dim3 blk(64 * kTileRows);
 #define BIC_PASSES(W, P, DG, DE)                                                        \
   if (single_pass) {                                                                    \
@@ -1032,14 +1067,6 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   }
 #undef BIC_CODERS
 #undef BIC_PASSES
-  const uint32_t fgrid = (uint32_t)((nrows + 255) / 256);
-  if (dg) {
-    const uint32_t rgrid = (uint32_t)((nrows + 3) / 4);
-    if (predict) k_rows_global<true><<<rgrid, 256, 0, s>>>(a);
-    else k_rows_global<false><<<rgrid, 256, 0, s>>>(a);
-  }
-  if (dg) k_fixup<<<fgrid, 256, 0, s>>>(fs.gboff, fs.glen, fs.gfrag, out_g, g.rows, nrows);
-  if (de) k_fixup<<<fgrid, 256, 0, s>>>(fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows);
 }
 
 }  // namespace bic

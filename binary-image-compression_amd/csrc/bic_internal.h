@@ -91,6 +91,8 @@ struct FusedScratch {
   size_t zero_bytes;  // counter + records, zeroed per launch
   uint64_t *gboff, *glen, *gfrag, *gslow, *eboff, *elen, *efrag;
   uint32_t* row_o;
+  uint32_t* slow_n;
+  uint64_t* slow_ids;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
@@ -101,7 +103,10 @@ void build_byte_lut(uint64_t* lut);
 void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
                   const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
-                  uint64_t* bits_e, uint32_t* flags, bool single_pass);
+                  uint64_t* bits_e, uint32_t* flags, bool single_pass, int stage);
+// launch_fused stages: zero the tickets and records; the row kernel(s); the LDS-overflow rows and
+// the words adjacent rows share
+constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2;
 
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
