@@ -17,9 +17,10 @@
 namespace bic {
 
 // ------------------------------------------------------------------------------------
-// K1: bitplanes (bitplane_tool.cpp:24-30). 4 lanes build one 64-pixel word: each lane
-// loads 16 pixels (one 16-byte load), an 8x8 bit transpose turns 8 pixels into one byte
-// per plane (MSB = leftmost pixel), and the 4 x 16-bit pieces meet in LDS.
+// K1: bitplanes (bitplane_tool.cpp:24-30). Lane l of a wave owns output word l of a row: it
+// loads its 64 pixels (four 16-byte loads), turns each group of 8 pixels into one byte per plane
+// with an 8x8 bit transpose (MSB = leftmost pixel) and stores one 64-bit word per plane; 64 lanes
+// store 512 contiguous bytes of each plane row. No LDS, no barrier.
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t transpose8x8(uint64_t x) {
   uint64_t t;
@@ -37,57 +38,51 @@ __global__ __launch_bounds__(kBlock) void k_bitplanes_u8(const uint8_t* __restri
                                                          uint32_t rows, uint32_t cols, uint32_t used,
                                                          int nplanes, uint64_t* __restrict__ planes,
                                                          uint32_t wpr) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][8][16][4];
-  const uint64_t total = (uint64_t)rows * used * 4;
-  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, grp = lane >> 2, sub = lane & 3;
-  uint64_t tl = 0, th = 0;
-  if (tid < total) {
-    const uint64_t widx = tid >> 2;
-    const uint32_t row = (uint32_t)(widx / used), w = (uint32_t)(widx % used);
-    const uint32_t j0 = w * 64 + sub * 16;
-    const uint8_t* src = gray + (uint64_t)row * pitch + j0;
-    uint64_t lo = 0, hi = 0;
-    if (VEC && j0 + 16 <= cols) {
-      const uint4 v = *reinterpret_cast<const uint4*>(src);
-      lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
-      hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
-    } else {
+  const uint32_t groups = (used + 63) / 64;  // 64-word groups per row
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (gw >= (uint64_t)rows * groups) return;
+  const uint32_t row = (uint32_t)(gw / groups), w = (uint32_t)(gw % groups) * 64 + lane_id();
+  if (w >= used) return;
+  const uint8_t* src = gray + (uint64_t)row * pitch + (uint64_t)w * 64;
+  uint64_t px[8];  // 8 groups of 8 pixels, little-endian bytes
+  if (VEC && (uint64_t)w * 64 + 64 <= cols) {
 #pragma unroll
-      for (int x = 0; x < 16; ++x) {
-        const uint64_t px = (j0 + x < cols) ? (uint64_t)src[x] : 0;
-        if (x < 8) lo |= px << (8 * x);
-        else hi |= px << (8 * (x - 8));
+    for (int i = 0; i < 4; ++i) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * i);
+      px[2 * i] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      px[2 * i + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+  } else {
+#pragma unroll
+    for (int g8 = 0; g8 < 8; ++g8) {
+      uint64_t v = 0;
+      for (int x = 0; x < 8; ++x) {
+        const uint32_t j = w * 64 + g8 * 8 + x;
+        if (j < cols) v |= (uint64_t)src[g8 * 8 + x] << (8 * x);
       }
+      px[g8] = v;
     }
-    tl = transpose8x8(bswap64(lo));
-    th = transpose8x8(bswap64(hi));
   }
+  uint64_t T[8];
 #pragma unroll
-  for (int b = 0; b < 8; ++b)
-    lds[wave][b][grp][3 - sub] = (uint16_t)((((tl >> (8 * b)) & 0xff) << 8) | ((th >> (8 * b)) & 0xff));
-  __syncthreads();
-  const int b = lane >> 3;
+  for (int g8 = 0; g8 < 8; ++g8) T[g8] = transpose8x8(bswap64(px[g8]));  // byte b = plane b's 8 bits
   const uint64_t plane_words = (uint64_t)rows * wpr;
+  uint64_t* dst = planes + (uint64_t)row * wpr + w;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int g2 = (lane & 7) * 2 + h;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kBlock + wave * 64 + g2 * 4;
-    if (b < nplanes && t0 < total) {
-      const uint64_t wi = t0 >> 2;
-      const uint32_t row = (uint32_t)(wi / used), w = (uint32_t)(wi % used);
-      uint64_t v;
-      __builtin_memcpy(&v, &lds[wave][b][g2][0], sizeof(v));  // (no type-punned load)
-      planes[b * plane_words + (uint64_t)row * wpr + w] = v;
-    }
+  for (int b = 0; b < 8; ++b) {
+    if (b >= nplanes) break;
+    uint64_t v = 0;
+#pragma unroll
+    for (int g8 = 0; g8 < 8; ++g8) v |= ((T[g8] >> (8 * b)) & 0xffull) << (56 - 8 * g8);
+    dst[b * plane_words] = v;
   }
 }
 
 void launch_bitplanes_u8(hipStream_t s, const uint8_t* gray, size_t pitch, uint32_t rows,
                          uint32_t cols, int nplanes, uint64_t* planes, uint32_t wpr) {
   const uint32_t used = (cols + 63) / 64;
-  const uint64_t total = (uint64_t)rows * used * 4;
-  const uint32_t grid = (uint32_t)((total + kBlock - 1) / kBlock);
+  const uint64_t waves = (uint64_t)rows * ((used + 63) / 64);
+  const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
   const bool vec = (pitch % 16 == 0) && (((uintptr_t)gray) % 16 == 0);
   if (vec)
     k_bitplanes_u8<true><<<grid, kBlock, 0, s>>>(gray, pitch, rows, cols, used, nplanes, planes, wpr);
