@@ -459,6 +459,28 @@ int bic_pack_streams(bic_ctx* ctx, const uint64_t* slots, int nplanes, size_t sl
   return BIC_OK;
 }
 
+int bic_pbm_unpack(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, uint64_t* plane, size_t wpr) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!geom_ok(rows, cols, wpr) || (rows && (!raster || !plane))) return BIC_EINVAL;
+  timed(ctx, "pbm_unpack", [&] {
+    bic::launch_pbm(ctx->cur, false, raster, nullptr, nullptr, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_pbm_pack(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, uint8_t* raster) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!geom_ok(rows, cols, wpr) || (rows && (!raster || !plane))) return BIC_EINVAL;
+  timed(ctx, "pbm_pack", [&] {
+    bic::launch_pbm(ctx->cur, true, nullptr, raster, plane, nullptr, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
 // log2 C(n, r): the reference's enumL / enumerative_codelength (coding.cpp:19-22,
 // compress7_test.cpp:25-28) without GSL. Exact at r in {0, n} (0) and, for power-of-two n,
 // at r in {1, n-1} (log2 n -- where GSL's last-ulp rounding is unpinned, SURVEY.md §8 c);

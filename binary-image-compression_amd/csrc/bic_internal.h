@@ -108,6 +108,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
 // the words adjacent rows share
 constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2;
 
+void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* raster_out, const uint64_t* plane_in,
+                uint64_t* plane_out, uint32_t rows, uint32_t cols, uint32_t wpr);
+
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
 

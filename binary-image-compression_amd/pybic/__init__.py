@@ -25,7 +25,7 @@ EXPORTS = [
     "bic_strerror", "bic_device_count", "bic_reserve", "bic_bitplanes_u8", "bic_med_residual",
     "bic_encode_planes", "bic_encode_planes2", "bic_ctx_set_option", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
-    "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset",
+    "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
 ]
 
 
@@ -81,6 +81,13 @@ def load(path=LIB_PATH):
     sig("bic_prof_collect", i32, [vp, C.c_char_p, sz])
     sig("bic_enum_codelength", C.c_double, [u32, u32])
     sig("bic_tile_lentab", i32, [u32, vp])
+    sig("bic_malloc", i32, [vp, sz, C.POINTER(vp)])
+    sig("bic_free", i32, [vp, vp])
+    sig("bic_memcpy_h2d", i32, [vp, vp, vp, sz])
+    sig("bic_memcpy_d2h", i32, [vp, vp, vp, sz])
+    sig("bic_memset", i32, [vp, vp, i32, sz])
+    sig("bic_pbm_unpack", i32, [vp, vp, sz, sz, vp, sz])
+    sig("bic_pbm_pack", i32, [vp, vp, sz, sz, sz, vp])
     _lib = L
     return L
 
@@ -275,6 +282,22 @@ class Context:
                                             cap_words, _p(stats)), "bic_patch_encode")
         return dict(weights=weights, w_nonpred=wo, w_pred=wO, modes=modes, resid=resid, stream=stream,
                     stats=stats)
+
+    def pbm_unpack(self, raster, rows, cols, wpr=None):
+        """P4 raster bytes (uint8 device tensor, rows x ceil(cols/8)) -> int64 plane [rows, wpr]."""
+        wpr = wpr or (cols + 63) // 64
+        plane = self.empty_i64(rows, wpr)
+        self._bind_stream()
+        self._chk(self.lib.bic_pbm_unpack(self.h, _p(raster), rows, cols, _p(plane), wpr), "bic_pbm_unpack")
+        return plane
+
+    def pbm_pack(self, plane, cols):
+        """int64 plane [rows, wpr] -> P4 raster bytes (uint8 device tensor)."""
+        rows, wpr = plane.shape
+        raster = self.torch.empty(rows * ((cols + 7) // 8), dtype=self.torch.uint8, device=self.dev)
+        self._bind_stream()
+        self._chk(self.lib.bic_pbm_pack(self.h, _p(plane), rows, cols, wpr, _p(raster)), "bic_pbm_pack")
+        return raster
 
     def pack_streams(self, slots, plane_bits, dst_words=None):
         n, slot_words = slots.shape

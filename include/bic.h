@@ -145,6 +145,13 @@ int bic_tile_lentab(unsigned W, uint64_t* lentab);
 int bic_pack_streams(bic_ctx* ctx, const uint64_t* slots, int nplanes, size_t slot_words,
                      const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
 
+/* ---- PBM (P4) rasters on the device (pbm.cpp:29-77) ------------------------------------------
+ * A P4 raster is rows x ceil(cols/8) bytes, MSB = leftmost pixel, rows byte-aligned (device
+ * memory, no header). unpack: raster -> planes (rows x wpr words; pad bits 0); pack: planes ->
+ * raster (pad bits of the last byte of a row 0), as read_pbm_data / write_pbm do bit by bit. */
+int bic_pbm_unpack(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, uint64_t* plane, size_t wpr);
+int bic_pbm_pack(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, uint8_t* raster);
+
 /* ---- kernel timing ------------------------------------------------------------------------
  * When enabled, every kernel launch of this ctx is bracketed by HIP events on the launch stream.
  * bic_prof_collect syncs, writes one line per kernel name ("name launches total_ms\n") into buf

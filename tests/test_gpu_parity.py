@@ -279,3 +279,17 @@ def test_pack_streams(ctx, oracle):
         nw = (eb + 63) // 64
         assert O[k + 1] - O[k] == nw
         assert D[O[k]:O[k] + nw].tobytes() == est.tobytes()
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (3, 7), (5, 64), (9, 65), (37, 70), (20, 1000), (4, 16384)])
+def test_pbm_raster_pack_unpack(ctx, oracle, rows, cols):
+    """device P4 rasters (pbm.cpp:29-77) against the host writer, both directions"""
+    from pnm_io import plane_to_p4_rows
+    P = oracle.gen_plane(rows * 7 + cols, 0.4, rows, cols)
+    raster = plane_to_p4_rows(P, cols)
+    d = ctx.torch.from_numpy(raster.reshape(-1).copy()).to(ctx.dev)
+    back = ctx.pbm_unpack(d, rows, cols)
+    ras2 = ctx.pbm_pack(ctx.to_dev(P), cols)
+    ctx.sync()
+    assert np.array_equal(as_u64(back), mask_pixels(P, cols))
+    assert ras2.cpu().numpy().tobytes() == raster.tobytes()
