@@ -52,12 +52,12 @@ for i, nm in enumerate(names):
 # where the time goes: per-phase percentiles, by wave slot in the tile and by claim order
 ids = np.nonzero(ok)[0]
 plane, row = ids // rows, ids % rows
-wave = row % 8
-claim = (row // 8) * nplanes + plane
+wave = row % 16
+claim = (row // 16) * nplanes + plane
 gol = d[:, 3]
 for nm, i in (("load", 0), ("eg", 2), ("golomb", 3), ("write", 5)):
     print(nm, "p10/p50/p90/p99:", np.percentile(d[:, i], [10, 50, 90, 99]).astype(int))
-print("golomb mean by wave slot:", [int(gol[wave == q].mean()) for q in range(8)])
+print("golomb mean by wave slot:", [int(gol[wave == q].mean()) for q in range(16)])
 nb = 8
 edges = np.linspace(0, claim.max() + 1, nb + 1)
 print("golomb mean by claim-order octile:", [int(gol[(claim >= edges[q]) & (claim < edges[q + 1])].mean()) for q in range(nb)])

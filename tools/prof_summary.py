@@ -55,9 +55,10 @@ def main():
                              "hbm_bytes_per_launch": int(hbm) if hbm is not None else None}
     # bench.py times launch sequences (bic_prof_* names); their HBM bytes per launch are the sums
     # over the kernels each sequence runs, per launch of its main kernel
-    timers = {"encode_rows_golomb_eg": ["k_encode_rows", "k_rows_global", "k_fixup"],
-              "encode_rows_golomb": ["k_encode_rows", "k_rows_global", "k_fixup"],
-              "encode_rows_eg": ["k_encode_rows", "k_fixup"],
+    timers = {"encode_rows_golomb_eg": ["k_encode_rows", "k_len_rows", "k_emit_rows"],
+              "encode_rows_golomb": ["k_encode_rows", "k_len_rows", "k_emit_rows"],
+              "encode_rows_eg": ["k_encode_rows", "k_len_rows", "k_emit_rows"],
+              "encode_finish": ["k_rows_global", "k_fixup"],
               "bitplanes_u8": ["k_bitplanes_u8"], "med_count": ["k_med_rows", "k_count", "k_plane_weight"],
               "tiles": ["k_tiles_aligned", "k_tiles"], "golomb_samples": ["k_samp_scan", "k_samp_emit"],
               "pack": ["k_pack"]}
