@@ -1,20 +1,23 @@
-// bic_fused.hip -- single-pass row encoder for rows of up to 256 words (16384 columns):
-// med residual -> per-row runs -> Golomb stream and/or EG stream, one wavefront per row.
+// bic_fused.hip -- row encoders for rows of up to 256 words (16384 columns): med residual ->
+// per-row runs -> Golomb stream and/or EG stream, one wavefront per row, 16-row tiles.
 //
 // Semantics are those of bic_kernels.hip (GolombCoder.cpp:13-34, eg.cpp:20-37, pred.cpp:3-15);
-// the difference is the schedule:
-//  * rows are claimed in order through an atomic counter, so every row a wave looks back at
-//    was claimed earlier and is resident or finished (no deadlock);
-//  * the row's 1-count is published at once and a decoupled look-back over the earlier rows
-//    of the plane yields the number of samples before the row (the Golomb coder state);
+// the difference is the schedule. The default single kernel (k_encode_rows):
+//  * tiles are claimed in order through an atomic ticket, so every tile a workgroup looks back
+//    at was claimed earlier and is running or finished (no deadlock, whatever the dispatch order);
+//  * the tile's 1-count is published at once and a decoupled look-back over the earlier tiles
+//    of the plane yields the number of samples before each row (the Golomb coder state);
 //  * every codeword is computed ONCE: each lane turns its word into a register string
 //    (first codeword's binary part, its unary zeros, then <= 128 bits), or -- when the k
 //    bounds prove k = 0 for every codeword of the word -- copies the word's bits (a k = 0
-//    codeword is exactly the run's zeros and its 1);
-//  * lane strings are OR'd into an LDS row image; the row's bit length is published and a
+//    codeword is exactly the run's zeros and its 1); constant k = 1..3 words go byte by byte
+//    through precomputed tables;
+//  * lane strings are OR'd into an LDS row image; the tile's bit length is published and a
 //    second look-back gives its offset; whole 64-bit words go to HBM with plain stores and
 //    the (at most two) words shared with neighbouring rows go to a fragment table that the
 //    fixup kernel combines (no atomics on the output, no pre-zeroing of the output).
+// The two-pass option (k_len_rows, k_emit_rows) computes lengths and offsets first and then
+// writes every row independently; same output, slower.
 // Inter-workgroup records are 8-byte {flag, value} granules written and polled with
 // agent-scope atomics (cdna_hip_programming.md §6 Guideline 16, R2), spins bounded.
 #include "bic_device.h"
