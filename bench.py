@@ -32,7 +32,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--rows", type=int, default=0, help="override image rows (c3/c2/c5)")
     ap.add_argument("--cols", type=int, default=0, help="override image cols")
     ap.add_argument("--cpu-rows", type=int, default=16384, help="rows per plane in the CPU baseline sample")
@@ -354,12 +354,84 @@ class C5(C3):
         return int(st[0]) == exp["bits"] and int(st[2]) == exp["L"]
 
 
+class C1(C3):
+    """compress_test.cpp's patch match search (configs[0]: 512x512 PBM, W = 5): for every tile the
+    least-distance window of the causal region -- the reference's dominant cost (§8 f2). Not part
+    of the default bench; value = image pixels per second."""
+
+    def __init__(self, ctx, args, rank):
+        import pybic
+        t = ctx.torch
+        self.ctx, self.pybic = ctx, pybic
+        self.rows = args.rows or 512
+        self.cols = args.cols or 512
+        self.W = 5
+        self.nplanes = 1
+        self.wpr = (self.cols + 63) // 64
+        g = t.Generator(device=ctx.dev)
+        g.manual_seed(0x5EED0000 + rank)
+        self.planes = rand_words(t, (1, self.rows, self.wpr), ctx.dev, g)
+        self.res = None
+        self.k = 0
+        self.pixels = self.rows * self.cols
+        self.bits_e = ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
+        self.workload = f"c1: {self.rows}x{self.cols} plane, compress_test patch search, W = {self.W}"
+
+    def step(self):
+        self.res = self.ctx.patch_search(self.planes[0], self.cols, self.W)
+        self.k += 1
+
+    def out_bytes(self):
+        return 0.0
+
+    def kernel_bytes(self):
+        return {}
+
+    def candidates(self, rows):
+        """windows the search visits for the tiles of the first `rows` rows (its work measure)"""
+        W, cols, n = self.W, self.cols, 0
+        for ti in range((rows + W - 1) // W):
+            i0 = ti * W
+            rows1 = i0 - W + 1 if i0 >= W else 0
+            for tj in range((cols + W - 1) // W):
+                j0 = tj * W
+                n += rows1 * cols + ((i0 - rows1 + 1) * (j0 - W + 1) if j0 >= W else 0)
+        return n
+
+    def check(self, oracle):
+        """the tiles of the first 60 rows depend on nothing below row 64: compare those"""
+        sub = 60
+        P = self.pybic.as_u64(self.planes[0])[:sub + self.W]
+        exp = oracle.patch_search(P, self.cols, self.W)
+        nx = (self.cols + self.W - 1) // self.W
+        nt = (sub // self.W) * nx
+        return all((g.cpu().numpy().view(np.uint32)[:nt] == e[:nt]).all() for g, e in zip(self.res, exp))
+
+    def cpu_time(self, rows):
+        """the reference's own search loop (oracle/_ref) on the first `rows` rows, extrapolated to
+        the whole image by the exact count of visited windows"""
+        from oracle_lib import Oracle, Ref, have_ref
+        P = np.ascontiguousarray(self.pybic.as_u64(self.planes[0])[:rows])
+        impl, kind = (Ref(), "reference") if have_ref() else (Oracle(), "port")
+        t0 = time.perf_counter()
+        impl.patch_search(P, self.cols, self.W)
+        dt = time.perf_counter() - t0
+        return dt * self.candidates(self.rows) / max(1, self.candidates(rows)), dt, kind
+
+
 # ------------------------------------------------------------------------------------------
 def cpu_baseline(wl, args):
     """The reference's own bit-serial med + GolombCoder + EGCoder (oracle/_ref, kind
     "reference") -- or the oracle restatement ("port") where _ref was not built -- on a bounded
     sample of the same workload, OpenMP over independent planes, on this host's cores."""
     from oracle_lib import Oracle, Ref, have_ref
+    if isinstance(wl, C1):
+        sample_rows = min(wl.rows, 120)
+        est, dt, kind = wl.cpu_time(sample_rows)
+        return {"value": wl.pixels / est / 1e6, "unit": "MPix/s", "cores": 1, "kind": kind,
+                "sample": f"search of the tiles in the first {sample_rows} rows ({dt:.1f} s, single thread: the "
+                          f"reference loop is serial), extrapolated to the {wl.rows}x{wl.cols} image by the count "
+                          f"of windows visited ({est:.1f} s)"}
     rows = min(args.cpu_rows, wl.rows)
     planes = np.ascontiguousarray(wl.host_planes(rows)) if hasattr(wl, "host_planes") else None
     if planes is None:
@@ -404,6 +476,8 @@ def main():
         wl = C2(ctx, args, rank)
     elif args.workload == "c4":
         wl = C4(ctx, args, rank, world)
+    elif args.workload == "c1":
+        wl = C1(ctx, args, rank)
     else:
         wl = C5(ctx, args, rank, world)
     dev = ctx.dev

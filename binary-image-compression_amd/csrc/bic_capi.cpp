@@ -459,6 +459,21 @@ int bic_pack_streams(bic_ctx* ctx, const uint64_t* slots, int nplanes, size_t sl
   return BIC_OK;
 }
 
+int bic_patch_search(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                     uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (W < 1 || W > 64 || !geom_ok(rows, cols, wpr) || rows > 0x7fffffffu) return BIC_EINVAL;
+  const size_t ntiles = ((W - 1 + rows) / W) * ((W - 1 + cols) / W);
+  if (ntiles && (!plane || !besti || !bestj || !bestd)) return BIC_EINVAL;
+  if ((unsigned long long)rows * cols >= (1ull << 40)) return BIC_EINVAL;  // scan index field
+  timed(ctx, "patch_search", [&] {
+    bic::launch_patch_search(ctx->cur, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, W, besti, bestj, bestd);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
 int bic_pbm_unpack(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, uint64_t* plane, size_t wpr) {
   int rc = bind(ctx);
   if (rc) return rc;

@@ -108,6 +108,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
 // the words adjacent rows share
 constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2;
 
+void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
+                         uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
+
 void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* raster_out, const uint64_t* plane_in,
                 uint64_t* plane_out, uint32_t rows, uint32_t cols, uint32_t wpr);
 

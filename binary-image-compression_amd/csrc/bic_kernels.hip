@@ -1007,6 +1007,93 @@ void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_
 }
 
 // ------------------------------------------------------------------------------------
+// K9: patch match search (compress_test.cpp:73-111). One workgroup per W x W tile; every
+// candidate position of the causal search region gets its Hamming distance; the result is the
+// first position in the reference's scan order with the least distance (its early exit at a
+// perfect match finds exactly that), or (0, 0, W*W) when nothing beats W*W. Tiles and candidates
+// are read with get_submatrix's flat word indexing (binmat.cpp:267-298): a window running past
+// the right edge continues in the next row, past the last row it reads 0.
+// ------------------------------------------------------------------------------------
+struct FlatImage {
+  const uint64_t* I;
+  uint32_t rows, used, wpr;
+  // 64 bits of row i starting at column j (j < 64 * used)
+  __device__ __forceinline__ uint64_t window(uint32_t i, uint32_t j) const {
+    if (i >= rows) return 0;
+    const uint32_t w = j >> 6, sh = j & 63;
+    const uint64_t a = I[(uint64_t)i * wpr + w];
+    if (!sh) return a;
+    uint64_t b = 0;
+    if (w + 1 < used) b = I[(uint64_t)i * wpr + w + 1];
+    else if (i + 1 < rows) b = I[(uint64_t)(i + 1) * wpr];
+    return (a << sh) | (b >> (64 - sh));
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void k_patch_search(FlatImage img, uint32_t cols, uint32_t W, uint32_t nx,
+                                                         uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+  __shared__ uint64_t P[64];
+  __shared__ unsigned long long red[kWaves];
+  const uint32_t tile = blockIdx.x, ti = tile / nx, tj = tile % nx;
+  const uint32_t i0 = ti * W, j0 = tj * W;
+  const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
+  if (threadIdx.x < W) P[threadIdx.x] = img.window(i0 + threadIdx.x, j0) & topW;
+  __syncthreads();
+  // the reference's loop bounds: int(i0 - W) and int(j0 - W) of unsigned differences
+  const int lim1 = (int)(i0 - W), lim2 = (int)(j0 - W);
+  const uint32_t rows1 = lim1 >= 0 ? (uint32_t)lim1 + 1 : 0;  // region 1: rows [0, rows1), all columns
+  const uint32_t ncol2 = lim2 >= 0 ? (uint32_t)lim2 + 1 : 0;  // region 2: rows [rows1, i0], columns [0, ncol2)
+  const uint64_t n1 = (uint64_t)rows1 * cols;
+  unsigned long long best = ~0ull;  // (distance << 40) | scan index
+  auto visit = [&](uint32_t i2, uint32_t j2, uint64_t idx) {
+    uint32_t d = 0;
+    for (uint32_t r = 0; r < W; ++r) d += (uint32_t)__popcll((P[r] ^ img.window(i2 + r, j2)) & topW);
+    const unsigned long long key = ((unsigned long long)d << 40) | idx;
+    best = key < best ? key : best;
+  };
+  for (uint32_t i2 = 0; i2 < rows1; ++i2)
+    for (uint32_t j2 = threadIdx.x; j2 < cols; j2 += kBlock) visit(i2, j2, (uint64_t)i2 * cols + j2);
+  if (ncol2)
+    for (uint32_t i2 = rows1; i2 <= i0; ++i2)
+      for (uint32_t j2 = threadIdx.x; j2 < ncol2; j2 += kBlock)
+        visit(i2, j2, n1 + (uint64_t)(i2 - rows1) * ncol2 + j2);
+#pragma unroll
+  for (int dd = 32; dd >= 1; dd >>= 1) {
+    const unsigned long long o = shfl_u64(best, lane_id() ^ dd);
+    best = o < best ? o : best;
+  }
+  if (lane_id() == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < kWaves; ++q) best = red[q] < best ? red[q] : best;
+    best = red[0] < best ? red[0] : best;
+    uint32_t bi = 0, bj = 0, bd = W * W;
+    if (best != ~0ull && (uint32_t)(best >> 40) < W * W) {
+      const uint64_t idx = best & ((1ull << 40) - 1);
+      bd = (uint32_t)(best >> 40);
+      if (idx < n1) {
+        bi = (uint32_t)(idx / cols);
+        bj = (uint32_t)(idx % cols);
+      } else {
+        bi = rows1 + (uint32_t)((idx - n1) / ncol2);
+        bj = (uint32_t)((idx - n1) % ncol2);
+      }
+    }
+    besti[tile] = bi;
+    bestj[tile] = bj;
+    bestd[tile] = bd;
+  }
+}
+
+void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
+                         uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+  const uint32_t nx = (W - 1 + cols) / W, ny = (W - 1 + rows) / W;
+  if (!nx || !ny) return;
+  FlatImage img{plane, rows, (cols + 63) / 64, wpr};
+  k_patch_search<<<nx * ny, kBlock, 0, s>>>(img, cols, W, nx, besti, bestj, bestd);
+}
+
+// ------------------------------------------------------------------------------------
 // PBM rasters (pbm.cpp:29-77): a plane word is a big-endian load of 8 raster bytes. One thread
 // per plane word; raster rows are only byte-aligned, so bytes move one at a time (coalesced
 // across the wave).

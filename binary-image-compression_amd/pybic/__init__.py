@@ -26,6 +26,7 @@ EXPORTS = [
     "bic_encode_planes", "bic_encode_planes2", "bic_ctx_set_option", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
+    "bic_patch_search",
 ]
 
 
@@ -88,6 +89,7 @@ def load(path=LIB_PATH):
     sig("bic_memset", i32, [vp, vp, i32, sz])
     sig("bic_pbm_unpack", i32, [vp, vp, sz, sz, vp, sz])
     sig("bic_pbm_pack", i32, [vp, vp, sz, sz, sz, vp])
+    sig("bic_patch_search", i32, [vp, vp, sz, sz, sz, u32, vp, vp, vp])
     _lib = L
     return L
 
@@ -282,6 +284,17 @@ class Context:
                                             cap_words, _p(stats)), "bic_patch_encode")
         return dict(weights=weights, w_nonpred=wo, w_pred=wO, modes=modes, resid=resid, stream=stream,
                     stats=stats)
+
+    def patch_search(self, plane, cols, W):
+        """compress_test.cpp's patch search -> (besti, bestj, bestd) int32 device tensors per tile."""
+        rows, wpr = plane.shape
+        n = ((rows + W - 1) // W) * ((cols + W - 1) // W)
+        t = self.torch
+        out = [t.empty(n, dtype=t.int32, device=self.dev) for _ in range(3)]
+        self._bind_stream()
+        self._chk(self.lib.bic_patch_search(self.h, _p(plane), rows, cols, wpr, W, *(_p(o) for o in out)),
+                  "bic_patch_search")
+        return tuple(out)
 
     def pbm_unpack(self, raster, rows, cols, wpr=None):
         """P4 raster bytes (uint8 device tensor, rows x ceil(cols/8)) -> int64 plane [rows, wpr]."""

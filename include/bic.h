@@ -133,6 +133,16 @@ int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
                      uint32_t* w_pred, uint8_t* modes, uint64_t* resid, uint64_t* stream,
                      size_t cap_words, uint64_t* stats);
 
+/* ---- patch match search (compress_test.cpp:73-111) ----------------------------
+ * For every W x W tile in raster order over ceil(rows/W) x ceil(cols/W) (1 <= W <= 64): the
+ * position (besti, bestj) and distance bestd of the least Hamming distance between the tile and a
+ * W x W window over the causal search region -- rows 0 .. i0-W at every column, then rows
+ * i0-W+1 .. i0 at columns 0 .. j0-W -- first in the reference's scan order; (0, 0, W*W) when no
+ * window beats W*W. Windows use get_submatrix's flat indexing (binmat.cpp:267-298: past the right
+ * edge they continue in the next row). Outputs: device u32 arrays, one entry per tile. */
+int bic_patch_search(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                     uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
+
 /* log2 C(n, r) (enumerative_codelength, coding.cpp:19-22) computed without GSL, and the tile
  * length table lentab[w] = (uint64)(2 + log2 C(W*W, w)) for w = 0..W*W (host memory, W*W+1
  * entries) that bic_patch_encode takes. Host-side helpers; no device needed. */

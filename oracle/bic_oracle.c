@@ -515,3 +515,42 @@ uint64_t bo_baseline_planes(const uint64_t* planes, int nplanes, size_t rows, si
     if (threads_used) *threads_used = nt;
     return total;
 }
+
+/* compress_test.cpp:73-111, loop for loop (int conversions included: int(i0 - W) of an
+ * unsigned difference is negative for i0 < W, so the first loop is skipped). */
+void bo_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                     uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+    const size_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+    const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
+    uint64_t P[64], P2[64];
+    size_t li = 0;
+    for (size_t i = 0; i < Ny; i++)
+        for (size_t j = 0; j < Nx; j++, li++) {
+            const size_t i0 = i * W, j0 = j * W;
+            bo_get_submatrix(I, rows, cols, wpr, i0, i0 + W, j0, j0 + W, P, 1);
+            size_t bi = 0, bj = 0, bd = (size_t)W * W;
+            int i2;
+            int perfect = 0;
+            for (i2 = 0; (i2 <= (int)(i0 - W)) && !perfect; i2++) {
+                for (int j2 = 0; j2 < (int)cols; j2++) {
+                    bo_get_submatrix(I, rows, cols, wpr, (size_t)i2, (size_t)i2 + W, (size_t)j2, (size_t)j2 + W, P2, 1);
+                    size_t d = 0;
+                    for (unsigned r = 0; r < W; r++) d += (size_t)__builtin_popcountll((P[r] ^ P2[r]) & topW);
+                    if (d < bd) { bd = d; bi = (size_t)i2; bj = (size_t)j2; }
+                    if (bd == 0) { perfect = 1; break; }
+                }
+            }
+            for (; (i2 <= (int)i0) && !perfect; i2++) {
+                for (int j2 = 0; j2 <= (int)(j0 - W); j2++) {
+                    bo_get_submatrix(I, rows, cols, wpr, (size_t)i2, (size_t)i2 + W, (size_t)j2, (size_t)j2 + W, P2, 1);
+                    size_t d = 0;
+                    for (unsigned r = 0; r < W; r++) d += (size_t)__builtin_popcountll((P[r] ^ P2[r]) & topW);
+                    if (d < bd) { bd = d; bi = (size_t)i2; bj = (size_t)j2; }
+                    if (bd == 0) { perfect = 1; break; }
+                }
+            }
+            besti[li] = (uint32_t)bi;
+            bestj[li] = (uint32_t)bj;
+            bestd[li] = (uint32_t)bd;
+        }
+}

@@ -144,6 +144,13 @@ int64_t bo_patch_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsig
                         const uint64_t* lentab, uint32_t* w_nonpred, uint32_t* w_pred,
                         char* modes, uint64_t* L_out, uint8_t* stream, size_t cap_bytes);
 
+/* compress_test.cpp:73-111 (patch match search): for each W x W tile in raster order over
+ * ceil(rows/W) x ceil(cols/W), the position (i2, j2) of the least Hamming distance over the
+ * causal search region, first in scan order, exactly as the reference's two loops with their
+ * early exit at a perfect match; (0, 0, W*W) when nothing beats W*W. */
+void bo_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                     uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
+
 /* ---- CPU baseline (bench.py cpu_baseline leg) ---------------------------- */
 /* med + Golomb + EG over nplanes planes, OpenMP over planes when built with it.
  * Returns total Golomb bits + EG bits; *threads_used receives the thread count. */

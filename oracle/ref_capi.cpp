@@ -247,3 +247,41 @@ double ref_baseline_planes(const uint64_t* planes, int nplanes, size_t rows, siz
 }
 
 }  // extern "C"
+
+// compress_test.cpp:73-111's search on the reference's own binary_matrix (get_submatrix, dist)
+extern "C" int ref_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                                uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+  binary_matrix A = from_words(I, rows, cols, wpr);
+  const idx_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+  binary_matrix P, P2;
+  idx_t li = 0;
+  for (idx_t i = 0; i < Ny; i++)
+    for (idx_t j = 0; j < Nx; j++, li++) {
+      const idx_t i0 = i * W, j0 = j * W;
+      P = A.get_submatrix(i0, i0 + W, j0, j0 + W);
+      idx_t bi = 0, bj = 0, bd = (idx_t)W * W;
+      int i2;
+      bool perfect = false;
+      for (i2 = 0; (i2 <= int(i0 - W)) && !perfect; i2++)
+        for (int j2 = 0; j2 < int(cols); j2++) {
+          P2 = A.get_submatrix(i2, i2 + W, j2, j2 + W);
+          const idx_t d = dist(P, P2);
+          if (d < bd) { bd = d; bi = i2; bj = j2; }
+          if (bd == 0) { perfect = true; break; }
+        }
+      for (; (i2 <= int(i0)) && !perfect; i2++)
+        for (int j2 = 0; j2 <= int(j0 - W); j2++) {
+          P2 = A.get_submatrix(i2, i2 + W, j2, j2 + W);
+          const idx_t d = dist(P, P2);
+          if (d < bd) { bd = d; bi = i2; bj = j2; }
+          if (bd == 0) { perfect = true; break; }
+        }
+      besti[li] = (uint32_t)bi;
+      bestj[li] = (uint32_t)bj;
+      bestd[li] = (uint32_t)bd;
+    }
+  P.destroy();
+  P2.destroy();
+  A.destroy();
+  return 0;
+}

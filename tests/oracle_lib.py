@@ -161,6 +161,16 @@ class Oracle:
                     modes=modes.raw[:n].decode(), residual=I, stream=stream)
 
 
+    def patch_search(self, I, cols, W):
+        """compress_test.cpp:73-111 search: (besti, bestj, bestd) per tile, raster order."""
+        I = np.ascontiguousarray(I)
+        rows, wpr = I.shape
+        n = ((rows + W - 1) // W) * ((cols + W - 1) // W)
+        bi, bj, bd = (np.zeros(n, np.uint32) for _ in range(3))
+        self.lib.bo_patch_search(ptr(I, u64p), rows, cols, wpr, W, ptr(bi, u32p), ptr(bj, u32p), ptr(bd, u32p))
+        return bi, bj, bd
+
+
 class Ref:
     """The reference's own objects (oracle/_ref/libref.so), this container only."""
 
@@ -235,6 +245,14 @@ class Ref:
     def pbm_roundtrip(self, path, out_path):
         rc = np.zeros(2, np.uint64)
         return self.lib.ref_pbm_roundtrip(path.encode(), out_path.encode(), ptr(rc, u64p))
+
+    def patch_search(self, I, cols, W):
+        I = np.ascontiguousarray(I)
+        rows, wpr = I.shape
+        n = ((rows + W - 1) // W) * ((cols + W - 1) // W)
+        bi, bj, bd = (np.zeros(n, np.uint32) for _ in range(3))
+        self.lib.ref_patch_search(ptr(I, u64p), rows, cols, wpr, W, ptr(bi, u32p), ptr(bj, u32p), ptr(bd, u32p))
+        return bi, bj, bd
 
     def baseline(self, planes, rows, cols, predict=1, do_eg=1, threads=0):
         planes = np.ascontiguousarray(planes)

@@ -293,3 +293,16 @@ def test_pbm_raster_pack_unpack(ctx, oracle, rows, cols):
     ctx.sync()
     assert np.array_equal(as_u64(back), mask_pixels(P, cols))
     assert ras2.cpu().numpy().tobytes() == raster.tobytes()
+
+
+@pytest.mark.parametrize("W,rows,cols,p", [(5, 37, 70, 0.3), (3, 20, 33, 0.5), (8, 40, 128, 0.1), (5, 26, 64, 0.02),
+                                           (4, 16, 50, 0.0), (32, 96, 200, 0.2), (5, 120, 300, 0.05)])
+def test_patch_search(ctx, oracle, W, rows, cols, p):
+    """compress_test.cpp's search (tiles past the edges wrap into the next row; sparse images give
+    perfect matches; p = 0 gives ties everywhere)"""
+    I = oracle.gen_plane(3000 + W + rows, p, rows, cols)
+    exp = oracle.patch_search(I, cols, W)
+    got = ctx.patch_search(ctx.to_dev(I), cols, W)
+    ctx.sync()
+    for name, e, g in zip(("besti", "bestj", "bestd"), exp, got):
+        assert np.array_equal(g.cpu().numpy().view(np.uint32), e), name

@@ -37,3 +37,14 @@ def test_random_tiles(oracle, ref, W):
     for k in ("bits", "L", "modes"):
         assert a[k] == b[k]
     assert np.array_equal(a["w_pred"], b["w_pred"])
+
+
+@pytest.mark.parametrize("W,rows,cols,p", [(5, 37, 70, 0.3), (3, 20, 33, 0.5), (8, 40, 128, 0.1), (5, 26, 64, 0.02),
+                                           (4, 16, 50, 0.0)])
+def test_patch_search(oracle, ref, W, rows, cols, p):
+    """compress_test.cpp's patch match search: oracle restatement == the reference's own
+    get_submatrix/dist loop (edge tiles wrap into the next row; sparse images hit perfect matches)"""
+    I = oracle.gen_plane(3000 + W + rows, p, rows, cols)
+    a, b = oracle.patch_search(I, cols, W), ref.patch_search(I, cols, W)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
