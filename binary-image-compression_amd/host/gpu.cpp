@@ -253,6 +253,28 @@ int Device::tiles(const binary_matrix& I, unsigned W, TileResult* out, const uin
   return BIC_OK;
 }
 
+int Device::patch_search(const binary_matrix& I, unsigned W, std::vector<uint32_t>* besti,
+                         std::vector<uint32_t>* bestj, std::vector<uint32_t>* bestd) {
+  BIC_TRY(status_);
+  if (!besti || !bestj || !bestd || W < 1 || W > 64) return BIC_EINVAL;
+  const idx_t rows = I.get_rows(), cols = I.get_cols(), wpr = I.get_blocks_per_row();
+  const size_t nt = ((W - 1 + rows) / W) * ((W - 1 + cols) / W);
+  besti->assign(nt, 0);
+  bestj->assign(nt, 0);
+  bestd->assign(nt, W * W);
+  if (nt == 0) return BIC_OK;
+  BIC_TRY(ensure(in_, rows * wpr * 8));
+  BIC_TRY(ensure(aux_, 3 * nt * 4));
+  uint32_t* d = static_cast<uint32_t*>(aux_.p);
+  BIC_TRY(upload(I, static_cast<uint64_t*>(in_.p)));
+  BIC_TRY(bic_patch_search(ctx_, static_cast<const uint64_t*>(in_.p), rows, cols, wpr, W, d, d + nt, d + 2 * nt));
+  BIC_TRY(bic_sync(ctx_));
+  BIC_TRY(bic_memcpy_d2h(ctx_, besti->data(), d, nt * 4));
+  BIC_TRY(bic_memcpy_d2h(ctx_, bestj->data(), d + nt, nt * 4));
+  BIC_TRY(bic_memcpy_d2h(ctx_, bestd->data(), d + 2 * nt, nt * 4));
+  return BIC_OK;
+}
+
 Device& default_device() {
   static Device* dev = new Device(0);
   if (dev->status() != BIC_OK) {

@@ -88,6 +88,11 @@ class Device {
   int tiles(const binary_matrix& I, unsigned W, TileResult* out, const uint64_t* lentab = nullptr,
             binary_matrix* resid = nullptr);
 
+  // compress_test.cpp:73-111: per W x W tile (raster order over ceil(rows/W) x ceil(cols/W)) the
+  // least-distance window of the causal search region, first in the reference's scan order.
+  int patch_search(const binary_matrix& I, unsigned W, std::vector<uint32_t>* besti,
+                   std::vector<uint32_t>* bestj, std::vector<uint32_t>* bestd);
+
  private:
   struct Buf {
     void* p = nullptr;

@@ -268,6 +268,43 @@ int gpu(int argc, char** argv) {
     CHECK((uint64_t)gt.bitcount == t.stream.bits, "tile stream bits");
   }
 
+  // compress_test.cpp's search, written with the reference API (get_submatrix, dist) as the
+  // driver does, against the GPU search on plane 0
+  {
+    const unsigned W = 5;
+    std::vector<uint32_t> bi, bj, bd;
+    CHECK(dev.patch_search(planes[0], W, &bi, &bj, &bd) == BIC_OK, "patch_search");
+    const idx_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+    binary_matrix P, P2;
+    idx_t li = 0;
+    const binary_matrix& I = planes[0];
+    for (idx_t i = 0; i < Ny && li < 40; i++)
+      for (idx_t j = 0; j < Nx && li < 40; j++, li++) {
+        const idx_t i0 = i * W, j0 = j * W;
+        P = I.get_submatrix(i0, i0 + W, j0, j0 + W);
+        idx_t besti = 0, bestj = 0, bestd = W * W;
+        int i2;
+        bool perfect = false;
+        for (i2 = 0; (i2 <= int(i0 - W)) && !perfect; i2++)
+          for (int j2 = 0; j2 < int(cols); j2++) {
+            P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+            const idx_t d = dist(P, P2);
+            if (d < bestd) { bestd = d; besti = i2; bestj = j2; }
+            if (bestd == 0) { perfect = true; break; }
+          }
+        for (; (i2 <= int(i0)) && !perfect; i2++)
+          for (int j2 = 0; j2 <= int(j0 - W); j2++) {
+            P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+            const idx_t d = dist(P, P2);
+            if (d < bestd) { bestd = d; besti = i2; bestj = j2; }
+            if (bestd == 0) { perfect = true; break; }
+          }
+        CHECK(bi[li] == besti && bj[li] == bestj && bd[li] == bestd, "patch search tile %lu", li);
+      }
+    P.destroy();
+    P2.destroy();
+  }
+
   for (auto& p : planes) p.destroy();
   A.destroy();
   std::printf("gpu %s planes=%d\n", failures ? "FAILED" : "ok", np);
