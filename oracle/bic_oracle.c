@@ -554,3 +554,102 @@ void bo_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, un
             bestd[li] = (uint32_t)bd;
         }
 }
+
+/* compress7_test.cpp:117-275 with a search window R and a match threshold T, loop for loop.
+ * Search region of tile (i0, j0) (:127-174): rows i0 .. mini2 at columns maxj2 .. minj, then rows
+ * i0-W .. mini at columns maxj .. minj, both scanned downwards, stopping at the first window with
+ * distance <= T. The image is read as it stands after the residual write-back of every earlier
+ * tile (:266, :272), so the search sees residuals, and at j0 = 0 its first window is the tile
+ * itself. Lengths follow :218-221 in double: nomatch 2 + enumL[w], match (2 + idx_len) + enumL[w]
+ * with idx_len = ceil(log2(search_win_size)); a search_win_size <= 0 (log2 of 0 or of a negative
+ * number, converted to idx_t: 2^63 on x86-64) makes the match length huge, so such a tile never
+ * takes the match branch. bestd = W*W+1 when the region holds no window (:124). */
+int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T, unsigned R,
+                    const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
+                    uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
+                    uint8_t* stream_nomatch, size_t cap_bytes) {
+    if (W == 0 || W > 64 || rows % W || cols % W) return -1;
+    const size_t Ny = rows / W, Nx = cols / W, M = (size_t)W * W;
+    const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
+    uint64_t P[64], P2[64], P3[64], dP[64], dP3[64];
+    bo_bw bwm, bwn;
+    bo_bw_init(&bwm, stream_match, cap_bytes);
+    bo_bw_init(&bwn, stream_nomatch, cap_bytes);
+    bo_golomb gm, gn;
+    bo_golomb_init(&gm);
+    bo_golomb_init(&gn);
+    uint64_t L = 0, matches = 0;
+    size_t li = 0;
+    const int iW = (int)W, iR = (int)R, icols = (int)cols;
+    for (size_t i = 0; i < Ny; i++)
+        for (size_t j = 0; j < Nx; j++, li++) {
+            const int i0 = (int)(i * W), j0 = (int)(j * W);
+            bo_get_submatrix(I, rows, cols, wpr, (size_t)i0, (size_t)i0 + W, (size_t)j0, (size_t)j0 + W, P, 1);
+            size_t bi = 0, bj = 0, bd = M + 1;
+            int perfect = 0;
+            const int mini = i0 > iR ? i0 - iR : 0;
+            const int minj = j0 > iR ? j0 - iR : 0;
+            const int maxj = (j0 + iR > icols - iW) ? icols - iW : j0 + iR;
+            const int mini2 = i0 > iW ? i0 - iW : 0;
+            const int maxj2 = j0 > iW ? j0 - iW : 0;
+            const int64_t swin = (int64_t)(i0 - mini2) * (maxj2 - minj) + (int64_t)(mini2 - mini) * (maxj - minj);
+            for (int pass = 0; pass < 2 && !perfect; pass++) {
+                const int ihi = pass ? i0 - iW : i0, ilo = pass ? mini : mini2, jhi = pass ? maxj : maxj2;
+                for (int i2 = ihi; i2 >= ilo && !perfect; i2--)
+                    for (int j2 = jhi; j2 >= minj; j2--) {
+                        bo_get_submatrix(I, rows, cols, wpr, (size_t)i2, (size_t)i2 + W, (size_t)j2, (size_t)j2 + W, P2, 1);
+                        size_t d = 0;
+                        for (unsigned r = 0; r < W; r++) d += (size_t)__builtin_popcountll((P[r] ^ P2[r]) & topW);
+                        if (d < bd) { bd = d; bi = (size_t)i2; bj = (size_t)j2; }
+                        if (bd <= T) { perfect = 1; break; }
+                    }
+            }
+            if (bd <= M) {                                               /* :185-190 */
+                bo_get_submatrix(I, rows, cols, wpr, bi, bi + W, bj, bj + W, P2, 1);
+                for (unsigned r = 0; r < W; r++) P3[r] = (P[r] ^ P2[r]) & topW;
+            } else {
+                for (unsigned r = 0; r < W; r++) P3[r] = P[r] & topW;
+            }
+            for (unsigned r = 0; r < W; r++) P[r] &= topW;
+            bo_med(P, dP, W, W, 1);
+            bo_med(P3, dP3, W, W, 1);
+            const uint64_t w_mn = bo_weight(P3, W, W, 1), w_nn = bo_weight(P, W, W, 1);
+            const uint64_t w_mp = bo_weight(dP3, W, W, 1), w_np = bo_weight(dP, W, W, 1);
+            uint64_t idx_len = 0x8000000000000000ull;                     /* :212 */
+            if (swin >= 1) idx_len = swin == 1 ? 0 : 64 - (uint64_t)__builtin_clzll((uint64_t)(swin - 1));
+            const uint64_t nn_len = (uint64_t)(2.0 + enumL[w_nn]), np_len = (uint64_t)(2.0 + enumL[w_np]);
+            uint64_t mn_len = ~0ull, mp_len = ~0ull;
+            if (swin >= 1) {
+                mn_len = (uint64_t)((double)(2 + idx_len) + enumL[w_mn]);
+                mp_len = (uint64_t)((double)(2 + idx_len) + enumL[w_mp]);
+            }
+            const int mpred = mn_len > mp_len, npred = nn_len > np_len;  /* :232, :243 */
+            const uint64_t match_len = mpred ? mp_len : mn_len, match_w = mpred ? w_mp : w_mn;
+            const uint64_t nomatch_len = npred ? np_len : nn_len, nomatch_w = npred ? w_np : w_nn;
+            const int take = nomatch_len > match_len;                   /* :255 */
+            const uint64_t* res = take ? (mpred ? dP3 : P3) : (npred ? dP : P);
+            const uint64_t w = take ? match_w : nomatch_w;
+            if (take) {
+                bo_golomb_code(&gm, (uint32_t)w, &bwm);
+                matches++;
+                L += match_len;
+            } else {
+                bo_golomb_code(&gn, (uint32_t)w, &bwn);
+                L += nomatch_len;
+            }
+            bo_set_submatrix(I, rows, cols, wpr, (size_t)i0, (size_t)j0, res, W, W, 1);
+            if (besti) besti[li] = (uint32_t)bi;
+            if (bestj) bestj[li] = (uint32_t)bj;
+            if (bestd) bestd[li] = (uint32_t)bd;
+            if (weights) weights[li] = (uint32_t)w;
+            if (modes) modes[li] = take ? (mpred ? 'X' : 'x') : (npred ? 'O' : 'o');
+        }
+    if (stats) {
+        stats[0] = matches;
+        stats[1] = (uint64_t)gm.bitcount;
+        stats[2] = (uint64_t)gn.bitcount;
+        stats[3] = L;
+    }
+    if ((stream_match && bwm.overflow) || (stream_nomatch && bwn.overflow)) return -1;
+    return 0;
+}

@@ -151,6 +151,20 @@ int64_t bo_patch_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsig
 void bo_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
                      uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
 
+/* compress7_test.cpp:117-275 with search window R and match threshold T (rows, cols multiples
+ * of W): per tile the causal search over the image as modified by the residual write-back of
+ * every earlier tile, modes 'X' 'x' (match, predicted or not) 'O' 'o' (no match), the chosen
+ * weight coded by golomb_match / golomb_nomatch, the residual written back into I (in place).
+ * enumL[w] = enumL(W*W, w) for w = 0..W*W. Outputs per tile (each nullable): besti, bestj,
+ * bestd (W*W+1 when the region is empty), weights, modes. stats (nullable) [4]: matches,
+ * golomb_match bits, golomb_nomatch bits, sum of the chosen lengths (L before the bitcounts).
+ * Streams (nullable, cap_bytes each) receive the two coders' codewords. Returns 0, -1 on a bad
+ * argument or stream overflow. */
+int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T, unsigned R,
+                    const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
+                    uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
+                    uint8_t* stream_nomatch, size_t cap_bytes);
+
 /* ---- CPU baseline (bench.py cpu_baseline leg) ---------------------------- */
 /* med + Golomb + EG over nplanes planes, OpenMP over planes when built with it.
  * Returns total Golomb bits + EG bits; *threads_used receives the thread count. */

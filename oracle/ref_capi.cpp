@@ -285,3 +285,104 @@ extern "C" int ref_patch_search(const uint64_t* I, size_t rows, size_t cols, siz
   A.destroy();
   return 0;
 }
+
+// compress7_test.cpp:117-275 with search window R and threshold T on the reference's own
+// binary_matrix (get_submatrix, dist, add, weight, set_submatrix), med (pred.cpp:3, the same
+// formula as compress7's local med) and two GolombCoders. enumL(W*W, w) comes from the caller
+// (GSL is absent here). The length expressions are the driver's, evaluated in double and
+// converted to idx_t the same way; only ceil(log2(search_win_size)) for a size <= 0 (an undefined
+// conversion on x86-64: 2^63) is taken as "no match" directly. dP / dP3 are cleared first (the
+// driver leaves their (0,0) uninitialised). stats [4]: matches, bits match, bits nomatch, L.
+extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
+                              unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                              uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats) {
+  binary_matrix I = from_words(Iw, rows, cols, wpr);
+  const int iW = (int)W, iR = (int)R;
+  const idx_t M = (idx_t)W * W;
+  const idx_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+  binary_matrix P, P2;
+  binary_matrix P3(W, W);
+  GolombCoder golomb_match, golomb_nomatch;
+  uint64_t L = 0, matches = 0;
+  idx_t li = 0;
+  for (idx_t i = 0; i < Ny; i++)
+    for (idx_t j = 0; j < Nx; j++, li++) {
+      const int i0 = i * W, j0 = j * W;
+      P = I.get_submatrix(i0, i0 + W, j0, j0 + W);
+      idx_t bi = 0, bj = 0, bd = M + 1;
+      int i2;
+      bool perfect = false;
+      const int mini = i0 > iR ? (i0 - iR) : 0;
+      const int minj = (j0 > iR) ? (j0 - iR) : 0;
+      const int maxj = ((j0 + iR) > (int(cols) - iW)) ? (cols - W) : (j0 + iR);
+      const int mini2 = (i0 > iW) ? (i0 - iW) : 0;
+      const int maxj2 = (j0 > iW) ? (j0 - iW) : 0;
+      const int swin = (i0 - mini2) * (maxj2 - minj) + (mini2 - mini) * (maxj - minj);
+      for (i2 = i0; (i2 >= mini2) && !perfect; i2--)
+        for (int j2 = maxj2; j2 >= minj; j2--) {
+          P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+          const idx_t d = dist(P, P2);
+          if (d < bd) { bd = d; bi = i2; bj = j2; }
+          if (bd <= T) { perfect = true; break; }
+        }
+      for (i2 = i0 - iW; (i2 >= mini) && !perfect; i2--)
+        for (int j2 = maxj; j2 >= minj; j2--) {
+          P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+          const idx_t d = dist(P, P2);
+          if (d < bd) { bd = d; bi = i2; bj = j2; }
+          if (bd <= T) { perfect = true; break; }
+        }
+      if (bd <= M) {
+        P2 = I.get_submatrix(bi, bi + W, bj, bj + W);
+        add(P, P2, P3);
+      } else {
+        P3 = P.get_copy();
+      }
+      const idx_t w_mn = P3.weight(), w_nn = P.weight();
+      binary_matrix dP(W, W), dP3(W, W);
+      dP.clear();
+      dP3.clear();
+      med(P, dP);
+      med(P3, dP3);
+      const idx_t w_mp = dP3.weight(), w_np = dP.weight();
+      const bool ok = swin > 0;
+      const idx_t idx_len = ok ? (idx_t)ceil(log2(swin)) : 0;
+      const idx_t nn_len = 1 + 1 + enuml[w_nn], np_len = 1 + 1 + enuml[w_np];
+      const idx_t mn_len = ok ? (idx_t)(1 + 1 + idx_len + enuml[w_mn]) : ~(idx_t)0;
+      const idx_t mp_len = ok ? (idx_t)(1 + 1 + idx_len + enuml[w_mp]) : ~(idx_t)0;
+      const bool mpred = mn_len > mp_len, npred = nn_len > np_len;
+      const idx_t match_len = mpred ? mp_len : mn_len, nomatch_len = npred ? np_len : nn_len;
+      const bool take = nomatch_len > match_len;
+      idx_t w;
+      if (take) {
+        w = mpred ? w_mp : w_mn;
+        golomb_match.codeSample(w);
+        matches++;
+        L += match_len;
+        I.set_submatrix(i0, j0, mpred ? dP3 : P3);
+      } else {
+        w = npred ? w_np : w_nn;
+        golomb_nomatch.codeSample(w);
+        L += nomatch_len;
+        I.set_submatrix(i0, j0, npred ? dP : P);
+      }
+      if (besti) besti[li] = (uint32_t)bi;
+      if (bestj) bestj[li] = (uint32_t)bj;
+      if (bestd) bestd[li] = (uint32_t)bd;
+      if (weights) weights[li] = (uint32_t)w;
+      if (modes) modes[li] = take ? (mpred ? 'X' : 'x') : (npred ? 'O' : 'o');
+      dP.destroy();
+      dP3.destroy();
+    }
+  to_words(I, Iw, wpr);
+  if (stats) {
+    stats[0] = matches;
+    stats[1] = (uint64_t)golomb_match.bitcount;
+    stats[2] = (uint64_t)golomb_nomatch.bitcount;
+    stats[3] = L;
+  }
+  P.destroy();
+  P2.destroy();
+  I.destroy();
+  return 0;
+}

@@ -14,6 +14,7 @@ u64p = C.POINTER(C.c_uint64)
 u32p = C.POINTER(C.c_uint32)
 i32p = C.POINTER(C.c_int32)
 u8p = C.POINTER(C.c_uint8)
+dp = C.POINTER(C.c_double)
 sz = C.c_size_t
 
 
@@ -48,6 +49,10 @@ class Oracle:
         _sig(L, "bo_patch_encode", C.c_int64,
              [u64p, sz, sz, sz, C.c_uint, u64p, u32p, u32p, C.c_char_p, u64p, u8p, sz])
         _sig(L, "bo_baseline_planes", C.c_uint64, [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, C.POINTER(C.c_int)])
+        _sig(L, "bo_patch_search", None, [u64p, sz, sz, sz, C.c_uint, u32p, u32p, u32p])
+        _sig(L, "bo_match_encode", C.c_int,
+             [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p,
+              u8p, u8p, sz])
 
     # -- inputs ----------------------------------------------------------
     def gen_plane(self, seed, p, rows, cols, wpr=None):
@@ -170,6 +175,34 @@ class Oracle:
         self.lib.bo_patch_search(ptr(I, u64p), rows, cols, wpr, W, ptr(bi, u32p), ptr(bj, u32p), ptr(bd, u32p))
         return bi, bj, bd
 
+    def enum_table(self, W):
+        """enumL(W*W, w) for w = 0..W*W (the double table the match loop takes)."""
+        M = W * W
+        return np.array([self.enumL(M, w) for w in range(M + 1)], np.float64)
+
+    def match_encode(self, I, cols, W, T=0, R=128, enuml=None, want_stream=True):
+        """compress7_test.cpp:117-275 with search window R, threshold T (bo_match_encode)."""
+        I = np.array(I, copy=True)
+        rows, wpr = I.shape
+        enuml = self.enum_table(W) if enuml is None else np.ascontiguousarray(enuml, np.float64)
+        n = (rows // W) * (cols // W)
+        bi, bj, bd, wt = (np.zeros(n, np.uint32) for _ in range(4))
+        modes = C.create_string_buffer(n + 1)
+        stats = np.zeros(4, np.uint64)
+        cap = n * 8 + 4096
+        bm = np.zeros(cap, np.uint8) if want_stream else None
+        bn = np.zeros(cap, np.uint8) if want_stream else None
+        rc = self.lib.bo_match_encode(ptr(I, u64p), rows, cols, wpr, W, T, R, ptr(enuml, dp), ptr(bi, u32p),
+                                      ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(stats, u64p),
+                                      ptr(bm, u8p), ptr(bn, u8p), cap if want_stream else 0)
+        assert rc == 0, rc
+        out = dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes.raw[:n].decode(), residual=I,
+                   matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]))
+        if want_stream:
+            out["stream_match"] = bm[: ((out["bits_match"] + 63) // 64) * 8].copy()
+            out["stream_nomatch"] = bn[: ((out["bits_nomatch"] + 63) // 64) * 8].copy()
+        return out
+
 
 class Ref:
     """The reference's own objects (oracle/_ref/libref.so), this container only."""
@@ -186,6 +219,9 @@ class Ref:
         _sig(L, "ref_pbm_roundtrip", C.c_int, [C.c_char_p, C.c_char_p, u64p])
         _sig(L, "ref_read_pbm", C.c_int, [C.c_char_p, u64p, sz, u64p])
         _sig(L, "ref_read_pgm", C.c_int, [C.c_char_p, C.POINTER(C.c_int), u32p])
+        _sig(L, "ref_patch_search", C.c_int, [u64p, sz, sz, sz, C.c_uint, u32p, u32p, u32p])
+        _sig(L, "ref_match_loop", C.c_int,
+             [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p])
         _sig(L, "ref_baseline_planes", C.c_double,
              [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, C.c_int, u64p, C.POINTER(C.c_int)])
 
@@ -254,6 +290,19 @@ class Ref:
         self.lib.ref_patch_search(ptr(I, u64p), rows, cols, wpr, W, ptr(bi, u32p), ptr(bj, u32p), ptr(bd, u32p))
         return bi, bj, bd
 
+    def match_loop(self, I, cols, W, T, R, enuml):
+        I = np.array(I, copy=True)
+        rows, wpr = I.shape
+        enuml = np.ascontiguousarray(enuml, np.float64)
+        n = (rows // W) * (cols // W)
+        bi, bj, bd, wt = (np.zeros(n, np.uint32) for _ in range(4))
+        modes = C.create_string_buffer(n + 1)
+        stats = np.zeros(4, np.uint64)
+        self.lib.ref_match_loop(ptr(I, u64p), rows, cols, wpr, W, T, R, ptr(enuml, dp), ptr(bi, u32p),
+                                ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(stats, u64p))
+        return dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes.raw[:n].decode(), residual=I,
+                    matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]))
+
     def baseline(self, planes, rows, cols, predict=1, do_eg=1, threads=0):
         planes = np.ascontiguousarray(planes)
         nplanes = planes.shape[0]
@@ -267,3 +316,23 @@ class Ref:
 
 def have_ref():
     return os.path.exists(REF_SO)
+
+
+def pack_rows(bits):
+    """bool (rows, cols) -> plane words (rows, ceil(cols/64)), MSB = leftmost pixel."""
+    rows, cols = bits.shape
+    wpr = max(1, (cols + 63) // 64)
+    pad = np.zeros((rows, wpr * 64), bool)
+    pad[:, :cols] = bits
+    return np.packbits(pad, axis=1).view(">u8").astype(np.uint64).reshape(rows, wpr)
+
+
+def periodic_plane(seed, rows, cols, ph, pw, p=0.5, flip=0.0):
+    """A random ph x pw block repeated over the plane, then bits flipped with probability
+    `flip`: inputs on which compress7's match search finds exact and near matches."""
+    rng = np.random.default_rng(seed)
+    blk = rng.random((ph, pw)) < p
+    bits = np.tile(blk, (rows // ph + 1, cols // pw + 1))[:rows, :cols]
+    if flip:
+        bits ^= rng.random((rows, cols)) < flip
+    return pack_rows(bits)

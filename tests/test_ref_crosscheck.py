@@ -48,3 +48,39 @@ def test_patch_search(oracle, ref, W, rows, cols, p):
     a, b = oracle.patch_search(I, cols, W), ref.patch_search(I, cols, W)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+MATCH_CASES = [  # W, rows, cols, T, R, input
+    (8, 64, 128, 0, 32, ("periodic", 8, 8, 0.5, 0.0)),
+    (8, 64, 96, 2, 24, ("periodic", 8, 24, 0.5, 0.01)),
+    (5, 40, 60, 0, 12, ("periodic", 7, 11, 0.4, 0.0)),
+    (4, 32, 64, 1, 4, ("random", 0.1)),
+    (4, 32, 64, 0, 2, ("random", 0.3)),   # R < W: empty regions, negative search_win_size
+    (16, 64, 128, 0, 40, ("periodic", 16, 32, 0.3, 0.002)),
+    (6, 36, 72, 40, 12, ("random", 0.5)),  # T >= W*W+1 - ...: the first window always ends the search
+    (8, 48, 64, 0, 128, ("random", 0.02)),
+]
+
+
+def match_input(oracle, seed, rows, cols, spec):
+    from oracle_lib import periodic_plane
+    if spec[0] == "periodic":
+        return periodic_plane(seed, rows, cols, spec[1], spec[2], spec[3], spec[4])
+    return oracle.gen_plane(seed, spec[1], rows, cols)
+
+
+@pytest.mark.parametrize("case", range(len(MATCH_CASES)))
+def test_match_encode(oracle, ref, case):
+    """compress7_test.cpp with a search window: oracle == the driver's loop over the reference's
+    own get_submatrix / dist / add / med / set_submatrix / GolombCoder"""
+    W, rows, cols, T, R, spec = MATCH_CASES[case]
+    I = match_input(oracle, 4000 + case, rows, cols, spec)
+    e = oracle.enum_table(W)
+    a = oracle.match_encode(I, cols, W, T, R, e, want_stream=False)
+    b = ref.match_loop(I, cols, W, T, R, e)
+    for k in ("besti", "bestj", "bestd", "weights", "residual"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in ("modes", "matches", "bits_match", "bits_nomatch", "L"):
+        assert a[k] == b[k], k
+    if spec[0] == "periodic":
+        assert a["matches"] > 0  # the inputs exercise the match branch
