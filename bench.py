@@ -32,7 +32,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c1m", "c2", "c3", "c4", "c5"])
     ap.add_argument("--rows", type=int, default=0, help="override image rows (c3/c2/c5)")
     ap.add_argument("--cols", type=int, default=0, help="override image cols")
     ap.add_argument("--cpu-rows", type=int, default=16384, help="rows per plane in the CPU baseline sample")
@@ -419,12 +419,70 @@ class C1(C3):
         return dt * self.candidates(self.rows) / max(1, self.candidates(rows)), dt, kind
 
 
+class C1M(C1):
+    """compress7_test.cpp's whole tile loop with its default search window (W = 16, T = 0,
+    R = 128) on configs[0]'s 512x512 plane: causal match search over the residual image, modes,
+    write-back, the two Golomb coders (§8 f2). The input is a synthetic text-like page (glyphs of a
+    small random alphabet), the kind of image the match search is for; value = pixels per second."""
+
+    def __init__(self, ctx, args, rank):
+        import pybic
+        from oracle_lib import text_plane  # input generator only (numpy); not the checker
+        self.ctx, self.pybic = ctx, pybic
+        self.rows = args.rows or 512
+        self.cols = args.cols or 512
+        self.W, self.T, self.R = 16, 0, 128
+        self.nplanes = 1
+        self.wpr = (self.cols + 63) // 64
+        self.host = text_plane(0x5EED + rank, self.rows, self.cols)
+        self.planes = ctx.to_dev(self.host)[None]
+        self.enuml = pybic.enum_table(self.W)
+        self.resid = ctx.empty_i64(self.rows, self.wpr)
+        self.res = None
+        self.k = 0
+        self.pixels = self.rows * self.cols
+        self.workload = (f"c1m: {self.rows}x{self.cols} text-like plane, compress7_test tile loop, "
+                         f"W = {self.W}, T = {self.T}, R = {self.R}")
+
+    def step(self):
+        self.res = self.ctx.match_encode(self.planes[0], self.cols, self.W, self.T, self.R, self.enuml,
+                                         resid=self.resid)
+        self.k += 1
+
+    def out_bytes(self):
+        st = self.pybic.as_u64(self.res["stats"])
+        return (int(st[1]) + int(st[2]) + int(st[3])) / 8.0
+
+    def check(self, oracle):
+        exp = oracle.match_encode(self.host, self.cols, self.W, self.T, self.R, self.enuml)
+        st = [int(x) for x in self.pybic.as_u64(self.res["stats"])]
+        return (st == [exp["matches"], exp["bits_match"], exp["bits_nomatch"], exp["L"]] and
+                bool((self.pybic.as_u64(self.resid) == exp["residual"]).all()))
+
+    def cpu_time(self, rows):
+        """the driver's loop over the reference's own objects (oracle/_ref), whole image"""
+        from oracle_lib import Oracle, Ref, have_ref
+        impl, kind = (Ref(), "reference") if have_ref() else (Oracle(), "port")
+        t0 = time.perf_counter()
+        if kind == "reference":
+            impl.match_loop(self.host, self.cols, self.W, self.T, self.R, self.enuml)
+        else:
+            impl.match_encode(self.host, self.cols, self.W, self.T, self.R, self.enuml, want_stream=False)
+        dt = time.perf_counter() - t0
+        return dt, dt, kind
+
+
 # ------------------------------------------------------------------------------------------
 def cpu_baseline(wl, args):
     """The reference's own bit-serial med + GolombCoder + EGCoder (oracle/_ref, kind
     "reference") -- or the oracle restatement ("port") where _ref was not built -- on a bounded
     sample of the same workload, OpenMP over independent planes, on this host's cores."""
     from oracle_lib import Oracle, Ref, have_ref
+    if isinstance(wl, C1M):
+        est, dt, kind = wl.cpu_time(wl.rows)
+        return {"value": wl.pixels / est / 1e6, "unit": "MPix/s", "cores": 1, "kind": kind,
+                "sample": f"the whole {wl.rows}x{wl.cols} loop once ({dt:.1f} s, single thread: the loop is "
+                          f"serial)"}
     if isinstance(wl, C1):
         sample_rows = min(wl.rows, 120)
         est, dt, kind = wl.cpu_time(sample_rows)
@@ -478,6 +536,8 @@ def main():
         wl = C4(ctx, args, rank, world)
     elif args.workload == "c1":
         wl = C1(ctx, args, rank)
+    elif args.workload == "c1m":
+        wl = C1M(ctx, args, rank)
     else:
         wl = C5(ctx, args, rank, world)
     dev = ctx.dev
@@ -525,7 +585,8 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong" if args.workload in ("c4", "c5") else "weak", "vs_baseline": None, "dtype": "u64",
-            "data": "synthetic (seeded uniform bytes / Bernoulli(0.5) words, device-resident)",
+            "data": ("synthetic text-like page (seeded glyph alphabet), device-resident" if args.workload == "c1m"
+                     else "synthetic (seeded uniform bytes / Bernoulli(0.5) words, device-resident)"),
             "config": {"workload": wl.workload, "rows": wl.rows, "cols": wl.cols, "planes_per_gpu": wl.nplanes,
                        "parallelism": {"c4": f"dp{world} (64 frames sharded)",
                                        "c5": f"dp{world} (tile-row bands, coder state exchanged)"}.get(

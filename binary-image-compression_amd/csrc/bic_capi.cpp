@@ -33,6 +33,11 @@ struct bic_ctx {
   uint64_t* staging = nullptr;    // pinned host staging for lentab
   size_t staging_cap = 0;         // entries
   std::vector<uint64_t> lentab_host;  // what ctx->lentab holds
+  double* enuml = nullptr;        // device copy of the match loop's enumL table
+  double* enuml_staging = nullptr;  // pinned host staging for it
+  size_t enuml_cap = 0;           // entries
+  std::vector<double> enuml_host;  // what ctx->enuml holds
+  unsigned match_parts = 0;       // bic_set_match_parts: workgroups per tile (0 = by region size)
   // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
   bool prof_on = false;
   bool force_multipass = false;
@@ -172,6 +177,8 @@ int bic_ctx_destroy(bic_ctx* ctx) {
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->flags) (void)hipFree(ctx->flags);
+  if (ctx->enuml) (void)hipFree(ctx->enuml);
+  if (ctx->enuml_staging) (void)hipHostFree(ctx->enuml_staging);
   if (ctx->lut) (void)hipFree(ctx->lut);
   if (ctx->lentab) (void)hipFree(ctx->lentab);
   if (ctx->staging) (void)hipHostFree(ctx->staging);
@@ -471,6 +478,79 @@ int bic_patch_search(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
     bic::launch_patch_search(ctx->cur, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, W, besti, bestj, bestd);
   });
   BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_match_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                     unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                     uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid,
+                     uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!plane || !resid || !enuml || !stream_match || !stream_nomatch || !stats || cap_words == 0)
+    return BIC_EINVAL;
+  if (W < 1 || W > 64 || rows % W || cols % W || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (R > 32767 || T > 0x7fffffffu || rows > 0x3fffffffu || cols > 0x3fffffffu) return BIC_EINVAL;
+  const size_t M = (size_t)W * W;
+  const size_t ntiles = (rows / W) * (cols / W);
+  if (ntiles >= 0x80000000ull / 64 || (unsigned long long)ntiles * M >= 0x80000000ull) return BIC_EINVAL;
+  for (size_t w = 0; w <= M; ++w)
+    if (!(enuml[w] >= 0.0 && enuml[w] < 1e15)) return BIC_EINVAL;  // lengths stay exact in double
+  if (ctx->enuml_host.size() != M + 1 || std::memcmp(ctx->enuml_host.data(), enuml, (M + 1) * sizeof(double)) != 0) {
+    BIC_HIP(hipStreamSynchronize(ctx->cur));  // the previous copy out of the staging buffer is done
+    if (ctx->enuml_cap < M + 1) {
+      if (ctx->enuml_staging) (void)hipHostFree(ctx->enuml_staging);
+      if (ctx->enuml) (void)hipFree(ctx->enuml);
+      ctx->enuml_staging = nullptr;
+      ctx->enuml = nullptr;
+      ctx->enuml_cap = 0;
+      if (hipHostMalloc(&ctx->enuml_staging, (M + 1) * sizeof(double)) != hipSuccess) return BIC_ENOMEM;
+      if (hipMalloc(&ctx->enuml, (M + 1) * sizeof(double)) != hipSuccess) return BIC_ENOMEM;
+      ctx->enuml_cap = M + 1;
+    }
+    std::memcpy(ctx->enuml_staging, enuml, (M + 1) * sizeof(double));
+    BIC_HIP(hipMemcpyAsync(ctx->enuml, ctx->enuml_staging, (M + 1) * sizeof(double), hipMemcpyHostToDevice,
+                           ctx->cur));
+    ctx->enuml_host.assign(enuml, enuml + M + 1);
+  }
+  if (ntiles == 0) {
+    BIC_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(uint64_t), ctx->cur));
+    return BIC_OK;
+  }
+  const bic::MatchSched sched = bic::match_schedule(W, R, (uint32_t)cols, ctx->match_parts);
+  if ((rc = ensure_scratch(ctx, bic::match_scratch_bytes(ntiles, sched)))) return rc;
+  if (resid != plane)
+    BIC_HIP(hipMemcpyAsync(resid, plane, rows * wpr * sizeof(uint64_t), hipMemcpyDeviceToDevice, ctx->cur));
+  bic::MatchArgs a{};
+  a.I = resid;
+  a.rows = (uint32_t)rows;
+  a.cols = (uint32_t)cols;
+  a.wpr = (uint32_t)wpr;
+  a.used = (uint32_t)((cols + 63) / 64);
+  a.W = W;
+  a.nx = (uint32_t)(cols / W);
+  a.ny = (uint32_t)(rows / W);
+  a.T = T;
+  a.R = (int)R;
+  a.enuml = ctx->enuml;
+  a.besti = besti;
+  a.bestj = bestj;
+  a.bestd = bestd;
+  a.weights = weights;
+  a.modes = modes;
+  a.flags = ctx->flags;
+  timed(ctx, "match_tiles", [&] { bic::launch_match_tiles(ctx->cur, a, sched, ctx->scratch); });
+  timed(ctx, "match_code", [&] {
+    bic::launch_match_code(ctx->cur, a, reinterpret_cast<unsigned long long*>(stream_match),
+                           reinterpret_cast<unsigned long long*>(stream_nomatch), cap_words, stats);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_set_match_parts(bic_ctx* ctx, unsigned parts) {
+  if (!ctx) return BIC_EINVAL;
+  ctx->match_parts = parts;
   return BIC_OK;
 }
 

@@ -111,6 +111,35 @@ constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2;
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
                          uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
 
+// compress7_test.cpp:117-275 with a search window (bic_match.hip). The plane I is modified in
+// place. Per-tile outputs left null are carved from the scratch by launch_match_tiles.
+struct MatchArgs {
+  uint64_t* I;
+  uint32_t rows, cols, wpr, used, W, nx, ny, T;
+  int R;
+  uint32_t G;                       // tile schedule: workgroups per tile
+  uint32_t H, K;                    // team schedule: helpers per tile row; tiles of slack
+  const double* enuml;              // device, W*W+1
+  uint32_t* counter;                // scratch: ticket
+  unsigned long long* key;          // scratch: per tile min key
+  uint32_t* done;                   // scratch: per tile
+  uint32_t* arrive;                 // scratch: per tile
+  uint32_t* lens;                   // scratch: per tile chosen length
+  uint32_t *besti, *bestj, *bestd, *weights;
+  uint8_t* modes;
+  uint32_t* flags;
+};
+constexpr uint32_t kSchedTiles = 0, kSchedRows = 1, kSchedTeam = 2;
+struct MatchSched {
+  uint32_t kind, G, H, K;
+};
+// code: 0 auto; 1..256 workgroups per tile; 0x10000 | H a team of 1 + H workgroups per tile row;
+// anything else: per-tile workgroups, count from W and R
+MatchSched match_schedule(uint32_t W, uint32_t R, uint32_t cols, uint32_t code);
+size_t match_scratch_bytes(size_t ntiles, const MatchSched& m);
+void launch_match_tiles(hipStream_t s, MatchArgs& a, const MatchSched& m, void* scratch);
+void launch_match_code(hipStream_t s, const MatchArgs& a, unsigned long long* out_m, unsigned long long* out_n,
+                       size_t cap_words, uint64_t* stats);
 void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* raster_out, const uint64_t* plane_in,
                 uint64_t* plane_out, uint32_t rows, uint32_t cols, uint32_t wpr);
 

@@ -26,7 +26,7 @@ EXPORTS = [
     "bic_encode_planes", "bic_encode_planes2", "bic_ctx_set_option", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
-    "bic_patch_search",
+    "bic_patch_search", "bic_match_encode", "bic_set_match_parts",
 ]
 
 
@@ -90,6 +90,8 @@ def load(path=LIB_PATH):
     sig("bic_pbm_unpack", i32, [vp, vp, sz, sz, vp, sz])
     sig("bic_pbm_pack", i32, [vp, vp, sz, sz, sz, vp])
     sig("bic_patch_search", i32, [vp, vp, sz, sz, sz, u32, vp, vp, vp])
+    sig("bic_match_encode", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
+    sig("bic_set_match_parts", i32, [vp, u32])
     _lib = L
     return L
 
@@ -296,6 +298,31 @@ class Context:
                   "bic_patch_search")
         return tuple(out)
 
+    def match_encode(self, plane, cols, W, T=0, R=128, enuml=None, cap_words=None, resid=None):
+        """compress7_test.cpp's tile loop with search window R and threshold T (bic_match_encode).
+        plane: int64 [rows, wpr] device tensor (not modified); enuml: numpy float64 [W*W+1] (host),
+        default enumL from this build. Returns device tensors per tile and the two streams."""
+        rows, wpr = plane.shape
+        nt = (rows // W) * (cols // W)
+        t = self.torch
+        bi, bj, bd, wt = (t.empty(nt, dtype=t.int32, device=self.dev) for _ in range(4))
+        modes = t.empty(nt, dtype=t.uint8, device=self.dev)
+        resid = self.empty_i64(rows, wpr) if resid is None else resid
+        cap_words = cap_words or max(1, (rows * cols + 33 * nt + 63) // 64 + 1)
+        sm, sn = self.empty_i64(cap_words), self.empty_i64(cap_words)
+        stats = self.empty_i64(4)
+        e = enum_table(W) if enuml is None else np.ascontiguousarray(enuml, np.float64)
+        self._bind_stream()
+        self._chk(self.lib.bic_match_encode(self.h, _p(plane), rows, cols, wpr, W, T, R,
+                                            e.ctypes.data_as(C.c_void_p), _p(bi), _p(bj), _p(bd), _p(wt),
+                                            _p(modes), _p(resid), _p(sm), _p(sn), cap_words, _p(stats)),
+                  "bic_match_encode")
+        return dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes, resid=resid, stream_match=sm,
+                    stream_nomatch=sn, stats=stats)
+
+    def set_match_parts(self, parts):
+        self._chk(self.lib.bic_set_match_parts(self.h, parts), "bic_set_match_parts")
+
     def pbm_unpack(self, raster, rows, cols, wpr=None):
         """P4 raster bytes (uint8 device tensor, rows x ceil(cols/8)) -> int64 plane [rows, wpr]."""
         wpr = wpr or (cols + 63) // 64
@@ -325,6 +352,12 @@ class Context:
 def enum_codelength(n, r):
     """log2 C(n, r) (coding.h enumerative_codelength), host-side, from libbic.so."""
     return float(load().bic_enum_codelength(n, r))
+
+
+def enum_table(W):
+    """enumL(W*W, w) for w = 0..W*W (float64), the table bic_match_encode takes."""
+    f = load().bic_enum_codelength
+    return np.array([f(W * W, w) for w in range(W * W + 1)], np.float64)
 
 
 def lentab(W):

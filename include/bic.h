@@ -143,6 +143,34 @@ int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
 int bic_patch_search(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
                      uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
 
+/* ---- compress7_test.cpp:117-275 with a search window --------------------------
+ * The driver's whole tile loop with its arguments W (argv[2]), T (argv[3]) and R (argv[4]): per W x W
+ * tile in raster order, the least-distance window of the causal search region of the image as the
+ * residual write-back of every earlier tile left it (rows i0 .. i0-W at columns j0-W .. j0-R, then
+ * rows i0-W .. i0-R at columns j0+R .. j0-R, scanned downwards, stopping at the first distance
+ * <= T), the four candidate lengths (2 + enumL, plus ceil(log2(search_win_size)) for a match), the
+ * mode 'X' / 'x' (match, med or not) or 'O' / 'o' (no match), the chosen weight coded by
+ * golomb_match or golomb_nomatch, and the residual written back.
+ *   plane: device, rows x wpr, not modified; resid: device, rows x wpr, receives the image after
+ *   the loop (may equal plane). enuml: HOST array of W*W+1 doubles, enuml[w] = enumL(W*W, w)
+ *   (bic_enum_codelength, or the caller's GSL values). Requires 1 <= W <= 64, rows % W == 0,
+ *   cols % W == 0, R <= 32767. Per tile (device, each nullable): besti, bestj, bestd (W*W+1 when
+ *   the region holds no window), weights (the coded weight), modes. stream_match / stream_nomatch:
+ *   device, cap_words each, the two coders' codewords. stats: device u64[4]: matches, bits of
+ *   golomb_match, bits of golomb_nomatch, sum of the chosen lengths (the driver's L before it adds
+ *   the two bitcounts). A search_win_size <= 0 (whose log2 the driver converts with undefined
+ *   behaviour; 2^63 on x86-64) makes a match impossible for that tile. */
+int bic_match_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                     unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                     uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid,
+                     uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats);
+/* Schedule of bic_match_encode (every schedule gives the same result): 0 (default) = automatic;
+ * N in 1..256 = N workgroups per tile, tiles in raster order with flags between them;
+ * 0x10000 | H = one workgroup per tile row walking its tiles, plus H helper workgroups that search
+ * ahead of it (W of 8, 16 or 32 and a band of (R + 2W) x (cols/32 + 2) 32-bit words <= 30 Ki; other
+ * W: the row workgroup alone); other values: per-tile workgroups, count from W and R. */
+int bic_set_match_parts(bic_ctx* ctx, unsigned parts);
+
 /* log2 C(n, r) (enumerative_codelength, coding.cpp:19-22) computed without GSL, and the tile
  * length table lentab[w] = (uint64)(2 + log2 C(W*W, w)) for w = 0..W*W (host memory, W*W+1
  * entries) that bic_patch_encode takes. Host-side helpers; no device needed. */

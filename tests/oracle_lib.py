@@ -336,3 +336,21 @@ def periodic_plane(seed, rows, cols, ph, pw, p=0.5, flip=0.0):
     if flip:
         bits ^= rng.random((rows, cols)) < flip
     return pack_rows(bits)
+
+
+def text_plane(seed, rows, cols, glyph_h=11, glyph_w=7, advance=8, line=16, nglyphs=40, p=0.45, space=0.15):
+    """A synthetic bilevel 'text' page: lines of glyphs drawn from a small random alphabet at a
+    fixed advance, with word gaps -- repeated shapes at offsets unrelated to the tile grid, the
+    kind of input compress7's match search is for."""
+    rng = np.random.default_rng(seed)
+    alpha = rng.random((nglyphs, glyph_h, glyph_w)) < p
+    bits = np.zeros((rows, cols), bool)
+    top = 2
+    while top + glyph_h <= rows:
+        x = 3 + int(rng.integers(0, advance))
+        while x + glyph_w <= cols:
+            if rng.random() >= space:
+                bits[top:top + glyph_h, x:x + glyph_w] = alpha[int(rng.integers(0, nglyphs))]
+            x += advance
+        top += line
+    return pack_rows(bits)
