@@ -17,6 +17,7 @@
 #ifdef BIC_STAMPS
 namespace bic {
 int read_stamps(uint64_t* host, size_t n);
+int read_match_stamps(uint64_t* host, size_t n);
 }
 #endif
 
@@ -638,6 +639,7 @@ int bic_prof_collect(bic_ctx* ctx, char* buf, size_t cap) {
 
 #ifdef BIC_STAMPS
 int bic_debug_stamps(uint64_t* host, size_t n) { return bic::read_stamps(host, n); }
+int bic_debug_match_stamps(uint64_t* host, size_t n) { return bic::read_match_stamps(host, n); }
 #endif
 
 }  // extern "C"

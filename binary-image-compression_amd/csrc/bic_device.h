@@ -76,6 +76,50 @@ __device__ __forceinline__ int wave_min(int x) {
   return x;
 }
 
+// DPP wave reductions: four in-row steps (quad swaps, half-row and row mirrors: a few cycles each,
+// against ~50 for a ds_bpermute shuffle) leave every lane with its 16-lane row's total; the four row
+// totals are combined from readlanes. The result is wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_total_u32(uint32_t v) {
+  v += dpp_u32<0xB1>(v);   // quad_perm(1,0,3,2)
+  v += dpp_u32<0x4E>(v);   // quad_perm(2,3,0,1)
+  v += dpp_u32<0x141>(v);  // row_half_mirror
+  v += dpp_u32<0x140>(v);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_min_step(unsigned long long v) {
+  const uint32_t lo = dpp_u32<CTRL>((uint32_t)v), hi = dpp_u32<CTRL>((uint32_t)(v >> 32));
+  const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+  return o < v ? o : v;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  v = dpp_min_step<0xB1>(v);
+  v = dpp_min_step<0x4E>(v);
+  v = dpp_min_step<0x141>(v);
+  v = dpp_min_step<0x140>(v);
+  unsigned long long m = v;
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) {
+    const unsigned long long o = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), r) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, r);
+    m = o < m ? o : m;
+  }
+  const unsigned long long m0 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), 0) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 0);
+  return m0 < m ? m0 : m;
+}
+// lane i receives lane i-1's value, lane 0 receives 0 (DPP wave_shr:1)
+__device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, true);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Exclusive block scan for blockDim.x <= 1024 (<= 16 waves). tmp: >= 17 entries of LDS.
 template <typename T>
 __device__ __forceinline__ T block_excl_scan(T x, T* tmp, T& total) {

@@ -22,14 +22,42 @@
 
 namespace bic {
 
+#ifdef BIC_STAMPS  // diagnostic build only (make stamps): per-tile phase clocks of the row workgroup
+__device__ unsigned long long g_mstamps[1 << 20];
+#define MSTAMP(tile, slot)                                                                   \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+    if ((uint64_t)(tile) * 16 + (slot) < (1u << 20)) g_mstamps[(uint64_t)(tile) * 16 + (slot)] = t_; \
+  } while (0)
+int read_match_stamps(uint64_t* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mstamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+}
+#else
+#define MSTAMP(tile, slot) \
+  do {                     \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int kMB = 256;                 // threads per workgroup
 constexpr int kPerThread = 4;            // windows per thread per chunk
 constexpr uint32_t kChunk = kMB * kPerThread;
 constexpr uint32_t kRegionWords = 4096;  // LDS image of the search region (32 KiB)
+// A window's place in the reference's scan order is pos = loop << 32 | a << 16 | c (loop 0 or 1,
+// a = rows down from the loop's first row, c = columns left of its first column): increasing pos is
+// the scan order, and pos decodes to the window without a division. Keys order windows for the
+// reduction: (d <= T ? 0 : d) << 51 | pos << 13 | d.
 constexpr int kIdxShift = 13, kDpShift = 51;
 constexpr uint64_t kIdxMask = (1ull << 38) - 1;
+
+__device__ __forceinline__ uint64_t scan_pos(uint32_t loop, uint32_t a, uint32_t c) {
+  return ((uint64_t)loop << 32) | ((uint64_t)a << 16) | c;
+}
+__device__ __forceinline__ unsigned long long make_key(uint32_t d, uint32_t T, uint64_t pos) {
+  return ((unsigned long long)(d <= T ? 0u : d) << kDpShift) | ((unsigned long long)pos << kIdxShift) | d;
+}
+__device__ __forceinline__ uint64_t key_pos(unsigned long long key) { return (key >> kIdxShift) & kIdxMask; }
 
 struct Region {
   int i0, j0, mini, minj, maxj, mini2, maxj2;
@@ -64,19 +92,47 @@ __device__ __forceinline__ Region make_region(const MatchArgs& a, uint32_t t) {
   return g;
 }
 
-// scan index -> window origin: loop 1 walks i2 = i0 .. mini2 and j2 = maxj2 .. minj, loop 2
-// i2 = i0-W .. mini and j2 = maxj .. minj (:138-174)
-__device__ __forceinline__ void window_pos(const Region& g, int W, uint32_t idx, int& i2, int& j2) {
+// Loop 1 walks i2 = i0 .. mini2 and j2 = maxj2 .. minj, loop 2 i2 = i0-W .. mini and
+// j2 = maxj .. minj (:138-174). Flat scan index -> position (the per-tile schedule splits flat ranges).
+__device__ __forceinline__ uint64_t flat_pos(const Region& g, uint32_t idx) {
   if (idx < g.n1) {
     const uint32_t q = idx / g.n1c;
-    i2 = g.i0 - (int)q;
-    j2 = g.maxj2 - (int)(idx - q * g.n1c);
-  } else {
-    idx -= (uint32_t)g.n1;
-    const uint32_t q = idx / g.n2c;
-    i2 = g.i0 - W - (int)q;
-    j2 = g.maxj - (int)(idx - q * g.n2c);
+    return scan_pos(0, q, idx - q * g.n1c);
   }
+  idx -= (uint32_t)g.n1;
+  const uint32_t q = idx / g.n2c;
+  return scan_pos(1, q, idx - q * g.n2c);
+}
+__device__ __forceinline__ void pos_window(const Region& g, int W, uint64_t pos, int& i2, int& j2) {
+  const int a = (int)((pos >> 16) & 0xffff), c = (int)(pos & 0xffff);
+  if (pos >> 32) {
+    i2 = g.i0 - W - a;
+    j2 = g.maxj - c;
+  } else {
+    i2 = g.i0 - a;
+    j2 = g.maxj2 - c;
+  }
+}
+
+// Cross-workgroup hand-offs without cache maintenance. An agent-scope release / acquire costs an L2
+// write-back (buffer_wbl2) / invalidation (buffer_inv) of the whole XCD per hand-off -- microseconds,
+// and under the feet of every other workgroup on it. Instead everything one workgroup writes for
+// another (image words, flags, progress) is stored with agent-scope atomic stores, which go to the
+// coherence point (sc1), and read with agent-scope atomic loads, which do not hit stale lines; a
+// producer waits for its stores to be acknowledged (s_waitcnt vmcnt(0)) before it raises a flag, and
+// a consumer issues its data loads only after it has seen the flag.
+__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_word(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_word(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0); }
+__device__ __forceinline__ void raise_flag(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // W bits of row `row` from column `col`, MSB-aligned, from the LDS image or the plane
@@ -90,17 +146,12 @@ __device__ __forceinline__ uint64_t row_bits(const MatchArgs& a, const Region& g
   } else {
     const uint32_t w = (uint32_t)col >> 6, sh = (uint32_t)col & 63;
     const uint64_t* p = a.I + (uint64_t)row * a.wpr + w;
-    const uint64_t hi = p[0];
-    const uint64_t lo = (sh && w + 1 < a.used) ? p[1] : 0;
+    const uint64_t hi = ld_word(p);
+    const uint64_t lo = (sh && w + 1 < a.used) ? ld_word(p + 1) : 0;
     return (hi << sh) | ((lo >> 1) >> (63 - sh));
   }
 }
 
-// polled with relaxed loads: an acquire load per poll would invalidate the XCD's L2 each time,
-// under the feet of the workgroups doing the searches; one acquire fence follows the wait
-__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // The tile's decision (:184-272), one lane per tile row r (lanes r >= W pass p = b = 0): p = tile
 // row, b = row of the best window (0 when the region is empty), both MSB-aligned W bits. Writes the
@@ -111,15 +162,14 @@ __device__ uint64_t decide_tile(const MatchArgs& a, const double* enuml, const R
   const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
   const uint64_t p3 = p ^ b;
   // med inside the tile (compress7_test.cpp:43-55; (0,0) is never written: 0 here)
-  uint64_t pu = shfl_up_u64(p, 1), p3u = shfl_up_u64(p3, 1);
-  if (r == 0) pu = p3u = 0;
+  const uint64_t pu = wave_shr1_u64(p), p3u = wave_shr1_u64(p3);  // the row above (0 for row 0)
   const uint64_t D = p ^ pu, D3 = p3 ^ p3u;
   const uint64_t lane_mask = r < W ? topW & (r == 0 ? ~BIC_MSB : ~0ull) : 0ull;
   const uint64_t dp = (D ^ (D >> 1)) & lane_mask, dp3 = (D3 ^ (D3 >> 1)) & lane_mask;
-  const uint32_t w_nn = (uint32_t)wave_sum_u64(__popcll(p));
-  const uint32_t w_mn = (uint32_t)wave_sum_u64(__popcll(p3));
-  const uint32_t w_np = (uint32_t)wave_sum_u64(__popcll(dp));
-  const uint32_t w_mp = (uint32_t)wave_sum_u64(__popcll(dp3));
+  // the four weights in 16-bit fields (each <= 64 * 64), two DPP reductions
+  const uint32_t s0 = wave_total_u32((uint32_t)__popcll(p) | (uint32_t)__popcll(p3) << 16);
+  const uint32_t s1 = wave_total_u32((uint32_t)__popcll(dp) | (uint32_t)__popcll(dp3) << 16);
+  const uint32_t w_nn = s0 & 0xffff, w_mn = s0 >> 16, w_np = s1 & 0xffff, w_mp = s1 >> 16;
   // lengths (:212-221) in double, converted to idx_t like the driver
   const uint64_t nn_len = (uint64_t)(2.0 + enuml[w_nn]), np_len = (uint64_t)(2.0 + enuml[w_np]);
   uint64_t mn_len = ~0ull, mp_len = ~0ull;  // search_win_size <= 0: log2 -> 2^63, never a match
@@ -156,7 +206,7 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
     for (uint32_t e = tid; e < nw; e += kMB) {
       const uint32_t r = e / g.stride, c = e - r * g.stride;
       const uint32_t wc = (uint32_t)g.wlo + c;
-      S[e] = (c + 1 < g.stride && wc < a.used) ? a.I[(uint64_t)(g.rlo + (int)r) * a.wpr + wc] : 0ull;
+      S[e] = (c + 1 < g.stride && wc < a.used) ? ld_word(a.I + (uint64_t)(g.rlo + (int)r) * a.wpr + wc) : 0ull;
     }
     __syncthreads();
   }
@@ -173,33 +223,29 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
       const uint64_t idx = base + (uint32_t)q * kMB + tid;
       if (idx < hi) {
         int i2, j2;
-        window_pos(g, W, (uint32_t)idx, i2, j2);
+        const uint64_t pos = flat_pos(g, (uint32_t)idx);
+        pos_window(g, W, pos, i2, j2);
         uint32_t d = 0;
         for (int r = 0; r < W; ++r) d += (uint32_t)__popcll((row_bits<LDS>(a, g, S, i2 + r, j2) ^ Pl[r]) & topW);
-        const unsigned long long key = ((unsigned long long)(d <= a.T ? 0u : d) << kDpShift) |
-                                       ((unsigned long long)idx << kIdxShift) | d;
+        const unsigned long long key = make_key(d, a.T, pos);
         best = key < best ? key : best;
       }
     }
     int stop = (best >> kDpShift) == 0;
     if ((chunk & 7) == 7 && tid == 0 && !stop) {  // a lower part already found one
       const unsigned long long k = __hip_atomic_load(&a.key[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      stop = (k >> kDpShift) == 0 && ((k >> kIdxShift) & kIdxMask) < base;
+      stop = (k >> kDpShift) == 0 && key_pos(k) < flat_pos(g, (uint32_t)base);
     }
     if (__syncthreads_or(stop)) break;
   }
-#pragma unroll
-  for (int dd = 32; dd >= 1; dd >>= 1) {
-    const unsigned long long o = shfl_u64(best, lane_id() ^ dd);
-    best = o < best ? o : best;
-  }
+  best = wave_min_u64(best);
   if (lane_id() == 0) red[tid >> 6] = best;
   __syncthreads();
   if (tid == 0) {
     for (int w = 1; w < kMB / 64; ++w) best = red[w] < best ? red[w] : best;
     best = red[0] < best ? red[0] : best;
     if (best != ~0ull) atomicMin(&a.key[t], best);
-    __threadfence();
+    stores_done();
     const uint32_t old = atomicAdd(&a.arrive[t], 1u);
     sh_last = old + 1 == a.G;
   }
@@ -207,7 +253,6 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
   if (!sh_last || tid >= 64) return;
 
   // ---- the last workgroup finishes the tile (one lane per tile row) ----
-  __threadfence();
   const unsigned long long key = __hip_atomic_load(&a.key[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int r = (int)tid;
   const uint32_t M = (uint32_t)(W * W);
@@ -215,7 +260,7 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
   int bi = 0, bj = 0;
   if (key != ~0ull) {  // :184-189 (any window at all beats M + 1)
     bd = (uint32_t)(key & 0x1fff);
-    window_pos(g, W, (uint32_t)((key >> kIdxShift) & kIdxMask), bi, bj);
+    pos_window(g, W, key_pos(key), bi, bj);
   }
   const uint64_t p = r < W ? Pl[r] : 0ull;
   const uint64_t b = (key != ~0ull && r < W) ? (row_bits<LDS>(a, g, S, bi + r, bj) & topW) : 0ull;
@@ -224,11 +269,11 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
   if (r < W) {
     uint64_t* row = a.I + (uint64_t)(g.i0 + r) * a.wpr + (g.j0 >> 6);
     const uint32_t sh = (uint32_t)g.j0 & 63;
-    row[0] = (row[0] & ~(topW >> sh)) | (res >> sh);
-    if (sh + (uint32_t)W > 64) row[1] = (row[1] & ~(topW << (64 - sh))) | (res << (64 - sh));
+    st_word(row, (ld_word(row) & ~(topW >> sh)) | (res >> sh));
+    if (sh + (uint32_t)W > 64) st_word(row + 1, (ld_word(row + 1) & ~(topW << (64 - sh))) | (res << (64 - sh)));
   }
-  __threadfence();
-  if (r == 0) __hip_atomic_store(&a.done[t], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  stores_done();
+  if (r == 0) raise_flag(&a.done[t], 1u);
 }
 
 __global__ __launch_bounds__(kMB) void k_match_tiles(MatchArgs a) {
@@ -262,7 +307,6 @@ __global__ __launch_bounds__(kMB) void k_match_tiles(MatchArgs a) {
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const uint32_t t = sh_q / a.G, part = sh_q % a.G;
   const Region g = make_region(a, t);
   if (g.nrows * g.stride <= kRegionWords)
@@ -280,8 +324,6 @@ __global__ __launch_bounds__(kMB) void k_match_tiles(MatchArgs a) {
 // write-backs; the rows above are (re)loaded column by column as the row above completes them.
 constexpr int kRB = 1024;
 constexpr uint32_t kRowLds = 30 * 1024;  // u32 words of the band image (120 KiB)
-// windows (consecutive i2) per search task: the extracted rows stay in registers
-template <int KW> constexpr int group_rows() { return KW >= 32 ? 4 : 8; }
 
 struct Band {
   int i0, lo;            // first tile row pixel, first band row
@@ -315,35 +357,36 @@ __device__ __forceinline__ void band_load(uint32_t* L, const Band& b, const Matc
                                           uint32_t w0, uint32_t w1) {
   if (r1 <= r0 || w1 <= w0) return;
   const uint32_t nw = w1 - w0, n = (uint32_t)(r1 - r0) * nw;
-  const uint32_t* I32 = reinterpret_cast<const uint32_t*>(a.I);
+  const uint32_t* I32 = reinterpret_cast<const uint32_t*>(a.I);  // other workgroups' stores: atomic loads
   for (uint32_t e = threadIdx.x; e < n; e += kRB) {
     const uint32_t rr = e / nw, w = w0 + (e - rr * nw);
     const int row = r0 + (int)rr;
     // u32 column w is the high (even w) or low half of u64 word w/2 (little-endian in memory)
-    L[(uint32_t)(row - b.lo) * b.pitch + w] = I32[((uint64_t)row * a.wpr + (w >> 1)) * 2 + ((w & 1) ^ 1)];
+    L[(uint32_t)(row - b.lo) * b.pitch + w] =
+        ld_relaxed(I32 + ((uint64_t)row * a.wpr + (w >> 1)) * 2 + ((w & 1) ^ 1));
   }
 }
 
 // Tasks [t0, t1) of one search loop of the reference (i2 = i_top - a for a < nrows, j2 = j_top - c for
-// c < ncols, scan index idx_base + a * idx_stride + c). Task t = (g, c) = (t / ncols, t % ncols) covers
+// c < ncols, position scan_pos(loop, a, c)). Task t = (g, c) = (t / ncols, t % ncols) covers
 // the kGK windows a = g*kGK .. g*kGK+kGK-1 down one column, whose kGK + KW - 1 rows are extracted once
 // into registers. Tasks with g*kGK < skip_a and c < skip_c are left out (another workgroup's share).
 // Chunks of kRB tasks; the scan stops once the best key has distance <= T and a scan index below
 // every window left (every window a later call of this workgroup scans has a larger index).
-template <int KW>
-__device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, const uint32_t* P, uint32_t T,
-                                           int i_top, uint32_t nrows, int j_top, uint32_t ncols,
-                                           uint32_t idx_base, uint32_t idx_stride, uint32_t t0, uint32_t t1,
-                                           uint32_t skip_a, uint32_t skip_c, unsigned long long& best,
-                                           bool& stop) {
-  constexpr int kGK = group_rows<KW>();
+template <int KW, int kGK>
+__device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, const uint32_t* PW, uint32_t T,
+                                           int i_top, uint32_t nrows, int j_top, uint32_t ncols, uint32_t loop,
+                                           uint32_t t0, uint32_t t1, uint32_t skip_a, uint32_t skip_c,
+                                           unsigned long long& best, bool& stop) {
+  // 32/KW consecutive rows of KW bits share one 32-bit word, so a window's distance is KW/(32/KW)
+  // xor + popcount pairs (PW: the tile's rows packed the same way)
+  constexpr int kPack = 32 / KW, kNW = KW / kPack, kNE = kGK + KW - 1, kNP = kNE - kPack + 1;
   if (stop || t1 <= t0 || ncols == 0) return;
-  // the tile's rows: in registers up to 16 of them, else read from LDS (one broadcast word)
-  constexpr bool kHoist = KW <= 16;
-  uint32_t Pr[kHoist ? KW : 1];
+  constexpr bool kHoist = kNW <= 8;  // packed tile rows in registers, else read from LDS (broadcast)
+  uint32_t Pr[kHoist ? kNW : 1];
   if constexpr (kHoist) {
 #pragma unroll
-    for (int r = 0; r < KW; ++r) Pr[r] = P[r];
+    for (int r = 0; r < kNW; ++r) Pr[r] = PW[r];
   }
   for (uint32_t base = t0; base < t1; base += kRB) {
     const uint32_t task = base + threadIdx.x;
@@ -354,22 +397,28 @@ __device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, co
         const int j2 = j_top - (int)c;
         const uint32_t kk = min((uint32_t)kGK, nrows - a0);
         const int ybase = i_top - (int)a0 - (kGK - 1);  // band row of e[0]
-        uint32_t e[kGK + KW - 1];
+        uint32_t e[kNE];
 #pragma unroll
-        for (int m = 0; m < kGK + KW - 1; ++m) {
+        for (int m = 0; m < kNE; ++m) {
           const int y = ybase + m;
           e[m] = y >= bd.lo ? band_bits<KW>(L, bd, y, j2) : 0u;
+        }
+        uint32_t pk[kNP];
+#pragma unroll
+        for (int m = 0; m < kNP; ++m) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int q = 0; q < kPack; ++q) v |= e[m + q] << (32 - KW * (q + 1));
+          pk[m] = v;
         }
 #pragma unroll
         for (int u = 0; u < kGK; ++u) {
           if ((uint32_t)u < kk) {
             uint32_t d = 0;
 #pragma unroll
-            for (int r = 0; r < KW; ++r)
-              d += (uint32_t)__popc(e[kGK - 1 - u + r] ^ (kHoist ? Pr[kHoist ? r : 0] : P[r]));
-            const uint32_t idx = idx_base + (a0 + (uint32_t)u) * idx_stride + c;
-            const unsigned long long key = ((unsigned long long)(d <= T ? 0u : d) << kDpShift) |
-                                           ((unsigned long long)idx << kIdxShift) | d;
+            for (int r = 0; r < kNW; ++r)
+              d += (uint32_t)__popc(pk[kGK - 1 - u + r * kPack] ^ (kHoist ? Pr[kHoist ? r : 0] : PW[r]));
+            const unsigned long long key = make_key(d, T, scan_pos(loop, a0 + (uint32_t)u, c));
             best = key < best ? key : best;
           }
         }
@@ -379,7 +428,7 @@ __device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, co
     bool s = (best >> kDpShift) == 0;
     if (s && nt < t1) {  // the first task left bounds the index of every window left
       const uint32_t g2 = nt / ncols, c2 = nt - g2 * ncols;
-      s = ((best >> kIdxShift) & kIdxMask) < idx_base + (uint64_t)g2 * kGK * idx_stride + c2;
+      s = key_pos(best) < scan_pos(loop, g2 * kGK, c2);
     }
     if (__syncthreads_or(s)) {
       stop = true;
@@ -388,20 +437,10 @@ __device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, co
   }
 }
 
-template <int KW>
-__device__ __forceinline__ void scan_loop_rows(const uint32_t* L, const Band& bd, const uint32_t* P, int i_top,
-                                               uint32_t nrows, int j_top, uint32_t ncols, uint32_t idx_base,
-                                               uint32_t T, unsigned long long& best, bool& stop) {
-  constexpr int kGK = group_rows<KW>();
-  const uint32_t ntasks = (nrows + kGK - 1) / kGK * ncols;
-  scan_tasks<KW>(L, bd, P, T, i_top, nrows, j_top, ncols, idx_base, ncols, 0, ntasks, 0, 0, best, stop);
-}
-
 // any W <= 64: one window per task
 __device__ __forceinline__ void scan_loop_any(const uint32_t* L, const Band& bd, const uint64_t* P, int W,
-                                              int i_top, uint32_t nrows, int j_top, uint32_t ncols,
-                                              uint32_t idx_base, uint32_t T, unsigned long long& best,
-                                              bool& stop) {
+                                              int i_top, uint32_t nrows, int j_top, uint32_t ncols, uint32_t loop,
+                                              uint32_t T, unsigned long long& best, bool& stop) {
   if (stop || nrows == 0 || ncols == 0) return;
   const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
   const uint32_t n = nrows * ncols;
@@ -412,12 +451,11 @@ __device__ __forceinline__ void scan_loop_any(const uint32_t* L, const Band& bd,
       const int i2 = i_top - (int)q, j2 = j_top - (int)(i - q * ncols);
       uint32_t d = 0;
       for (int r = 0; r < W; ++r) d += (uint32_t)__popcll((band_bits64(L, bd, i2 + r, j2) ^ P[r]) & topW);
-      const unsigned long long key = ((unsigned long long)(d <= T ? 0u : d) << kDpShift) |
-                                     ((unsigned long long)(idx_base + i) << kIdxShift) | d;
+      const unsigned long long key = make_key(d, T, scan_pos(loop, q, i - q * ncols));
       best = key < best ? key : best;
     }
     const uint32_t nt = base + kRB;
-    const bool s = (best >> kDpShift) == 0 && (nt >= n || ((best >> kIdxShift) & kIdxMask) < idx_base + nt);
+    const bool s = (best >> kDpShift) == 0 && (nt >= n || key_pos(best) < scan_pos(loop, nt / ncols, nt % ncols));
     if (__syncthreads_or(s)) {
       stop = true;
       return;
@@ -425,14 +463,12 @@ __device__ __forceinline__ void scan_loop_any(const uint32_t* L, const Band& bd,
   }
 }
 
-template <int KW>
 __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progress) {
   __shared__ uint32_t L[kRowLds];
   __shared__ uint64_t P64[64];
-  __shared__ uint32_t P32[64];
   __shared__ unsigned long long red[kRB / 64];
   __shared__ uint32_t sh_row;
-  const int W = KW ? KW : (int)a.W;
+  const int W = (int)a.W;
   const uint32_t tid = threadIdx.x;
   const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
   if (tid == 0) sh_row = atomicAdd(a.counter, 1u);
@@ -469,7 +505,6 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
             break;
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       __syncthreads();
       // the word holding column final_col + 1 may have been loaded before it was final: reload it
@@ -480,7 +515,6 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
     if (tid < (uint32_t)W) {
       const uint64_t pr = band_bits64(L, bd, bd.i0 + (int)tid, g.j0) & topW;
       P64[tid] = pr;
-      P32[tid] = (uint32_t)(pr >> (64 - (W > 32 ? 32 : W)));  // the low W bits when W <= 32
     }
     __syncthreads();
     unsigned long long best = ~0ull;
@@ -489,18 +523,9 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
     const uint32_t n1r = (uint32_t)(g.i0 - g.mini2 + 1);
     const int n2r_ = g.i0 - W - g.mini + 1;
     const uint32_t n2r = n2r_ > 0 ? (uint32_t)n2r_ : 0;
-    if constexpr (KW > 0) {
-      scan_loop_rows<KW>(L, bd, P32, g.i0, n1r, g.maxj2, g.n1c, 0, a.T, best, stop);
-      scan_loop_rows<KW>(L, bd, P32, g.i0 - W, n2r, g.maxj, g.n2c, (uint32_t)g.n1, a.T, best, stop);
-    } else {
-      scan_loop_any(L, bd, P64, W, g.i0, n1r, g.maxj2, g.n1c, 0, a.T, best, stop);
-      scan_loop_any(L, bd, P64, W, g.i0 - W, n2r, g.maxj, g.n2c, (uint32_t)g.n1, a.T, best, stop);
-    }
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-      const unsigned long long o = shfl_u64(best, lane_id() ^ dd);
-      best = o < best ? o : best;
-    }
+    scan_loop_any(L, bd, P64, W, g.i0, n1r, g.maxj2, g.n1c, 0, a.T, best, stop);
+    scan_loop_any(L, bd, P64, W, g.i0 - W, n2r, g.maxj, g.n2c, 1, a.T, best, stop);
+    best = wave_min_u64(best);
     if (lane_id() == 0) red[tid >> 6] = best;
     __syncthreads();
     if (tid < 64) {
@@ -511,7 +536,7 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
       int bi = 0, bj = 0;
       if (key != ~0ull) {
         bdist = (uint32_t)(key & 0x1fff);
-        window_pos(g, W, (uint32_t)((key >> kIdxShift) & kIdxMask), bi, bj);
+        pos_window(g, W, key_pos(key), bi, bj);
       }
       const uint64_t p = r < W ? P64[r] : 0ull;
       const uint64_t b = (key != ~0ull && r < W) ? (band_bits64(L, bd, bi + r, bj) & topW) : 0ull;
@@ -520,8 +545,8 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
         // write-back: the plane (for the rows below) and the band image (for the tiles to the right)
         uint64_t* row = a.I + (uint64_t)(g.i0 + r) * a.wpr + (g.j0 >> 6);
         const uint32_t sh = (uint32_t)g.j0 & 63;
-        row[0] = (row[0] & ~(topW >> sh)) | (res >> sh);
-        if (sh + (uint32_t)W > 64) row[1] = (row[1] & ~(topW << (64 - sh))) | (res << (64 - sh));
+        st_word(row, (ld_word(row) & ~(topW >> sh)) | (res >> sh));
+        if (sh + (uint32_t)W > 64) st_word(row + 1, (ld_word(row + 1) & ~(topW << (64 - sh))) | (res << (64 - sh)));
         uint32_t* q = L + (uint32_t)(g.i0 + r - bd.lo) * bd.pitch + ((uint32_t)g.j0 >> 5);
         const int s32 = g.j0 & 31;
 #pragma unroll
@@ -534,8 +559,8 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
           q[k] = (q[k] & ~m) | v;
         }
       }
-      __threadfence();
-      if (r == 0) __hip_atomic_store(&progress[ti], tj + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      stores_done();
+      if (r == 0) raise_flag(&progress[ti], tj + 1);
     }
     __syncthreads();
   }
@@ -556,12 +581,13 @@ constexpr unsigned long long kSlotSet = 1ull << 63;
 template <int KW>
 __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progress, unsigned long long* slots) {
   constexpr int W = KW;
-  constexpr int kGK = group_rows<KW>();
+  constexpr int kGK = 4;  // windows per helper task
   constexpr uint64_t topW = ~(~0ull >> W);
   __shared__ uint32_t L[kRowLds];
   __shared__ double E[KW * KW + 1];
   __shared__ uint64_t P64[KW];
   __shared__ uint32_t P32[KW];
+  __shared__ uint32_t PW[KW];
   __shared__ unsigned long long red[kRB / 64];
   __shared__ uint32_t sh_q;
   const uint32_t tid = threadIdx.x, H = a.H, KWc = a.K * W;
@@ -588,6 +614,7 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
     const uint32_t t = ti * a.nx + tj;
     const Region g = make_region(a, t);
     const int cmax = g.maxj + W - 1;
+    if (role == 0 && tid == 0) MSTAMP(t, 0);
     const bool need_above = ti > 0 && cmax > final_col;
     const uint32_t need_main = (role > 0 && tj > a.K) ? tj - a.K : 0;  // tiles the main must have done
     const int cb = (int)need_main * W - 1;
@@ -615,7 +642,6 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
             }
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       __syncthreads();
       if (need_above) {
@@ -628,16 +654,26 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
       }
     }
     __syncthreads();
+    if (role == 0 && tid == 0) MSTAMP(t, 1);
     if (tid < (uint32_t)W) {
       const uint64_t pr = band_bits64(L, bd, bd.i0 + (int)tid, g.j0) & topW;
       P64[tid] = pr;
-      P32[tid] = (uint32_t)(pr >> (64 - W));
+      P32[tid] = (uint32_t)(pr >> 32);  // rows packed 32/W per word, first row at the top
     }
     __syncthreads();
-    if (role == 0 && tid < 64 && tj > 0) {  // publish the previous tile
-      __threadfence();
-      if (tid == 0) __hip_atomic_store(&progress[ti], tj, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < (uint32_t)(W * W / 32)) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int q = 0; q < 32 / W; ++q) v |= P32[tid * (32 / W) + q] >> (W * q);
+      PW[tid] = v;
     }
+    __syncthreads();
+    if (role == 0 && tid == 0) MSTAMP(t, 2);
+    if (role == 0 && tid < 64 && tj > 0) {  // publish the previous tile
+      stores_done();
+      if (tid == 0) raise_flag(&progress[ti], tj);
+    }
+    if (role == 0 && tid == 0) MSTAMP(t, 3);
     unsigned long long best = ~0ull;
     bool stop = false;
     const uint32_t n1r = (uint32_t)(g.i0 - g.mini2 + 1);
@@ -646,28 +682,26 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
     const uint32_t N1 = (n1r + kGK - 1) / kGK * g.n1c, N2 = (n2r + kGK - 1) / kGK * g.n2c;
     if (role == 0) {
       if (H == 0) {
-        scan_tasks<KW>(L, bd, P32, a.T, g.i0, n1r, g.maxj2, g.n1c, 0, g.n1c, 0, N1, 0, 0, best, stop);
-        scan_tasks<KW>(L, bd, P32, a.T, g.i0 - W, n2r, g.maxj, g.n2c, (uint32_t)g.n1, g.n2c, 0, N2, 0, 0, best,
-                       stop);
-      } else {  // the windows over the K tiles to the left: loop 1, a < W, c < K*W
+        scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0, n1r, g.maxj2, g.n1c, 0, 0, N1, 0, 0, best, stop);
+        scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0 - W, n2r, g.maxj, g.n2c, 1, 0, N2, 0, 0, best, stop);
+      } else {  // the windows over the K tiles to the left (loop 1, a < W, c < K*W), one per thread
         const uint32_t fa = min(n1r, (uint32_t)W), fc = min(g.n1c, KWc);
-        scan_tasks<KW>(L, bd, P32, a.T, g.i0, fa, g.maxj2, fc, 0, g.n1c, 0, (fa + kGK - 1) / kGK * fc, 0, 0, best,
-                       stop);
+        if (tid == 0) MSTAMP(t, 8);
+        scan_tasks<KW, 4>(L, bd, PW, a.T, g.i0, fa, g.maxj2, fc, 0, 0, (fa + 3) / 4 * fc, 0, 0, best, stop);
+        if (tid == 0) MSTAMP(t, 9);
       }
     } else {
       const uint32_t h = role - 1, N = N1 + N2;
       const uint32_t lo = (uint32_t)((uint64_t)h * N / H), hi = (uint32_t)((uint64_t)(h + 1) * N / H);
-      scan_tasks<KW>(L, bd, P32, a.T, g.i0, n1r, g.maxj2, g.n1c, 0, g.n1c, lo, min(hi, N1), W, KWc, best, stop);
-      scan_tasks<KW>(L, bd, P32, a.T, g.i0 - W, n2r, g.maxj, g.n2c, (uint32_t)g.n1, g.n2c, max(lo, N1) - N1,
-                     hi > N1 ? hi - N1 : 0, 0, 0, best, stop);
+      scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0, n1r, g.maxj2, g.n1c, 0, lo, min(hi, N1), W, KWc, best, stop);
+      scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0 - W, n2r, g.maxj, g.n2c, 1, max(lo, N1) - N1, hi > N1 ? hi - N1 : 0,
+                          0, 0, best, stop);
     }
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-      const unsigned long long o = shfl_u64(best, lane_id() ^ dd);
-      best = o < best ? o : best;
-    }
+    best = wave_min_u64(best);
+    if (role == 0 && tid == 0) MSTAMP(t, 10);
     if (lane_id() == 0) red[tid >> 6] = best;
     __syncthreads();
+    if (role == 0 && tid == 0) MSTAMP(t, 4);
     if (tid < 64) {
       unsigned long long key = red[0];
       for (int w = 1; w < kRB / 64; ++w) key = red[w] < key ? red[w] : key;
@@ -677,9 +711,9 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
                              __HIP_MEMORY_SCOPE_AGENT);
       } else {
         const int r = (int)tid;
-        // the helpers' windows start at scan index K*W (loop 1, a = 0), W * n1c (a = W) or n1
-        const uint64_t hmin = g.n1c > KWc ? KWc : (n1r > (uint32_t)W ? (uint64_t)W * g.n1c : g.n1);
-        if (H > 0 && !((key >> kDpShift) == 0 && ((key >> kIdxShift) & kIdxMask) < hmin)) {
+        // the helpers' windows start at (loop 1, a = 0, c = K*W), (loop 1, a = W) or loop 2
+        const uint64_t hmin = g.n1c > KWc ? scan_pos(0, 0, KWc) : (n1r > (uint32_t)W ? scan_pos(0, W, 0) : scan_pos(1, 0, 0));
+        if (H > 0 && !((key >> kDpShift) == 0 && key_pos(key) < hmin)) {
           unsigned long long v = ~0ull;  // lanes without a helper: no window
           if (r < (int)H) {
             const unsigned long long* sl = &slots[(uint64_t)t * H + r];
@@ -693,18 +727,15 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
             }
           }
           v = v == ~0ull ? ~0ull : (v & ~kSlotSet);  // ~0: that helper had no window
-#pragma unroll
-          for (int dd = 32; dd >= 1; dd >>= 1) {
-            const unsigned long long o = shfl_u64(v, lane_id() ^ dd);
-            v = o < v ? o : v;
-          }
+          v = wave_min_u64(v);
           key = v < key ? v : key;
         }
+        if (tid == 0) MSTAMP(t, 5);
         uint32_t bdist = (uint32_t)(W * W) + 1;
         int bi = 0, bj = 0;
         if (key != ~0ull) {
           bdist = (uint32_t)(key & 0x1fff);
-          window_pos(g, W, (uint32_t)((key >> kIdxShift) & kIdxMask), bi, bj);
+          pos_window(g, W, key_pos(key), bi, bj);
         }
         const uint64_t p = r < W ? P64[r] : 0ull;
         const uint64_t b = (key != ~0ull && r < W) ? (band_bits64(L, bd, bi + r, bj) & topW) : 0ull;
@@ -725,15 +756,17 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
           const uint32_t w0 = (uint32_t)g.j0 >> 6, w1 = (uint32_t)(g.j0 + W - 1) >> 6;
           const uint32_t* lr = L + (uint32_t)(g.i0 + r - bd.lo) * bd.pitch;
           for (uint32_t w = w0; w <= w1; ++w)
-            a.I[(uint64_t)(g.i0 + r) * a.wpr + w] = ((uint64_t)lr[2 * w] << 32) | lr[2 * w + 1];
+            st_word(a.I + (uint64_t)(g.i0 + r) * a.wpr + w, ((uint64_t)lr[2 * w] << 32) | lr[2 * w + 1]);
         }
+        if (tid == 0) MSTAMP(t, 6);
       }
     }
     __syncthreads();
+    if (role == 0 && tid == 0) MSTAMP(t, 7);
   }
   if (role == 0 && tid < 64) {
-    __threadfence();
-    if (tid == 0) __hip_atomic_store(&progress[ti], a.nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    stores_done();
+    if (tid == 0) raise_flag(&progress[ti], a.nx);
   }
 }
 
@@ -866,7 +899,7 @@ MatchSched match_schedule(uint32_t W, uint32_t R, uint32_t cols, uint32_t code) 
   if (code == 0 || (code & 0xffff0000u) == 0x10000u) {
     if (fit && team_w) {
       m.kind = kSchedTeam;
-      const uint64_t h = (nmax + 4095) / 4096;
+      const uint64_t h = (nmax + 2047) / 2048;  // helpers: ~2K windows (a couple of tasks per thread) each
       m.H = code ? (code & 0xffffu) : (uint32_t)(h < 1 ? 1 : h > 16 ? 16 : h);
       if (m.H > 64) m.H = 64;
       m.K = W == 8 ? 4 : W == 16 ? 3 : 2;
@@ -918,7 +951,7 @@ void launch_match_tiles(hipStream_t s, MatchArgs& a, const MatchSched& m, void* 
       else k_match_team<32><<<a.ny * (m.H + 1), kRB, 0, s>>>(a, progress, slots);
       break;
     case kSchedRows:
-      k_match_rows<0><<<a.ny, kRB, 0, s>>>(a, progress);
+      k_match_rows<<<a.ny, kRB, 0, s>>>(a, progress);
       break;
     default:
       k_match_tiles<<<ntiles * a.G, kMB, 0, s>>>(a);

@@ -275,6 +275,63 @@ int Device::patch_search(const binary_matrix& I, unsigned W, std::vector<uint32_
   return BIC_OK;
 }
 
+int Device::match_encode(binary_matrix& I, unsigned W, unsigned T, unsigned R, MatchResult* out,
+                         GolombCoder* golomb_match, GolombCoder* golomb_nomatch, const double* enuml) {
+  BIC_TRY(status_);
+  if (!out || W < 1 || W > 64) return BIC_EINVAL;
+  if ((golomb_match && !coder_state::fresh(*golomb_match)) || (golomb_nomatch && !coder_state::fresh(*golomb_nomatch)))
+    return BIC_EINVAL;
+  const idx_t rows = I.get_rows(), cols = I.get_cols(), wpr = I.get_blocks_per_row();
+  if (rows % W || cols % W) return BIC_EINVAL;
+  const size_t nt = (rows / W) * (cols / W), M = (size_t)W * W;
+  *out = MatchResult();
+  if (nt == 0) return BIC_OK;
+  std::vector<double> table;
+  if (!enuml) {
+    table.resize(M + 1);
+    for (size_t w = 0; w <= M; ++w) table[w] = bic_enum_codelength((unsigned)M, (unsigned)w);
+    enuml = table.data();
+  }
+  const size_t cap = (rows * cols + 33 * nt + 63) / 64 + 1;  // both streams, always enough
+  const size_t tile_bytes = ((4 * 4 + 1) * nt + 255) & ~(size_t)255;
+  BIC_TRY(ensure(in_, rows * wpr * 8));
+  BIC_TRY(ensure(out_a_, 2 * cap * 8));
+  BIC_TRY(ensure(aux_, tile_bytes));
+  BIC_TRY(ensure(small_, 64));
+  uint64_t* d_I = static_cast<uint64_t*>(in_.p);
+  uint64_t* d_s = static_cast<uint64_t*>(out_a_.p);
+  uint32_t* d_t = static_cast<uint32_t*>(aux_.p);
+  uint64_t* d_st = static_cast<uint64_t*>(small_.p);
+  BIC_TRY(upload(I, d_I));
+  BIC_TRY(bic_match_encode(ctx_, d_I, rows, cols, wpr, W, T, R, enuml, d_t, d_t + nt, d_t + 2 * nt, d_t + 3 * nt,
+                           reinterpret_cast<uint8_t*>(d_t + 4 * nt), d_I, d_s, d_s + cap, cap, d_st));
+  BIC_TRY(bic_sync(ctx_));
+  uint64_t st[4];
+  BIC_TRY(bic_memcpy_d2h(ctx_, st, d_st, sizeof(st)));
+  std::vector<uint32_t>* arrs[4] = {&out->besti, &out->bestj, &out->bestd, &out->weights};
+  for (int k = 0; k < 4; ++k) {
+    arrs[k]->resize(nt);
+    BIC_TRY(bic_memcpy_d2h(ctx_, arrs[k]->data(), d_t + k * nt, nt * 4));
+  }
+  out->modes.resize(nt);
+  BIC_TRY(bic_memcpy_d2h(ctx_, out->modes.data(), d_t + 4 * nt, nt));
+  BIC_TRY(fetch_stream(d_s, st[1], &out->stream_match));
+  BIC_TRY(fetch_stream(d_s + cap, st[2], &out->stream_nomatch));
+  BIC_TRY(download(d_I, I));
+  out->matches = st[0];
+  out->L = st[3];
+  // the coders' state: samples, their sum and bits per coder
+  uint64_t n[2] = {0, 0}, sum[2] = {0, 0};
+  for (size_t i = 0; i < nt; ++i) {
+    const int c = (out->modes[i] == 'X' || out->modes[i] == 'x') ? 0 : 1;
+    n[c] += 1;
+    sum[c] += out->weights[i];
+  }
+  if (golomb_match) coder_state::advance(*golomb_match, n[0], sum[0], st[1]);
+  if (golomb_nomatch) coder_state::advance(*golomb_nomatch, n[1], sum[1], st[2]);
+  return BIC_OK;
+}
+
 Device& default_device() {
   static Device* dev = new Device(0);
   if (dev->status() != BIC_OK) {

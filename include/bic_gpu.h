@@ -53,6 +53,16 @@ struct TileResult {
   uint64_t L = 0;                   // sum of lentab[chosen weight]
 };
 
+// Result of compress7_test.cpp's tile loop with a search window (Device::match_encode), per tile
+// in raster order, plus the state the driver's two GolombCoders end in.
+struct MatchResult {
+  std::vector<uint32_t> besti, bestj, bestd;  // the search (:184; bestd = W*W+1: empty region)
+  std::vector<uint32_t> weights;              // the coded weight
+  std::vector<uint8_t> modes;                 // 'X' 'x' (match) or 'O' 'o'
+  Stream stream_match, stream_nomatch;        // golomb_match / golomb_nomatch codewords
+  uint64_t matches = 0, L = 0;                // L: sum of the chosen lengths (before the bitcounts)
+};
+
 class Device {
  public:
   explicit Device(int ordinal = 0);
@@ -92,6 +102,13 @@ class Device {
   // least-distance window of the causal search region, first in the reference's scan order.
   int patch_search(const binary_matrix& I, unsigned W, std::vector<uint32_t>* besti,
                    std::vector<uint32_t>* bestj, std::vector<uint32_t>* bestd);
+
+  // compress7_test.cpp:117-275 with W, T, R as its argv[2..4] (rows, cols multiples of W): I is
+  // replaced by the image after the residual write-back; golomb_match / golomb_nomatch (fresh)
+  // end in the state the driver's coders end in. enuml[w] = enumL(W*W, w) (nullptr: this build's).
+  int match_encode(binary_matrix& I, unsigned W, unsigned T, unsigned R, MatchResult* out,
+                   GolombCoder* golomb_match = nullptr, GolombCoder* golomb_nomatch = nullptr,
+                   const double* enuml = nullptr);
 
  private:
   struct Buf {

@@ -305,6 +305,99 @@ int gpu(int argc, char** argv) {
     P2.destroy();
   }
 
+  // compress7_test.cpp's loop with a search window, written with this build's reference API as
+  // the driver writes it (get_submatrix, dist, add, med, weight, set_submatrix, GolombCoder),
+  // against bic::Device::match_encode on the top-left multiple-of-W part of plane np-1
+  {
+    const unsigned W = 8, T = 1, R = 24;
+    const idx_t mr = rows / W * W, mc = cols / W * W;
+    if (mr && mc) {
+      binary_matrix I = planes[np - 1].get_submatrix(0, mr, 0, mc), I2 = I.get_copy();
+      const idx_t M = W * W;
+      std::vector<double> e(M + 1);
+      for (idx_t w = 0; w <= M; ++w) e[w] = enumerative_codelength(M, w);
+      bic::MatchResult res;
+      GolombCoder gm_gpu, gn_gpu;
+      CHECK(dev.match_encode(I2, W, T, R, &res, &gm_gpu, &gn_gpu, e.data()) == BIC_OK, "match_encode");
+      GolombCoder golomb_match, golomb_nomatch;
+      binary_matrix P, P2, P3(W, W);
+      idx_t li = 0, matches = 0, L = 0;
+      const int iW = W, iR = R;
+      for (idx_t i = 0; i < mr / W; i++)
+        for (idx_t j = 0; j < mc / W; j++, li++) {
+          const int i0 = i * W, j0 = j * W;
+          P = I.get_submatrix(i0, i0 + W, j0, j0 + W);
+          idx_t besti = 0, bestj = 0, bestd = M + 1;
+          int i2;
+          bool perfect = false;
+          const int mini = i0 > iR ? i0 - iR : 0, minj = j0 > iR ? j0 - iR : 0;
+          const int maxj = (j0 + iR > int(mc) - iW) ? int(mc) - iW : j0 + iR;
+          const int mini2 = i0 > iW ? i0 - iW : 0, maxj2 = j0 > iW ? j0 - iW : 0;
+          const int swin = (i0 - mini2) * (maxj2 - minj) + (mini2 - mini) * (maxj - minj);
+          for (i2 = i0; i2 >= mini2 && !perfect; i2--)
+            for (int j2 = maxj2; j2 >= minj; j2--) {
+              P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+              const idx_t d = dist(P, P2);
+              if (d < bestd) { bestd = d; besti = i2; bestj = j2; }
+              if (bestd <= T) { perfect = true; break; }
+            }
+          for (i2 = i0 - iW; i2 >= mini && !perfect; i2--)
+            for (int j2 = maxj; j2 >= minj; j2--) {
+              P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+              const idx_t d = dist(P, P2);
+              if (d < bestd) { bestd = d; besti = i2; bestj = j2; }
+              if (bestd <= T) { perfect = true; break; }
+            }
+          if (bestd <= M) {
+            P2 = I.get_submatrix(besti, besti + W, bestj, bestj + W);
+            add(P, P2, P3);
+          } else {
+            P3 = P.get_copy();
+          }
+          binary_matrix dP(W, W), dP3(W, W);
+          med(P, dP);
+          med(P3, dP3);
+          const idx_t wmn = P3.weight(), wnn = P.weight(), wmp = dP3.weight(), wnp = dP.weight();
+          const bool ok = swin > 0;
+          const idx_t idx_len = ok ? (idx_t)ceil(log2(swin)) : 0;
+          const idx_t nn = 1 + 1 + e[wnn], np_ = 1 + 1 + e[wnp];
+          const idx_t mn = ok ? (idx_t)(1 + 1 + idx_len + e[wmn]) : ~(idx_t)0;
+          const idx_t mp = ok ? (idx_t)(1 + 1 + idx_len + e[wmp]) : ~(idx_t)0;
+          const bool mpred = mn > mp, npred = nn > np_;
+          const idx_t mlen = mpred ? mp : mn, nlen = npred ? np_ : nn;
+          const bool take = nlen > mlen;
+          const idx_t w = take ? (mpred ? wmp : wmn) : (npred ? wnp : wnn);
+          if (take) {
+            golomb_match.codeSample(w);
+            matches++;
+            L += mlen;
+            I.set_submatrix(i0, j0, mpred ? dP3 : P3);
+          } else {
+            golomb_nomatch.codeSample(w);
+            L += nlen;
+            I.set_submatrix(i0, j0, npred ? dP : P);
+          }
+          const char mode = take ? (mpred ? 'X' : 'x') : (npred ? 'O' : 'o');
+          CHECK(res.besti[li] == besti && res.bestj[li] == bestj && res.bestd[li] == bestd && res.weights[li] == w &&
+                    res.modes[li] == (uint8_t)mode, "match tile %lu", li);
+          dP.destroy();
+          dP3.destroy();
+        }
+      CHECK(dist(I, I2) == 0, "match residual image");
+      CHECK(res.matches == matches && res.L == L, "match totals");
+      CHECK(gm_gpu.bitcount == golomb_match.bitcount && gn_gpu.bitcount == golomb_nomatch.bitcount,
+            "match coders: %ld %ld vs %ld %ld", gm_gpu.bitcount, gn_gpu.bitcount, golomb_match.bitcount,
+            golomb_nomatch.bitcount);
+      CHECK(bic::coder_state::k(gm_gpu) == bic::coder_state::k(golomb_match) &&
+                bic::coder_state::k(gn_gpu) == bic::coder_state::k(golomb_nomatch),
+            "match coder state");
+      I.destroy();
+      I2.destroy();
+      P.destroy();
+      P2.destroy();
+    }
+  }
+
   for (auto& p : planes) p.destroy();
   A.destroy();
   std::printf("gpu %s planes=%d\n", failures ? "FAILED" : "ok", np);
