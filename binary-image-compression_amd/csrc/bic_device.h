@@ -22,58 +22,106 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   const uint32_t hi = __shfl((unsigned)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
 }
+
+// ---- DPP primitives (every lane of the wave active) --------------------------------------
+// Cross-lane steps through DPP (a few cycles each) instead of ds_bpermute (an LDS round trip,
+// ~50+ cycles): the scans and reductions below are dependent chains, so their latency is what
+// a row's wave waits for. CTRL: 0x111.. row_shr:n, 0x138 wave_shr:1, 0x140 row_mirror,
+// 0x141 row_half_mirror, 0x142 row_bcast:15, 0x143 row_bcast:31, 0xB1 / 0x4E quad swaps.
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {  // invalid source lanes / masked rows read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, true);
+}
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ int dpp_or(int old, int v) {  // invalid source lanes / masked rows read old
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane63_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+__device__ __forceinline__ uint64_t lane63_u64(uint64_t v) {
+  return ((uint64_t)lane63_u32((uint32_t)(v >> 32)) << 32) | lane63_u32((uint32_t)v);
+}
+// lane i gets lane i-d's value, lanes < d their own (__shfl_up semantics); d = 1 through DPP
 __device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+  if (d == 1) {
+    const uint32_t lo = (uint32_t)dpp_or<0x138>((int)(uint32_t)v, (int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)dpp_or<0x138>((int)(uint32_t)(v >> 32), (int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+  }
   const uint32_t lo = __shfl_up((unsigned)(v & 0xffffffffu), d);
   const uint32_t hi = __shfl_up((unsigned)(v >> 32), d);
   return ((uint64_t)hi << 32) | lo;
 }
 
+// inclusive scans: Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4, 8), then the row
+// totals carried into rows 1 and 3 (row_bcast:15) and into rows 2 and 3 (row_bcast:31)
 __device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d);
-    if (l >= d) x += y;
-  }
+  x += dpp0<0x111>(x);
+  x += dpp0<0x112>(x);
+  x += dpp0<0x114>(x);
+  x += dpp0<0x118>(x);
+  x += dpp0<0x142, 0xA>(x);
+  x += dpp0<0x143, 0xC>(x);
   return x;
 }
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ uint64_t dpp0_u64(uint64_t v) {
+  return ((uint64_t)dpp0<CTRL, RM>((uint32_t)(v >> 32)) << 32) | dpp0<CTRL, RM>((uint32_t)v);
+}
 __device__ __forceinline__ uint64_t wave_incl_sum_u64(uint64_t x) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = shfl_up_u64(x, d);
-    if (l >= d) x += y;
-  }
+  x += dpp0_u64<0x111>(x);
+  x += dpp0_u64<0x112>(x);
+  x += dpp0_u64<0x114>(x);
+  x += dpp0_u64<0x118>(x);
+  x += dpp0_u64<0x142, 0xA>(x);
+  x += dpp0_u64<0x143, 0xC>(x);
   return x;
 }
 __device__ __forceinline__ int wave_incl_max(int x) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d);
-    if (l >= d) x = max(x, y);
-  }
+  x = max(x, dpp_or<0x111>(INT_MIN, x));
+  x = max(x, dpp_or<0x112>(INT_MIN, x));
+  x = max(x, dpp_or<0x114>(INT_MIN, x));
+  x = max(x, dpp_or<0x118>(INT_MIN, x));
+  x = max(x, dpp_or<0x142, 0xA>(INT_MIN, x));
+  x = max(x, dpp_or<0x143, 0xC>(INT_MIN, x));
   return x;
 }
+// reductions (wave-uniform results): quad swaps and the two mirrors give every lane its row's
+// total, the four rows are combined from readlanes
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+  x += dpp0_u64<0xB1>(x);
+  x += dpp0_u64<0x4E>(x);
+  x += dpp0_u64<0x141>(x);
+  x += dpp0_u64<0x140>(x);
+  uint64_t s = 0;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += shfl_u64(x, lane_id() ^ d);
-  return x;
+  for (int r = 0; r < 64; r += 16)
+    s += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), r) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, r);
+  return s;
 }
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-  return x;
+  x += dpp0<0xB1>(x);
+  x += dpp0<0x4E>(x);
+  x += dpp0<0x141>(x);
+  x += dpp0<0x140>(x);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) + (uint32_t)__builtin_amdgcn_readlane((int)x, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)x, 32) + (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
 }
 __device__ __forceinline__ int wave_max(int x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x = max(x, __shfl_xor(x, d));
-  return x;
+  x = max(x, dpp_or<0xB1>(x, x));
+  x = max(x, dpp_or<0x4E>(x, x));
+  x = max(x, dpp_or<0x141>(x, x));
+  x = max(x, dpp_or<0x140>(x, x));
+  return max(max(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+             max(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
 }
 __device__ __forceinline__ int wave_min(int x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d));
-  return x;
+  x = min(x, dpp_or<0xB1>(x, x));
+  x = min(x, dpp_or<0x4E>(x, x));
+  x = min(x, dpp_or<0x141>(x, x));
+  x = min(x, dpp_or<0x140>(x, x));
+  return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+             min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
 }
 
 // DPP wave reductions: four in-row steps (quad swaps, half-row and row mirrors: a few cycles each,
@@ -254,8 +302,8 @@ __device__ __forceinline__ uint64_t resid_word(RowCtx& rc, const Geom& g, uint32
     const uint64_t u = (valid && rc.up) ? rc.up[w] : 0;
     uint64_t pl = shfl_up_u64(p, 1), ul = shfl_up_u64(u, 1);
     if (lane_id() == 0) { pl = rc.pcarry; ul = rc.ucarry; }
-    rc.pcarry = shfl_u64(p, 63);
-    rc.ucarry = shfl_u64(u, 63);
+    rc.pcarry = lane63_u64(p);
+    rc.ucarry = lane63_u64(u);
     r = p ^ u ^ ((p >> 1) | (pl << 63)) ^ ((u >> 1) | (ul << 63));
     if (row == 0 && w == 0) r &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
   } else {
@@ -293,7 +341,7 @@ __device__ __forceinline__ void resid_row(const uint64_t* planes, const Geom& g,
       if (row) d ^= u[t];
       uint64_t dl = shfl_up_u64(d, 1);
       if (lane == 0) dl = carry;
-      carry = shfl_u64(d, 63);
+      carry = lane63_u64(d);
       d ^= (d >> 1) | (dl << 63);
       if (row == 0 && w == 0) d &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
     }
@@ -334,13 +382,12 @@ __device__ __forceinline__ void step_prefix(uint64_t r, uint32_t w, StepState& s
   const uint32_t pc = (uint32_t)__popcll(r);
   const uint32_t inc = wave_incl_sum_u32(pc);
   n_w = st.n_carry + inc - pc;
-  st.n_carry += __shfl(inc, 63);
+  st.n_carry += lane63_u32(inc);
   const int lastc = r ? (int)(w * 64 + 63 - __builtin_ctzll(r)) : -1;
   const int mx = wave_incl_max(lastc);
-  int ex = __shfl_up(mx, 1);
-  if (lane_id() == 0) ex = -1;
+  const int ex = dpp_or<0x138>(-1, mx);  // lane 0: -1
   jp_w = max(st.jp_carry, ex);
-  st.jp_carry = max(st.jp_carry, __shfl(mx, 63));
+  st.jp_carry = max(st.jp_carry, (int)lane63_u32((uint32_t)mx));
 }
 
 

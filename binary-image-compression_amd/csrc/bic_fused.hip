@@ -434,7 +434,7 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
                                          ByteTables{reinterpret_cast<const uint32_t*>(a.lut + 256), a.lut});
     const uint32_t inc = wave_incl_sum_u32(e.len);
     const uint64_t off = carry + inc - e.len;
-    carry += __shfl(inc, 63);
+    carry += lane63_u32(inc);
     emit_word(fs, off, x, w, n, jp, arow, eol, g.cols);
   }
   fs.flush();
@@ -594,7 +594,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
 #endif
         const uint32_t inc = wave_incl_sum_u32(e.len);
         const uint64_t off = loc + inc - e.len;
-        loc += __shfl(inc, 63);
+        loc += lane63_u32(inc);
         if (fits && loc <= kCapBits) {
           if (!e.lng) {
             place_small(gimg, (uint32_t)off, e.head, e.k0);
@@ -820,7 +820,7 @@ __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geo
     if (j == eolw) X |= eolbit;
     uint64_t Xl = shfl_up_u64(X, 1);
     if (lane == 0) Xl = carry;
-    carry = shfl_u64(X, 63);
+    carry = lane63_u64(X);
     const uint64_t v = sh ? (Xl << (64 - sh)) | (X >> sh) : X;
     if (j < nw) {
       const uint64_t wi = w0 + j;
@@ -920,7 +920,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
         emit_word(ls, p, x, w, n, jp, arow, eol, g.cols);
         ls.flush();
       }
-      loc += __shfl(inc, 63);
+      loc += lane63_u32(inc);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       // flush the complete 64-bit words; the row's first word, if shared, is a fragment

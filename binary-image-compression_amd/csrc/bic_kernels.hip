@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_med_rows(Geom g, const uint64_t* __r
         const uint64_t D0 = p0[t] ^ up0[t], D1 = p1[t] ^ up1[t];
         uint64_t Dl = shfl_up_u64(D1, 1);
         if (lane == 0) Dl = carry;
-        carry = shfl_u64(D1, 63);
+        carry = lane63_u64(D1);
         R0 = D0 ^ ((D0 >> 1) | (Dl << 63));
         R1 = D1 ^ ((D1 >> 1) | (D0 << 63));
         if (row == 0 && w == 0) R0 &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
@@ -431,7 +431,7 @@ __device__ __forceinline__ void emit_chunk(const Geom& g, const uint64_t* planes
     const uint32_t bits = w < g.used ? wb[w] : 0;
     const uint32_t binc = wave_incl_sum_u32(bits);
     uint64_t off = off_carry + binc - bits;
-    off_carry += __shfl(binc, 63);
+    off_carry += lane63_u32(binc);
     const bool eol = (w == g.used - 1);
     while (x || eol) {
       int j;
