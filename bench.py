@@ -38,8 +38,10 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=16384, help="rows per plane in the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="repeat the CPU baseline sample until this much CPU time has been measured")
-    ap.add_argument("--encoder", default="single-pass", choices=["single-pass", "two-pass", "multipass"],
+    ap.add_argument("--encoder", default="staged", choices=["staged", "single-kernel", "two-pass", "multipass"],
                     help="row encoder for rows <= 16384 columns (bic_ctx_set_option)")
+    ap.add_argument("--separate", action="store_true",
+                    help="c3: bic_bitplanes_u8 then bic_encode_planes2 instead of the one-call bic_encode_gray")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
@@ -141,15 +143,20 @@ class C3:
         self.bits_e = ctx.empty_i64(self.nplanes)
         ctx.reserve(self.nplanes, self.rows, self.cols)
         self.k = 0
+        self.separate = args.separate
         self.pixels = self.rows * self.cols * self.nplanes
         self.workload = (f"c3: {self.rows}x{self.cols} 8-bit gray -> 8 bitplanes -> med -> per-row runs "
                          f"-> Golomb + EG streams per plane")
 
     def step(self):
-        c, p = self.ctx, self.pybic
-        c.bitplanes_u8(self.gray[self.k & 1], nplanes=8, out=self.planes)
-        c.encode_planes2(self.planes, self.cols, True, slots=(self.slot_g, self.slot_e),
-                         outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
+        c = self.ctx
+        if self.separate:
+            c.bitplanes_u8(self.gray[self.k & 1], nplanes=8, out=self.planes)
+            c.encode_planes2(self.planes, self.cols, True, slots=(self.slot_g, self.slot_e),
+                             outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
+        else:  # one call: bitplanes + both streams (bic_encode_gray)
+            c.encode_gray(self.gray[self.k & 1], nplanes=8, planes=self.planes, slots=(self.slot_g, self.slot_e),
+                          outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
         self.k += 1
 
     def out_bytes(self):
@@ -161,7 +168,8 @@ class C3:
         plane_b = self.nplanes * self.rows * self.wpr * 8
         g = int(self.pybic.as_u64(self.bits_g).astype(np.int64).sum()) // 8
         e = int(self.pybic.as_u64(self.bits_e).astype(np.int64).sum()) // 8
-        return {"bitplanes_u8": self.rows * self.cols + plane_b, "med_count": plane_b, "golomb_bits": plane_b,
+        return {"bitplanes_u8": self.rows * self.cols + plane_b, "bitplanes_count": self.rows * self.cols + plane_b,
+                "med_count": plane_b, "golomb_bits": plane_b,
                 "golomb_emit": plane_b + g, "eg_emit": plane_b + e, "encode_rows_golomb_eg": plane_b + g + e}
 
     def host_planes(self, rows):
@@ -526,8 +534,7 @@ def main():
     world, rank, local = dist_setup(args)
     import pybic
     ctx = pybic.Context(local)
-    ctx.set_two_pass(args.encoder == "two-pass")
-    ctx.set_multipass(args.encoder == "multipass")
+    ctx.set_encoder(args.encoder)
     if args.workload == "c3":
         wl = C3(ctx, args, rank)
     elif args.workload == "c2":

@@ -28,7 +28,7 @@ struct bic_ctx {
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   uint64_t* lut = nullptr;        // device [3][256] byte table of the fused encoder
-  uint32_t* flags = nullptr;      // device [4]: overflow, domain, look-back timeout, spare
+  uint32_t* flags = nullptr;      // device [4]: overflow, domain, look-back timeout, internal length check
   uint64_t* lentab = nullptr;     // device copy of the tile length table
   size_t lentab_cap = 0;          // entries
   uint64_t* staging = nullptr;    // pinned host staging for lentab
@@ -42,7 +42,8 @@ struct bic_ctx {
   // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
   bool prof_on = false;
   bool force_multipass = false;
-  bool two_pass = false;  // BIC_OPT_TWO_PASS: the two-pass row encoder instead of the single-kernel one
+  bool two_pass = false;       // BIC_OPT_TWO_PASS: the two-pass row encoder instead of the staged one
+  bool single_kernel = false;  // BIC_OPT_SINGLE_KERNEL: the single kernel with decoupled look-backs
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -205,8 +206,9 @@ int bic_sync(bic_ctx* ctx) {
   BIC_HIP(hipGetLastError());
   uint32_t f[4] = {0, 0, 0, 0};
   BIC_HIP(hipMemcpy(f, ctx->flags, sizeof(f), hipMemcpyDeviceToHost));
-  if (f[0] || f[1] || f[2]) BIC_HIP(hipMemset(ctx->flags, 0, sizeof(f)));
+  if (f[0] || f[1] || f[2] || f[3]) BIC_HIP(hipMemset(ctx->flags, 0, sizeof(f)));
   if (f[2]) return BIC_EDEVICE;  // a look-back record never arrived (should not happen)
+  if (f[3]) return BIC_EDEVICE;  // the row encoder's length pass disagreed with its emission (a bug)
   if (f[1]) return BIC_EINVAL;
   if (f[0]) return BIC_ENOSPC;
   return BIC_OK;
@@ -275,6 +277,10 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
     ctx->two_pass = value != 0;
     return BIC_OK;
   }
+  if (option == BIC_OPT_SINGLE_KERNEL) {
+    ctx->single_kernel = value != 0;
+    return BIC_OK;
+  }
   return BIC_EINVAL;
 }
 
@@ -341,11 +347,16 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
     // one pass: residual -> runs -> both streams (bic_fused.hip)
     if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
     const bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
+    const int mode = ctx->two_pass ? bic::kEncTwoPass
+                     : (ctx->single_kernel || !bic::med_rows_supported(g, planes, nullptr)) ? bic::kEncSingle
+                                                                                            : bic::kEncStaged;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
-                        bits_eg, ctx->flags, !ctx->two_pass, st);
+                        bits_eg, ctx->flags, mode, st);
     };
     stage(bic::kFusedPrep);
+    // staged encoder: per-row counts, scans and Golomb lengths (every row's offsets known up front)
+    if (mode == bic::kEncStaged) timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
     // the row kernel alone is timed under the encoder's name (bench.py's roofline kernel)
     timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
           [&] { stage(bic::kFusedRows); });
@@ -372,6 +383,44 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
       bic::launch_eg_emit(ctx->cur, g, planes, pr, cs, out_eg, slot_eg, bits_eg, ctx->flags);
     });
   }
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,
+                    uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                    uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (nplanes < 1 || nplanes > 8 || pitch < cols || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (!out_golomb && !out_eg) return BIC_EINVAL;
+  if (out_golomb && (!bits_golomb || slot_golomb == 0)) return BIC_EINVAL;
+  if (out_eg && (!bits_eg || slot_eg == 0)) return BIC_EINVAL;
+  if (rows && (!gray || !planes)) return BIC_EINVAL;
+  const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
+  const bool fuse = rows && bic::fused_supported(g) && !ctx->force_multipass && !ctx->two_pass && !ctx->single_kernel &&
+                    bic::med_rows_supported(g, planes, nullptr) && bic::gray_rows_supported(g, gray, pitch, planes);
+  if (!fuse) {  // the same result through the two separate calls
+    if ((rc = bic_bitplanes_u8(ctx, gray, pitch, rows, cols, nplanes, planes, wpr))) return rc;
+    return bic_encode_planes2(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
+                              out_eg, slot_eg, bits_eg);
+  }
+  const int pr = predict ? 1 : 0;
+  if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
+  bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
+  fs.counted = true;
+  auto stage = [&](int st) {
+    bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
+                      bits_eg, ctx->flags, bic::kEncStaged, st);
+  };
+  stage(bic::kFusedPrep);
+  timed(ctx, "bitplanes_count", [&] {
+    bic::launch_gray_rows(ctx->cur, gray, pitch, g, pr, planes, fs.sones, fs.krec, fs.kpos);
+  });
+  timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
+  timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
+        [&] { stage(bic::kFusedRows); });
+  timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
   BIC_HIP(hipGetLastError());
   return BIC_OK;
 }

@@ -274,6 +274,79 @@ __device__ __forceinline__ uint32_t golomb_k_state(uint32_t n, uint32_t A) {
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
+// Bits of the Golomb codewords whose '1' lies in residual word w of a row (plus the end-of-row
+// codeword when eol) -- the length the row encoder's emission produces for that word -- without
+// forming any codeword. n = samples of the plane before the word's first 1, jp = column of the
+// row's last 1 before the word (-1: none), arow = row * (cols + 1) (so A = arow + jp + 1 - n).
+// When every codeword of the word has the same k (k bounds as in encode_word) and k <= 3, the
+// sum of s >> k over the word's inner runs is counted word-parallel: an inner zero at column p
+// adds one bit iff its index in its run is 2^k - 1 mod 2^k, i.e. iff p = j mod 2^k for the 1 at
+// column j that opened the run. With the word bit-reversed (column b at significance b), the
+// zeros following the 1s of one residue class c are Z & ~(Z + (E_c << 1)) (the carry of each
+// E_c bit ripples through its run and stops at the next 1), so each class costs one add and a
+// popcount. Other words walk their codewords (GolombCoder.cpp:29-34 lengths).
+// kor |= 1 << k for every k the word's codewords use (k capped at 31).
+__device__ __forceinline__ uint32_t word_len(uint64_t x, uint32_t w, uint32_t n, int jp, uint32_t arow, bool eol,
+                                             uint32_t cols, uint32_t& kor) {
+  if (!x && !eol) return 0;
+  if (x && n) {
+    const uint32_t m = (uint32_t)__popcll(x);
+    const uint32_t bf = (uint32_t)__builtin_clzll(x), bl = 63u - (uint32_t)__builtin_ctzll(x);
+    const uint32_t pfirst = w * 64 + bf, plast = w * 64 + bl;
+    const uint32_t khi = golomb_k(n, arow + plast - (n + m - 1));
+    const uint32_t klo = golomb_k(n + m - 1 + (eol ? 1u : 0u), arow + (uint32_t)(jp + 1) - n);
+    if (khi == klo && khi <= 3) {
+      const uint32_t k = khi;
+      kor |= 1u << k;
+      uint32_t len = m * (k + 1) + ((pfirst - (uint32_t)(jp + 1)) >> k);
+      if (eol) len += k + 1 + ((cols - 1 - plast) >> k);
+      if (m > 1) {
+        const uint64_t xr = __builtin_bitreverse64(x);
+        const uint64_t between = ((1ull << bl) - 1ull) & ~((2ull << bf) - 1ull);  // bf < bl here
+        const uint64_t Z = ~xr & between;
+        if (k == 0) {
+          len += (uint32_t)__popcll(Z);
+        } else {
+          const uint64_t pat = k == 1 ? 0x5555555555555555ull : (k == 2 ? 0x1111111111111111ull : 0x0101010101010101ull);
+          const uint32_t ncls = 1u << k;
+          uint64_t rest = Z;
+          for (uint32_t c = 0; c + 1 < ncls; ++c) {
+            const uint64_t P = pat << c;
+            const uint64_t F = Z & ~(Z + ((xr & P) << 1));
+            len += (uint32_t)__popcll(F & P);
+            rest &= ~F;
+          }
+          len += (uint32_t)__popcll(rest & (pat << (ncls - 1)));
+        }
+      }
+      return len;
+    }
+  }
+  uint32_t len = 0;
+  for (;;) {
+    int j;
+    uint32_t s;
+    if (x) {
+      const int cz = __builtin_clzll(x);
+      x ^= BIC_MSB >> cz;
+      j = (int)(w * 64) + cz;
+      s = (uint32_t)(j - jp - 1);
+    } else if (eol) {
+      j = (int)cols;
+      s = cols - 1 - (uint32_t)jp;
+      eol = false;
+    } else {
+      break;
+    }
+    const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
+    kor |= 1u << min(k, 31u);
+    len += k + 1 + (s >> k);
+    ++n;
+    jp = j;
+  }
+  return len;
+}
+
 // ------------------------------------------------------------------------------------
 // residual word of a chunk step (med in word form), shared by every chunk kernel
 // ------------------------------------------------------------------------------------
@@ -350,6 +423,43 @@ __device__ __forceinline__ void resid_row(const uint64_t* planes, const Geom& g,
   }
 }
 
+// resid_row (c0 = 0) split into its loads and its arithmetic, so a loop can have the next row's
+// loads in flight while it works on this one.
+template <int WPL, bool PREDICT>
+__device__ __forceinline__ void row_load(const uint64_t* planes, const Geom& g, uint32_t plane, uint32_t row,
+                                         uint64_t (&p)[WPL], uint64_t (&u)[WPL]) {
+  const uint64_t* cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
+  const uint64_t* up = row ? cur - g.wpr : cur;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = t * 64 + lane_id();
+    const uint32_t wc = w < g.used ? w : g.used - 1;
+    p[t] = cur[wc];
+    u[t] = PREDICT && row ? up[wc] : 0;
+  }
+}
+template <int WPL, bool PREDICT>
+__device__ __forceinline__ void row_resid(const Geom& g, uint32_t row, const uint64_t (&p)[WPL],
+                                          const uint64_t (&u)[WPL], uint64_t (&r)[WPL]) {
+  const int lane = lane_id();
+  uint64_t carry = 0;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = t * 64 + lane;
+    uint64_t d = p[t];
+    if constexpr (PREDICT) {
+      d ^= u[t];
+      uint64_t dl = shfl_up_u64(d, 1);
+      if (lane == 0) dl = carry;
+      carry = lane63_u64(d);
+      d ^= (d >> 1) | (dl << 63);
+      if (row == 0 && w == 0) d &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+    }
+    if (w == g.used - 1) d &= g.trail;
+    r[t] = w < g.used ? d : 0;
+  }
+}
+
 struct ChunkId {
   uint32_t plane, row, c;
   uint64_t id;
@@ -390,6 +500,16 @@ __device__ __forceinline__ void step_prefix(uint64_t r, uint32_t w, StepState& s
   st.jp_carry = max(st.jp_carry, (int)lane63_u32((uint32_t)mx));
 }
 
+
+// The column of the row's last 1 before the lane's word (-1: none), carried across steps.
+__device__ __forceinline__ int step_jp(uint64_t r, uint32_t w, int& jp_carry) {
+  const int lastc = r ? (int)(w * 64 + 63 - __builtin_ctzll(r)) : -1;
+  const int mx = wave_incl_max(lastc);
+  const int ex = dpp_or<0x138>(-1, mx);  // lane 0: -1
+  const int jp = max(jp_carry, ex);
+  jp_carry = max(jp_carry, (int)lane63_u32((uint32_t)mx));
+  return jp;
+}
 
 // Codeword sinks: OR the bits of a codeword (k-bit binary part, then the '1' after the
 // unary zeros) into an LDS image (u32 words) or into global big-endian 64-bit words.

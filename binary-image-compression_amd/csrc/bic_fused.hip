@@ -21,6 +21,9 @@
 // Inter-workgroup records are 8-byte {flag, value} granules written and polled with
 // agent-scope atomics (cdna_hip_programming.md §6 Guideline 16, R2), spins bounded.
 #include "bic_device.h"
+#include "bic_kstat.h"
+
+#include <algorithm>
 
 namespace bic {
 
@@ -213,6 +216,142 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
   return e;
 }
 
+// OR the nb (1..64) low bits of v into the 128-bit MSB-first string (t0, t1) at bit pos
+// (pos + nb <= 128 whenever v != 0), branch-free.
+__device__ __forceinline__ void or128(uint64_t& t0, uint64_t& t1, uint64_t v, uint32_t pos, uint32_t nb) {
+  const uint32_t end = pos + nb;
+  const uint64_t p0 = end <= 64 ? v << ((64 - end) & 63) : v >> ((end - 64) & 63);
+  t0 |= pos < 64 ? p0 : 0ull;
+  t1 |= end > 64 ? v << ((128 - end) & 63) : 0ull;
+}
+
+// encode_word for a row whose codewords all have k = 1 (kK1Row): no k bounds, no sample count, no
+// divergent paths. The first codeword (binary part in head, its q zeros in z) is cut off as in
+// encode_word; the rest goes byte by byte through the k = 1 table: byte i's first 1 closes the open
+// run (c zeros before the byte + t): its binary bit, q zeros, then the table's '1' + R -- one
+// pattern appended to a right-aligned 128-bit accumulator (two 64-bit shifts and an or); the word's
+// first byte appends '1' + R only. <= 128 bits except through long runs (then lng: placed by
+// emit_word_k1).
+__device__ __forceinline__ void acc_put(uint64_t& hi, uint64_t& lo, uint64_t pat, uint32_t nb) {  // nb 1..63
+  hi = (hi << nb) | (lo >> (64 - nb));
+  lo = (lo << nb) | pat;
+}
+__device__ __forceinline__ void acc_zeros(uint64_t& hi, uint64_t& lo, uint32_t nb) {  // nb <= 128
+  if (nb >= 64) {
+    hi = lo;
+    lo = 0;
+    nb -= 64;
+  }
+  if (nb) {
+    hi = (hi << nb) | (lo >> (64 - nb));
+    lo <<= nb;
+  }
+}
+// append bin, q zeros, then pat (np bits, 1..63): total 1 + q + np bits
+__device__ __forceinline__ void acc_codeword(uint64_t& hi, uint64_t& lo, uint32_t& p, uint32_t bin, uint32_t q,
+                                             uint64_t pat, uint32_t np) {
+  const uint32_t nb = 1 + q + np;
+  if (p + nb <= 128) {
+    if (nb <= 63) {
+      acc_put(hi, lo, ((uint64_t)bin << (nb - 1)) | pat, nb);
+    } else {
+      acc_put(hi, lo, bin, 1);
+      acc_zeros(hi, lo, q);
+      acc_put(hi, lo, pat, np);
+    }
+  }
+  p += nb;
+}
+
+__device__ __forceinline__ LaneEnc encode_word_k1(uint64_t x, uint32_t w, int jp, bool eol, uint32_t cols,
+                                                  const uint32_t* T1) {
+  LaneEnc e{};
+  e.k0 = 1;
+  uint32_t c = w * 64 - (uint32_t)(jp + 1);  // zeros of the open run
+  if (!x) {
+    if (eol) {
+      const uint32_t s = cols - 1 - (uint32_t)jp;
+      e.head = s & 1u;
+      e.z = s >> 1;
+      e.t0 = BIC_MSB;
+      e.tlen = 1;
+      e.len = 2 + e.z;
+    }
+    return e;
+  }
+  const uint32_t bf = (uint32_t)__builtin_clzll(x);
+  const uint32_t s1 = c + bf, fb = bf >> 3;
+  e.head = s1 & 1u;
+  e.z = s1 >> 1;
+  uint64_t hi = 0, lo = 0;
+  uint32_t p = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t v = (uint32_t)(x >> (56 - 8 * i)) & 0xffu;
+    if (v) {
+      const uint32_t en = T1[v];
+      const uint32_t R = en & 0x1fffffu, lr = (en >> 21) & 31u, t = (en >> 26) & 7u, tz = en >> 29;
+      const uint64_t pat = (1ull << lr) | R;
+      if (i == fb) {
+        acc_put(hi, lo, pat, lr + 1);
+        p += lr + 1;
+      } else {
+        const uint32_t s = c + t;
+        acc_codeword(hi, lo, p, s & 1u, s >> 1, pat, lr + 1);
+      }
+      c = tz;
+    } else {
+      c += 8;
+    }
+  }
+  if (eol) {  // the row's trailing zeros (pad columns excluded)
+    const uint32_t s = c - (w * 64 + 64 - cols);
+    acc_codeword(hi, lo, p, s & 1u, s >> 1, 1ull, 1);
+  }
+  e.tlen = p;
+  e.len = 1 + e.z + p;
+  e.lng = p > 128;
+  if (!e.lng) {  // left-align the p-bit string
+    const uint32_t sh = 128 - p;
+    if (sh >= 64) {
+      e.t0 = lo << (sh - 64);
+      e.t1 = 0;
+    } else if (sh) {
+      e.t0 = (hi << sh) | (lo >> (64 - sh));
+      e.t1 = lo << sh;
+    } else {
+      e.t0 = hi;
+      e.t1 = lo;
+    }
+  }
+  return e;
+}
+
+// emit_word for k = 1 rows (the lng fallback of encode_word_k1).
+template <typename Sink, typename Off>
+__device__ __forceinline__ void emit_word_k1(Sink& sk, Off off, uint64_t x, uint32_t w, int jp, bool eol, uint32_t cols) {
+  for (;;) {
+    int j;
+    uint32_t s;
+    if (x) {
+      const int cz = __builtin_clzll(x);
+      x ^= BIC_MSB >> cz;
+      j = (int)(w * 64) + cz;
+      s = (uint32_t)(j - jp - 1);
+    } else if (eol) {
+      j = (int)cols;
+      s = cols - 1 - (uint32_t)jp;
+      eol = false;
+    } else {
+      break;
+    }
+    if (s & 1u) sk.put(off, 1u, 1);
+    sk.bit(off + 1 + (s >> 1));
+    off += 2 + (s >> 1);
+    jp = j;
+  }
+}
+
 // Emit one word's codewords through a sink at bit offset `off` (fallback paths).
 template <typename Sink, typename Off>
 __device__ __forceinline__ void emit_word(Sink& sk, Off off, uint64_t x, uint32_t w, uint32_t n, int jp,
@@ -344,7 +483,12 @@ struct FusedArgs {
   uint64_t* bits_rec;  // zeroed per launch
   uint64_t *gboff, *glen, *gfrag, *gslow;
   uint64_t *eboff, *elen, *efrag;
-  uint32_t* row_o;     // two-pass encoder: ones of the plane before each row
+  uint32_t* row_o;     // two-pass / staged encoders: ones of the plane before each row
+  uint32_t* sones;     // staged encoder: per (plane, row, strip) 1-counts and k statistics
+  int4* krec;
+  uint32_t* kpos;
+  uint32_t ns;         // strips per row
+  uint32_t* walk_ids;  // staged encoder: rows k_row_walk walks (count in counter[2])
   uint32_t* slow_n;    // number of rows k_rows_global must write (zeroed per launch)
   uint64_t* slow_ids;  // their row ids
   uint64_t* out_g;
@@ -356,6 +500,7 @@ struct FusedArgs {
   uint32_t* flags;
 #ifdef BIC_STAMPS
   int known;
+  int dbg;  // diagnostic (BIC_EMIT_DBG): k_emit_known skips 1 = LDS-image Golomb rows, 2 = EG rows, 4 = k = 0 copies
 #endif
 };
 
@@ -467,7 +612,7 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * (kGImg + kEImg)];
-  __shared__ uint64_t sh_cnt[kTileRows], sh_pre[2];
+  __shared__ uint64_t sh_cnt[kTileRows], sh_len[kTileRows], sh_pre[2];
   __shared__ uint32_t sh_tile;
   __shared__ uint32_t s_lut[512];  // k = 1, 2 byte tables
   const Geom& g = a.g;
@@ -547,6 +692,51 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   uint64_t O = sh_pre[0];
   for (int q = 0; q < wave; ++q) O += sh_cnt[q];
 
+  // ---- Golomb length of the row (word_len: no codewords formed), published for the tile at once:
+  // the tiles after this one find its bit count before its codewords exist, so the bit-offset
+  // look-back does not wait on any tile's emission. Wave 0 looks back while the others emit. ----
+  uint64_t L = 0;
+  if constexpr (DO_G) {
+    if (valid) {
+      StepState st{(uint32_t)(O + row), -1};
+      const uint32_t arow = row * (g.cols + 1);
+      uint32_t ll = 0;
+      for (uint32_t w0 = 0; w0 < g.used; w0 += 64) {
+        const uint32_t w = w0 + lane;
+        const uint64_t x = img_resid(eimg, g, w);
+        uint32_t n;
+        int jp;
+        step_prefix(x, w, st, n, jp);
+        uint32_t kor = 0;
+        ll += word_len(x, w, n, jp, arow, w == g.used - 1, g.cols, kor);
+      }
+      L = wave_sum_u32(ll);
+    }
+    if (lane == 0) sh_len[wave] = L;
+    __syncthreads();
+#ifdef BIC_STAMPS
+    if (a.known) {
+      if (threadIdx.x == 0) sh_pre[1] = g_known[1][rid];
+    } else
+#endif
+    if (wave == 0) {
+      uint64_t tile_bits = 0;
+      for (int q = 0; q < kTileRows; ++q) tile_bits += sh_len[q];
+      uint64_t Gt = 0;
+      if (trow == 0) {
+        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | tile_bits);
+      } else {
+        if (lane == 0) rec_store(&a.bits_rec[rid], kAgg | tile_bits);
+        Gt = lookback(a.bits_rec, rbase, rid, a.flags);
+        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | (Gt + tile_bits));
+      }
+      if (lane == 0) sh_pre[1] = Gt;
+#ifdef BIC_STAMPS
+      if (lane == 0 && rid < (1u << 17)) g_known[1][rid] = Gt;
+#endif
+    }
+  }
+
   // ---- EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1 ----
   if (DO_E && valid) {
     const bool f_here = O == 0 && ones > 0;
@@ -569,17 +759,16 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   }
 
   STAMP(3);
-  // ---- Golomb ------------------------------------------------------------------------------
+  // ---- Golomb codewords into the row image (rows longer than the LDS window: k_rows_global) ----
   if constexpr (DO_G) {
-    uint64_t L = 0;
-    bool fits = true;
+    constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+    const bool fits = L <= kCapBits;
 #ifdef BIC_STAMPS
     uint32_t dbg_slow = 0;
 #endif
-    if (valid) {
+    if (valid && fits) {
       StepState st{(uint32_t)(O + row), -1};
       const uint32_t arow = row * (g.cols + 1);
-      constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
       uint64_t loc = 0;
       for (uint32_t w0 = 0; w0 < g.used; w0 += 64) {
         const uint32_t w = w0 + lane;
@@ -595,20 +784,16 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
         const uint32_t inc = wave_incl_sum_u32(e.len);
         const uint64_t off = loc + inc - e.len;
         loc += lane63_u32(inc);
-        if (fits && loc <= kCapBits) {
-          if (!e.lng) {
-            place_small(gimg, (uint32_t)off, e.head, e.k0);
-            place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
-          } else {
-            LdsSink ls{gimg, 0, 0};
-            emit_word(ls, (uint32_t)off, x, w, n, jp, arow, eol, g.cols);
-            ls.flush();
-          }
+        if (!e.lng) {
+          place_small(gimg, (uint32_t)off, e.head, e.k0);
+          place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
         } else {
-          fits = false;
+          LdsSink ls{gimg, 0, 0};
+          emit_word(ls, (uint32_t)off, x, w, n, jp, arow, eol, g.cols);
+          ls.flush();
         }
       }
-      L = loc;
+      if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
     }
     STAMP(4);
 #ifdef BIC_STAMPS
@@ -617,34 +802,11 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
       if (lane == 0 && (uint64_t)id * 8 + 7 < (1u << 21)) g_stamps[(uint64_t)id * 8 + 7] = tot;
     }
 #endif
-    if (lane == 0) sh_cnt[wave] = L;
-    __syncthreads();
-#ifdef BIC_STAMPS
-    if (a.known) {
-      if (threadIdx.x == 0) sh_pre[1] = g_known[1][rid];
-    } else
-#endif
-    if (wave == 0) {
-      uint64_t tile_bits = 0;
-      for (int q = 0; q < kTileRows; ++q) tile_bits += sh_cnt[q];
-      uint64_t Gt = 0;
-      if (trow == 0) {
-        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | tile_bits);
-      } else {
-        if (lane == 0) rec_store(&a.bits_rec[rid], kAgg | tile_bits);
-        Gt = lookback(a.bits_rec, rbase, rid, a.flags);
-        if (lane == 0) rec_store(&a.bits_rec[rid], kInc | (Gt + tile_bits));
-      }
-      if (lane == 0) sh_pre[1] = Gt;
-#ifdef BIC_STAMPS
-      if (lane == 0 && rid < (1u << 17)) g_known[1][rid] = Gt;
-#endif
-    }
     __syncthreads();
     STAMP(5);
     if (valid) {
       uint64_t Grel = sh_pre[1];
-      for (int q = 0; q < wave; ++q) Grel += sh_cnt[q];
+      for (int q = 0; q < wave; ++q) Grel += sh_len[q];
       const uint64_t cap = a.slot_g * 64;
       const uint64_t G = (uint64_t)plane * cap + Grel;
       if (lane == 0 && row == g.rows - 1) a.bits_g[plane] = Grel + L;
@@ -758,8 +920,8 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
         uint32_t n;
         int jp;
         step_prefix(rr[t], w, st, n, jp);
-        const LaneEnc e = encode_word<false>(rr[t], w, n, jp, arow, w == g.used - 1, g.cols, ByteTables{s_lut, a.lut});
-        const uint32_t tot = wave_sum_u32(e.len);
+        uint32_t kor = 0;
+        const uint32_t tot = wave_sum_u32(word_len(rr[t], w, n, jp, arow, w == g.used - 1, g.cols, kor));
         L += tot;
         step_max = max(step_max, tot);
       }
@@ -802,7 +964,8 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
 // EG row from registers: row bit b (b < cols) is ~R, bit cols is the end-of-row '1'; output word
 // j of the row holds row bits [64j - g, 64j - g + 64) with g = Ge % 64. Lane l forms words
 // j = 64t + l from its own row word and its left neighbour's (one shuffle per step).
-template <int WPL>
+// INV = false: the row bits are R itself (a Golomb row whose codewords all have k = 0).
+template <int WPL, bool INV = true>
 __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geom& g, uint64_t Ge, uint64_t Le,
                                             uint64_t* out, uint64_t* frag) {
   const int lane = lane_id();
@@ -816,7 +979,7 @@ __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geo
     const uint32_t j = t * 64 + lane;
     if (t * 64 >= (int)nw) break;
     uint64_t X = 0;
-    if (t < WPL && j < g.used) X = ~rr[t] & (j == g.used - 1 ? g.trail : ~0ull);
+    if (t < WPL && j < g.used) X = INV ? ~rr[t] & (j == g.used - 1 ? g.trail : ~0ull) : rr[t];
     if (j == eolw) X |= eolbit;
     uint64_t Xl = shfl_up_u64(X, 1);
     if (lane == 0) Xl = carry;
@@ -953,6 +1116,327 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
   }
 }
 
+// ==========================================================================================
+// Staged encoder (default): every inter-row dependency is resolved by a kernel boundary instead of
+// a decoupled look-back, so no workgroup ever waits on another (a cross-XCD look-back hop costs
+// microseconds, MI355X_MICROARCH.md barrier-counter row, and a tile waiting on one holds its
+// CU's waves idle). Stages: per-row residual 1-counts (k_med_rows<ROWS>) -> per-plane scan ->
+// per-row Golomb lengths (word_len) -> per-plane scan of the lengths -> k_emit_known, where each
+// wave walks its rows independently (persistent waves, static row order, no barriers).
+// ==========================================================================================
+
+// Exclusive per-plane scan of per-row values, one 1024-thread workgroup per plane, each thread
+// owning a run of consecutive rows. ONES: the strips' 1-counts (sones) -> row_o[], the ones before each row.
+// Otherwise: glen[] Golomb lengths -> gboff[] absolute bit offsets in the plane's slot, bits_g[]
+// the plane's total; rows past the slot's end get glen = 0 and raise the overflow flag.
+constexpr uint64_t kK0Row = 1ull << 63;  // glen flags: every codeword of the row has k = 0,
+constexpr uint64_t kK1Row = 1ull << 62;  // every codeword of the row has k = 1
+constexpr uint64_t kLenMask = kK1Row - 1;
+template <bool ONES>
+__global__ __launch_bounds__(1024) void k_scan_plane(FusedArgs a) {
+  __shared__ uint64_t tmp[17];
+  const Geom& g = a.g;
+  const uint32_t plane = blockIdx.x;
+  const uint64_t base = (uint64_t)plane * g.rows;
+  constexpr int kPer = 16;  // rows per thread and pass: all loads in flight before any is used
+  uint64_t carry = 0;
+  for (uint32_t c0 = 0; c0 < g.rows; c0 += 1024 * kPer) {
+    const uint32_t r0 = c0 + threadIdx.x * kPer;
+    uint64_t v[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t r = r0 + i;
+      if constexpr (ONES) {
+        uint64_t o = 0;
+        if (r < g.rows)
+          for (uint32_t q = 0; q < a.ns; ++q) o += a.sones[(base + r) * a.ns + q];
+        v[i] = o;
+      } else {
+        v[i] = r < g.rows ? (a.glen[base + r] & kLenMask) : 0;
+      }
+    }
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) sum += v[i];
+    uint64_t tot;
+    uint64_t pre = block_excl_scan<uint64_t>(sum, tmp, tot) + carry;
+    carry += tot;
+    if constexpr (ONES) {
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        if (r0 + i < g.rows) a.row_o[base + r0 + i] = (uint32_t)pre;
+        pre += v[i];
+      }
+    } else {
+      const uint64_t cap = a.slot_g * 64;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const uint32_t r = r0 + i;
+        if (r < g.rows) {
+          a.gboff[base + r] = (uint64_t)plane * cap + pre;
+          if (pre + v[i] > cap) {
+            a.glen[base + r] = 0;  // overflowed: nothing written, fixup skips
+            atomicOr(&a.flags[0], 1u);
+          }
+        }
+        pre += v[i];
+      }
+    }
+  }
+  if (!ONES && threadIdx.x == 0) a.bits_g[plane] = carry;
+}
+
+// Golomb length of every row from its sample base (ones before it), one lane per row: rows whose k
+// statistics (bic_kstat.h) prove every codeword k = 0 (length cols + 1: the residual row and its
+// end-of-row '1') or k = 1 (2n + (zeros - odd runs) / 2) get their length without being read; the
+// others are appended to a list (k_row_walk).
+__global__ __launch_bounds__(256) void k_row_class(FusedArgs a) {
+  const Geom& g = a.g;
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  bool walk = false;
+  if (id < nrows) {
+    const uint32_t row = (uint32_t)(id % g.rows);
+    walk = true;
+    if (row > 0) {  // (the plane's first sample has k = 1 from the fresh state, Golomb.h:18)
+      const uint32_t O = a.row_o[id];
+      const RowK rk = row_kstats(a.krec + id * a.ns, a.kpos + id * a.ns, a.ns, g.cols);
+      const int64_t N0 = (int64_t)O + row, A0 = (int64_t)row * g.cols - O;
+      if (A0 - N0 + rk.q0 <= 0) {
+        a.glen[id] = kK0Row | (g.cols + 1);
+        walk = false;
+      } else if (A0 - 2 * N0 + rk.qh <= 0 && A0 - N0 + rk.ql > 0) {
+        const uint64_t n = rk.ones + 1, zeros = g.cols - rk.ones, odd = n - rk.chg;
+        a.glen[id] = kK1Row | (2 * n + (zeros - odd) / 2);
+        walk = false;
+      }
+    }
+  }
+  // wave-aggregated append to the list of rows to walk
+  const uint64_t m = __ballot(walk);
+  if (!m) return;
+  uint32_t base = 0;
+  const int leader = __builtin_ctzll(m);
+  if (lane_id() == leader) base = atomicAdd(a.counter + 2, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, leader);
+  if (walk) a.walk_ids[base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)id;
+}
+
+// The listed rows' Golomb lengths, one wave per row (codeword walk, word_len); a fixed grid strides
+// over the list, whose length k_row_class left in counter[2].
+constexpr uint32_t kWalkBlocks = 1024;
+template <int WPL, bool PREDICT>
+__global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  const uint32_t nlist = __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < nlist; i += kWalkBlocks * 4) {
+    const uint64_t id = a.walk_ids[i];
+    const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+    const uint32_t O = a.row_o[id];
+    uint64_t rr[WPL];
+    resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
+    StepState st{O + row, -1};
+    const uint32_t arow = row * (g.cols + 1);
+    uint32_t ll = 0, kor = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = t * 64 + lane;
+      if (t * 64 >= (int)g.used) break;
+      uint32_t n;
+      int jp;
+      step_prefix(rr[t], w, st, n, jp);
+      ll += word_len(rr[t], w, n, jp, arow, w == g.used - 1, g.cols, kor);
+    }
+    ll = wave_sum_u32(ll);
+    const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);
+    if (lane == 0) a.glen[id] = ll | (!ks ? kK0Row : (!k1s ? kK1Row : 0));
+  }
+}
+
+// The rows with every prefix known. EG rows, and Golomb rows whose codewords all have k = 0 (the
+// residual row and its '1'), are shifted copies formed in registers. Other Golomb rows: the row
+// image in LDS (encode_word), written with plain stores; rows whose image exceeds the LDS window
+// go to the k_rows_global list. The words shared with neighbouring rows go to the fragment tables
+// (k_fixup). One wave per row, 4-wave workgroups, no barriers after the byte tables are staged
+// (XCD-remapped block order: the waves of one XCD hold consecutive rows, the row above is an L2 hit).
+constexpr int kEmitWaves = 4;
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+__global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * (kGImg + kEImg)];
+  __shared__ uint32_t s_lut[512];
+  const Geom& g = a.g;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t* gimg = lds + wave * (kGImg + kEImg);
+  uint32_t* eimg = gimg + kGImg;
+  if (DO_G)
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+  __syncthreads();  // the only workgroup barrier
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+  // persistent waves: rows id, id + stride, ... with the next row's loads in flight
+  const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
+  uint64_t id = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
+  uint64_t np_[WPL], nu_[WPL];
+  uint32_t nO = 0;
+  uint64_t nLf = 0;
+  if (id < nrows) {
+    row_load<WPL, PREDICT>(a.planes, g, (uint32_t)(id / g.rows), (uint32_t)(id % g.rows), np_, nu_);
+    nO = a.row_o[id];
+    nLf = DO_G ? a.glen[id] : 0;
+  }
+  for (; id < nrows; id += stride) {
+  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+  uint64_t cp_[WPL], cu_[WPL];
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    cp_[t] = np_[t];
+    cu_[t] = nu_[t];
+  }
+  const uint32_t O = nO;
+  const uint64_t Lf = nLf;
+  if (id + stride < nrows) {
+    const uint64_t id2 = id + stride;
+    row_load<WPL, PREDICT>(a.planes, g, (uint32_t)(id2 / g.rows), (uint32_t)(id2 % g.rows), np_, nu_);
+    nO = a.row_o[id2];
+    nLf = DO_G ? a.glen[id2] : 0;
+  }
+  const uint64_t L = Lf & kLenMask;
+  const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
+  bool gen = DO_G && L && !k0 && fits;  // Golomb row through the LDS image
+#ifdef BIC_STAMPS
+  if (a.dbg & 1) gen = false;
+#endif
+  if (gen) {  // zero the Golomb image
+    uint4* z = reinterpret_cast<uint4*>(gimg);
+    for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  uint64_t rr[WPL];
+  row_resid<WPL, PREDICT>(g, row, cp_, cu_, rr);
+  bool f_here = false;  // the plane's first 1 is in this row: EG inserts a '0' after it
+  int fcol = INT_MAX;
+  if (DO_E && O == 0) {
+    uint32_t ones = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      ones += (uint32_t)__popcll(rr[t]);
+      if (rr[t] && fcol == INT_MAX) fcol = (int)((t * 64 + lane) * 64 + __builtin_clzll(rr[t]));
+    }
+    f_here = wave_sum_u32(ones) > 0;
+    fcol = wave_min(fcol);
+  }
+  if (f_here) {  // EG image (~R, pad-masked, EOL '1') of the row holding the plane's first 1 (write_row inserts its '0')
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = t * 64 + lane;
+      if (w < g.used) {
+        const uint64_t v = ~rr[t] & (w == g.used - 1 ? g.trail : ~0ull);
+        eimg[2 * w] = (uint32_t)(v >> 32);
+        eimg[2 * w + 1] = (uint32_t)v;
+      }
+    }
+    if (lane < kPad + 1) eimg[2 * g.used + lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) eimg[g.cols >> 5] |= 0x80000000u >> (g.cols & 31);  // EOL '1'
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+#ifdef BIC_STAMPS
+  if (!(a.dbg & 2))
+#endif
+  if constexpr (DO_E) {  // EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1
+    const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
+    const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
+    const uint64_t cap = a.slot_e * 64;
+    const uint64_t Ge = (uint64_t)plane * cap + Ge_rel;
+    if (Ge_rel + Le <= cap) {
+      if (f_here) write_row(eimg, Le, Ge, (int64_t)fcol + 1, a.out_e, a.efrag + 2 * id);
+      else eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
+      if (lane == 0) { a.eboff[id] = Ge; a.elen[id] = Le; }
+    } else if (lane == 0) {
+      a.eboff[id] = Ge;
+      a.elen[id] = 0;
+      atomicOr(&a.flags[0], 1u);
+    }
+    if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
+  }
+  if constexpr (DO_G) {
+    if (k0 && L) {
+#ifdef BIC_STAMPS
+      if (!(a.dbg & 4))
+#endif
+      eg_row_regs<WPL, false>(rr, g, a.gboff[id], L, a.out_g, a.gfrag + 2 * id);
+    } else if (gen && k1) {  // every codeword k = 1: branch-free byte-table words
+      int jpc = -1;
+      uint32_t loc = 0;
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        if (t * 64 >= (int)g.used) break;
+        const uint32_t w = t * 64 + lane;
+        const uint64_t x = rr[t];
+        const int jp = step_jp(x, w, jpc);
+        const bool eol = w == g.used - 1;
+        const LaneEnc e = encode_word_k1(x, w, jp, eol, g.cols, s_lut);
+        const uint32_t inc = wave_incl_sum_u32(e.len);
+        const uint32_t off = loc + inc - e.len;
+        loc += lane63_u32(inc);
+        if (!e.lng) {
+          place_small(gimg, off, e.head, 1);
+          place128(gimg, off + 1 + e.z, e.t0, e.t1, e.tlen);
+        } else {
+          LdsSink ls{gimg, 0, 0};
+          emit_word_k1(ls, off, x, w, jp, eol, g.cols);
+          ls.flush();
+        }
+      }
+      if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
+    } else if (gen) {
+      StepState st{O + row, -1};
+      const uint32_t arow = row * (g.cols + 1);
+      uint64_t loc = 0;
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        if (t * 64 >= (int)g.used) break;
+        const uint32_t w = t * 64 + lane;
+        const uint64_t x = rr[t];
+        uint32_t n;
+        int jp;
+        step_prefix(x, w, st, n, jp);
+        const bool eol = w == g.used - 1;
+        const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols, ByteTables{s_lut, a.lut});
+        const uint32_t inc = wave_incl_sum_u32(e.len);
+        const uint64_t off = loc + inc - e.len;
+        loc += lane63_u32(inc);
+        if (!e.lng) {
+          place_small(gimg, (uint32_t)off, e.head, e.k0);
+          place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
+        } else {
+          LdsSink ls{gimg, 0, 0};
+          emit_word(ls, (uint32_t)off, x, w, n, jp, arow, eol, g.cols);
+          ls.flush();
+        }
+      }
+      if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
+    }
+    if (lane == 0) {
+      if (k0 || k1) a.glen[id] = L;  // drop the flags: k_fixup reads plain lengths
+      const bool slow = L && !k0 && !fits;
+      a.gslow[id] = slow ? O + row + 1 : 0;  // k_rows_global writes the row
+      if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS images
+  __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // Combine the fragments of the words rows share: the row holding a shared word's first bit
 // owns it and ORs in the head fragments of the following rows that start inside that word.
 __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff, const uint64_t* __restrict__ len,
@@ -987,7 +1471,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 10 + n * 4 + 1024;
+  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 2 + 1024;
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -1007,7 +1491,13 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
   fs.elen = q; q += n;
   fs.efrag = q; q += 2 * n;
   fs.slow_ids = q; q += n;
-  fs.row_o = reinterpret_cast<uint32_t*>(q);
+  fs.krec = reinterpret_cast<int4*>(q);
+  fs.kpos = reinterpret_cast<uint32_t*>(fs.krec + n * kMaxStrips);
+  fs.sones = fs.kpos + n * kMaxStrips;
+  fs.row_o = fs.sones + n * kMaxStrips;
+  fs.walk_ids = fs.row_o + n;
+  fs.ns = 1;
+  fs.counted = false;
   fs.slow_n = fs.counter + 1;  // zeroed with the counter
   return fs;
 }
@@ -1023,16 +1513,18 @@ int read_stamps(uint64_t* host, size_t n) {
 void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
                   const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
-                  uint64_t* bits_e, uint32_t* flags, bool single_pass, int stage) {
+                  uint64_t* bits_e, uint32_t* flags, int mode, int stage) {
   if (stage == kFusedPrep) {
-    (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
+    (void)hipMemsetAsync(fs.counter, 0, mode == kEncStaged ? 256 : fs.zero_bytes, s);
     return;
   }
+  const bool single_pass = mode == kEncSingle;
   FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
-              fs.eboff, fs.elen, fs.efrag, fs.row_o, fs.slow_n, fs.slow_ids, out_g, slot_g, bits_g, out_e, slot_e,
+              fs.eboff, fs.elen, fs.efrag, fs.row_o, fs.sones, fs.krec, fs.kpos, fs.counted ? fs.ns : 1u, fs.walk_ids, fs.slow_n, fs.slow_ids, out_g, slot_g, bits_g, out_e, slot_e,
               bits_e, flags};
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
+  a.dbg = getenv("BIC_EMIT_DBG") ? atoi(getenv("BIC_EMIT_DBG")) : 0;
 #endif
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t grid = (uint32_t)((g.rows + kTileRows - 1) / kTileRows * (uint64_t)g.nplanes);  // one per tile
@@ -1050,6 +1542,46 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
                                                         dg && de ? fgrid : 0xffffffffu);
     return;
   }
+  const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
+  if (mode == kEncStaged) {
+    if (stage == kFusedPrefix) {
+      if (!fs.counted) launch_row_ones(s, g, planes, predict, fs.sones, fs.krec, fs.kpos);
+      k_scan_plane<true><<<g.nplanes, 1024, 0, s>>>(a);
+      if (dg) {
+        k_row_class<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
+#define BIC_WALK(W) \
+  if (predict) k_row_walk<W, true><<<kWalkBlocks, 256, 0, s>>>(a); else k_row_walk<W, false><<<kWalkBlocks, 256, 0, s>>>(a)
+        if (wpl == 1) { BIC_WALK(1); } else if (wpl == 2) { BIC_WALK(2); } else { BIC_WALK(4); }
+#undef BIC_WALK
+        k_scan_plane<false><<<g.nplanes, 1024, 0, s>>>(a);
+      }
+      return;
+    }
+    // persistent grid: 8 workgroups per CU at most (more rows per wave when the image is larger)
+    static thread_local int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    const uint32_t egrid2 = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 8);
+#define BIC_EMIT1(W, P, DG, DE)                                                                        \
+  {                                                                                                  \
+    k_emit_known<W, P, DG, DE><<<egrid2, 64 * kEmitWaves, 0, s>>>(a);                                \
+  }
+#define BIC_EMIT(W, P)                                                                                \
+  if (dg && de) BIC_EMIT1(W, P, true, true) else if (dg) BIC_EMIT1(W, P, true, false) else BIC_EMIT1(W, P, false, true)
+    if (predict) {
+      if (wpl == 1) { BIC_EMIT(1, true); } else if (wpl == 2) { BIC_EMIT(2, true); } else { BIC_EMIT(4, true); }
+    } else {
+      if (wpl == 1) { BIC_EMIT(1, false); } else if (wpl == 2) { BIC_EMIT(2, false); } else { BIC_EMIT(4, false); }
+    }
+#undef BIC_EMIT
+#undef BIC_EMIT1
+    return;
+  }
+  if (stage == kFusedPrefix) return;
   const dim3 blk(64 * kTileRows);
 #define BIC_PASSES(W, P, DG, DE)                                                        \
   if (single_pass) {                                                                    \
@@ -1062,7 +1594,6 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   if (dg && de) { BIC_PASSES(W, P, true, true) }                                        \
   else if (dg) { BIC_PASSES(W, P, true, false) }                                        \
   else { BIC_PASSES(W, P, false, true) }
-  const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
   if (predict) {
     if (wpl == 1) { BIC_CODERS(1, true) } else if (wpl == 2) { BIC_CODERS(2, true) } else { BIC_CODERS(4, true) }
   } else {

@@ -90,7 +90,15 @@ struct FusedScratch {
   uint64_t *ones_rec, *bits_rec;
   size_t zero_bytes;  // counter + records, zeroed per launch
   uint64_t *gboff, *glen, *gfrag, *gslow, *eboff, *elen, *efrag;
-  uint32_t* row_o;
+  uint32_t* row_o;   // ones of the plane before each row (two-pass / staged encoders)
+  // staged encoder's count pass: per (plane, row, strip) the residual 1-count and the Golomb k
+  // statistics record (bic_kstat.h); ns records per row
+  uint32_t* sones;
+  int4* krec;
+  uint32_t* kpos;
+  uint32_t ns;
+  uint32_t* walk_ids;  // rows whose Golomb length is walked (k_row_walk)
+  bool counted;      // the count pass already ran (bic_encode_gray's fused bitplane kernel)
   uint32_t* slow_n;
   uint64_t* slow_ids;
 };
@@ -103,10 +111,19 @@ void build_byte_lut(uint64_t* lut);
 void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const uint64_t* lut, int predict,
                   const FusedScratch& fs,
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
-                  uint64_t* bits_e, uint32_t* flags, bool single_pass, int stage);
-// launch_fused stages: zero the tickets and records; the row kernel(s); the LDS-overflow rows and
-// the words adjacent rows share
-constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2;
+                  uint64_t* bits_e, uint32_t* flags, int mode, int stage);
+// launch_fused modes: the staged encoder (prefix kernels, then independent rows; planes 16-byte
+// aligned with an even row pitch), the single kernel with decoupled look-backs, the two-pass one
+constexpr int kEncStaged = 0, kEncSingle = 1, kEncTwoPass = 2;
+// launch_fused stages: zero the tickets and records; the staged encoder's prefix kernels (counts,
+// scans, lengths); the row kernel(s); the LDS-overflow rows and the words adjacent rows share
+constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2, kFusedPrefix = 3;
+void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint32_t* sones,
+                     int4* krec, uint32_t* kpos);
+// bitplanes + the count pass in one read of the gray image (bic_encode_gray)
+bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes);
+void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
+                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos);
 
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
                          uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd);

@@ -13,6 +13,7 @@
 //   bitplanes (bitplane_tool.cpp:24-30)
 //   tile path (compress7_test.cpp:184-275 with R = 0)
 #include "bic_device.h"
+#include "bic_kstat.h"
 
 namespace bic {
 
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(1024) void k_plane_weight(const uint32_t* __restric
 // K2b: bic_med_residual for rows of up to 256 words (even row pitch, 16-byte aligned planes):
 // one wave walks RPW consecutive rows of a plane, keeping the row above in registers, with
 // 16-byte loads (lane l holds words 2l, 2l+1 of each 128-word half). Writes the residual if
-// asked and one 1-count per wave; k_plane_weight adds those up per plane.
+// asked and one 1-count per wave (k_plane_weight adds those up per plane).
 template <int NP, int RPW, bool PREDICT>
 __global__ __launch_bounds__(kBlock) void k_med_rows(Geom g, const uint64_t* __restrict__ planes,
                                                      uint64_t* __restrict__ resid, uint32_t* __restrict__ part) {
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void k_med_rows(Geom g, const uint64_t* __r
       if (w + 1 >= g.used) R1 = 0;
       if (w == g.used - 1) R0 &= g.trail;
       if (w + 1 == g.used - 1) R1 &= g.trail;
-      ones += (uint32_t)(__popcll(R0) + __popcll(R1));
+      ones += (uint32_t)__popcll(R0) + (uint32_t)__popcll(R1);
       if (resid && w < g.wpr) {
         uint64_t* dst = resid + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr + w;
         *reinterpret_cast<ulonglong2*>(dst) = make_ulonglong2(R0, R1);
@@ -216,6 +217,208 @@ __global__ __launch_bounds__(kBlock) void k_med_rows(Geom g, const uint64_t* __r
   }
   ones = wave_sum_u32(ones);
   if (lane == 0) part[gw] = ones;
+}
+
+// ------------------------------------------------------------------------------------
+// The staged encoder's count pass (bic_kstat.h): per row of every plane its residual 1-count and k
+// statistics record. Each wave walks rows whole, lane l owning the LW consecutive words
+// LW*l .. LW*l + LW - 1 (64 * LW >= the row's words), so the k statistics accumulate inside the
+// lane and one scan pair and one set of reductions per (plane, row) finish them (lanek_store).
+// ------------------------------------------------------------------------------------
+// From the planes (planes 16-byte aligned, even row pitch; med_rows_supported): RPW rows of one
+// plane per wave, the row above kept in registers, the next row's loads in flight while this one is
+// used.
+template <int LW, int RPW, bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_med_kstat(Geom g, const uint64_t* __restrict__ planes,
+                                                      uint32_t* __restrict__ sones, int4* __restrict__ krec,
+                                                      uint32_t* __restrict__ kpos) {
+  const int lane = lane_id();
+  const uint32_t wpp = (g.rows + RPW - 1) / RPW;  // waves per plane
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  if (gw >= (uint64_t)wpp * g.nplanes) return;  // whole wave
+  const uint32_t plane = (uint32_t)(gw / wpp), r0 = (uint32_t)(gw % wpp) * RPW;
+  const uint64_t* pl = planes + (uint64_t)plane * g.plane_words;
+  const uint32_t w0 = LW * lane;
+  auto load = [&](uint32_t row, uint64_t (&v)[LW]) {
+    const uint64_t* src = pl + (uint64_t)row * g.wpr + w0;
+    if constexpr (LW == 1) {
+      v[0] = w0 < g.used ? src[0] : 0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < LW; i += 2) {  // pairs below `used` lie inside the (even) row pitch
+        ulonglong2 t = make_ulonglong2(0, 0);
+        if (w0 + i < g.used) t = *reinterpret_cast<const ulonglong2*>(src + i);
+        v[i] = t.x;
+        v[i + 1] = t.y;
+      }
+    }
+  };
+  uint64_t up[LW], cur[LW];
+#pragma unroll
+  for (int i = 0; i < LW; ++i) up[i] = 0;
+  if (PREDICT && r0) load(r0 - 1, up);
+  load(r0, cur);
+  const uint32_t nr = min((uint32_t)RPW, g.rows - r0);
+  for (uint32_t r = 0; r < nr; ++r) {
+    const uint32_t row = r0 + r;
+    uint64_t nxt[LW];
+    if (r + 1 < nr) load(row + 1, nxt);
+    LaneK k;
+    uint64_t D[LW];
+#pragma unroll
+    for (int i = 0; i < LW; ++i) D[i] = PREDICT ? cur[i] ^ up[i] : cur[i];
+    const uint64_t dl = wave_shr1_u64(D[LW - 1]);  // word LW*l - 1 (lane l - 1's last; lane 0: 0)
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const uint32_t w = w0 + i;
+      uint64_t R = D[i];
+      if constexpr (PREDICT) {
+        R = D[i] ^ ((D[i] >> 1) | ((i ? D[i - 1] : dl) << 63));
+        if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+      }
+      R = w < g.used ? (w == g.used - 1 ? R & g.trail : R) : 0;
+      lanek_word(k, R, (int32_t)(w * 64));
+      up[i] = cur[i];
+    }
+    const uint64_t id = (uint64_t)plane * g.rows + row;
+    lanek_store(k, krec + id, kpos + id, sones + id);
+#pragma unroll
+    for (int i = 0; i < LW; ++i) cur[i] = nxt[i];
+  }
+}
+
+void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint32_t* sones,
+                     int4* krec, uint32_t* kpos) {
+  constexpr int RPW = 8;
+  const uint32_t wpp = (g.rows + RPW - 1) / RPW;
+  const uint32_t grid = (uint32_t)(((uint64_t)wpp * g.nplanes + kWaves - 1) / kWaves);
+#define BIC_KST(LW, P) k_med_kstat<LW, RPW, P><<<grid, kBlock, 0, s>>>(g, planes, sones, krec, kpos)
+  if (g.used <= 64) { if (predict) BIC_KST(1, true); else BIC_KST(1, false); }
+  else if (g.used <= 128) { if (predict) BIC_KST(2, true); else BIC_KST(2, false); }
+  else { if (predict) BIC_KST(4, true); else BIC_KST(4, false); }
+#undef BIC_KST
+}
+
+// From the gray image (bic_encode_gray: bitplane_tool.cpp:24-30 and the count pass in one read):
+// kGrayRows whole rows per wave; lane l loads the 64 * LW pixels of its words (16-byte loads),
+// turns each 64 into one word per plane (K1's 8x8 transposes), stores the plane words, and forms
+// the med residual from the row above (plane words kept in registers) and the left neighbour (the
+// pixel before each word: the lane's own bytes, or lane l - 1's last). The gray rows must hold
+// used * 64 readable bytes (pitch >= used * 64, 16-byte aligned; gray_rows_supported).
+constexpr int kGrayRows = 8;
+
+__device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&pw)[8], uint64_t mask) {
+  uint64_t T[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    T[2 * i] = transpose8x8(bswap64((uint64_t)v[i].x | ((uint64_t)v[i].y << 32)));
+    T[2 * i + 1] = transpose8x8(bswap64((uint64_t)v[i].z | ((uint64_t)v[i].w << 32)));
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int g8 = 0; g8 < 8; ++g8) x |= ((T[g8] >> (8 * b)) & 0xffull) << (56 - 8 * g8);
+    pw[b] = x & mask;
+  }
+}
+
+template <int LW, bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_gray_rows(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
+                                                      uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
+                                                      int4* __restrict__ krec, uint32_t* __restrict__ kpos) {
+  const int lane = lane_id();
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  const uint32_t r0 = (uint32_t)gw * kGrayRows;
+  if (r0 >= g.rows) return;  // whole wave
+  const int np = (int)g.nplanes;
+  const uint32_t w0 = LW * lane;
+  auto load = [&](uint32_t row, uint4 (&v)[LW][4]) {
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const uint4* src = reinterpret_cast<const uint4*>(gray + (uint64_t)row * pitch + (uint64_t)(w0 + i) * 64);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[i][q] = (w0 + i < g.used) ? src[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // the last pixel of each of the lane's words, packed 8 bits per word
+  auto lasts = [&](const uint4 (&v)[LW][4]) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < LW; ++i) x |= (v[i][3].w >> 24) << (8 * i);
+    return x;
+  };
+  uint64_t up[LW][8];
+#pragma unroll
+  for (int i = 0; i < LW; ++i)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) up[i][b] = 0;
+  uint32_t ulast = 0;  // lasts() of the row above
+  uint4 cur[LW][4];
+  if (PREDICT && r0) {
+    load(r0 - 1, cur);
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const uint32_t w = w0 + i;
+      gray_to_planes(cur[i], up[i], w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull);
+    }
+    ulast = lasts(cur);
+  }
+  const uint32_t nr = min((uint32_t)kGrayRows, g.rows - r0);
+  for (uint32_t r = 0; r < nr; ++r) {
+    const uint32_t row = r0 + r;
+    load(row, cur);
+    // D bits of the pixel left of each word (8 planes per byte): own words' last pixels, lane l - 1's
+    // last word for the first
+    const uint32_t cl = lasts(cur);
+    const uint32_t dl = (PREDICT && row) ? cl ^ ulast : cl;
+    const uint32_t dprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(dl >> (8 * (LW - 1))), 0x138, 0xf, 0xf, true);
+    ulast = cl;
+    LaneK k[8];
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const uint32_t w = w0 + i;
+      const uint64_t mask = w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
+      uint64_t pw[8];
+      gray_to_planes(cur[i], pw, mask);
+      const uint32_t left = i ? (dl >> (8 * (i - 1))) & 0xffu : dprev & 0xffu;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b >= np) break;
+        if (w < g.used) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = pw[b];
+        uint64_t R = pw[b];
+        if constexpr (PREDICT) {
+          const uint64_t D = pw[b] ^ up[i][b];
+          R = (D ^ ((D >> 1) | ((uint64_t)((left >> b) & 1u) << 63))) & mask;
+          if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+          up[i][b] = pw[b];
+        }
+        lanek_word(k[b], R, (int32_t)(w * 64));
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      if (b >= np) break;
+      const uint64_t id = (uint64_t)b * g.rows + row;
+      lanek_store(k[b], krec + id, kpos + id, sones + id);
+    }
+  }
+}
+
+bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes) {
+  return g.used <= 256 && pitch % 16 == 0 && pitch >= (size_t)g.used * 64 &&
+         reinterpret_cast<uintptr_t>(gray) % 16 == 0 && reinterpret_cast<uintptr_t>(planes) % 8 == 0;
+}
+
+void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
+                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos) {
+  const uint64_t waves = (g.rows + kGrayRows - 1) / kGrayRows;
+  const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
+#define BIC_GRAY(LW, P) k_gray_rows<LW, P><<<grid, kBlock, 0, s>>>(gray, pitch, g, planes, sones, krec, kpos)
+  if (g.used <= 64) { if (predict) BIC_GRAY(1, true); else BIC_GRAY(1, false); }
+  else if (g.used <= 128) { if (predict) BIC_GRAY(2, true); else BIC_GRAY(2, false); }
+  else { if (predict) BIC_GRAY(4, true); else BIC_GRAY(4, false); }
+#undef BIC_GRAY
 }
 
 void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,

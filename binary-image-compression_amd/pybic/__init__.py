@@ -26,7 +26,7 @@ EXPORTS = [
     "bic_encode_planes", "bic_encode_planes2", "bic_ctx_set_option", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
-    "bic_patch_search", "bic_match_encode", "bic_set_match_parts",
+    "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
 ]
 
 
@@ -92,6 +92,7 @@ def load(path=LIB_PATH):
     sig("bic_patch_search", i32, [vp, vp, sz, sz, sz, u32, vp, vp, vp])
     sig("bic_match_encode", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_set_match_parts", i32, [vp, u32])
+    sig("bic_encode_gray", i32, [vp, vp, sz, sz, sz, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
     _lib = L
     return L
 
@@ -244,11 +245,45 @@ class Context:
                                               _p(bg), _p(oe), se, _p(be)), "bic_encode_planes2")
         return (og, bg) if golomb else None, (oe, be) if eg else None
 
+    def encode_gray(self, gray, cols=None, nplanes=8, predict=True, planes=None, slots=(None, None),
+                    outs=(None, None), bits=(None, None), golomb=True, eg=True):
+        """gray uint8 [rows, pitch] -> (planes, (out_g, bits_g) or None, (out_e, bits_e) or None):
+        the bitplanes and both streams of every plane in one call (bic_encode_gray)."""
+        rows, pitch = gray.shape
+        cols = pitch if cols is None else cols
+        wpr = (cols + 63) // 64
+        if planes is None:
+            planes = self.empty_i64(nplanes, rows, wpr)
+        wpr = planes.shape[-1]
+        res = []
+        for on, coder, slot, out, b in ((golomb, CODER_GOLOMB, slots[0], outs[0], bits[0]),
+                                        (eg, CODER_EG, slots[1], outs[1], bits[1])):
+            if not on:
+                res.append((None, 0, None))
+                continue
+            slot = slot or self.slot_words(rows, cols, coder)
+            out = self.empty_i64(nplanes, slot) if out is None else out
+            b = self.empty_i64(nplanes) if b is None else b
+            res.append((out, slot, b))
+        (og, sg, bg), (oe, se, be) = res
+        self._bind_stream()
+        self._chk(self.lib.bic_encode_gray(self.h, _p(gray), pitch, rows, cols, nplanes, _p(planes), wpr,
+                                           int(predict), _p(og), sg, _p(bg), _p(oe), se, _p(be)), "bic_encode_gray")
+        return planes, ((og, bg) if golomb else None), ((oe, be) if eg else None)
+
+    def set_encoder(self, name):
+        """row encoder for rows <= 16384 columns: "staged" (default), "single-kernel", "two-pass",
+        "multipass" (bic_ctx_set_option)"""
+        assert name in ("staged", "single-kernel", "two-pass", "multipass"), name
+        self.set_multipass(name == "multipass")
+        self._chk(self.lib.bic_ctx_set_option(self.h, 2, int(name == "two-pass")), "bic_ctx_set_option")
+        self._chk(self.lib.bic_ctx_set_option(self.h, 3, int(name == "single-kernel")), "bic_ctx_set_option")
+
     def set_multipass(self, on=True):
         self._chk(self.lib.bic_ctx_set_option(self.h, 1, int(on)), "bic_ctx_set_option")
 
     def set_two_pass(self, on=True):
-        """the two-pass row encoder instead of the default single-kernel one"""
+        """the two-pass row encoder instead of the default staged one"""
         self._chk(self.lib.bic_ctx_set_option(self.h, 2, int(on)), "bic_ctx_set_option")
 
     def golomb_encode_samples(self, samples, n0=0, a0=0, bit0=0, cap_words=None, out=None):

@@ -70,10 +70,14 @@ int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
 /* Options: BIC_OPT_MULTIPASS = 1 forces the multi-pass chunk kernels for every geometry
  * (cross-checking the row encoders); 0 (default) picks a row encoder where it applies. */
 #define BIC_OPT_MULTIPASS 1
-/* BIC_OPT_TWO_PASS = 1 selects the two-pass row encoder (lengths and offsets first, then every
- * row written independently) instead of the default single-kernel one (rows stage in LDS until
- * their offset is known). Same output; kept as a cross-check and for comparison. */
+/* Row encoders (same output; the alternatives are kept as cross-checks and for comparison).
+ * Default: the staged encoder -- per-row sample counts, per-plane scans and per-row Golomb
+ * lengths first, then every row written independently (planes 16-byte aligned, even row pitch;
+ * otherwise the single kernel is used). BIC_OPT_TWO_PASS = 1: lengths and offsets found by
+ * decoupled look-backs, then every row written. BIC_OPT_SINGLE_KERNEL = 1: one kernel, rows staged
+ * in LDS until decoupled look-backs give their offsets. */
 #define BIC_OPT_TWO_PASS 2
+#define BIC_OPT_SINGLE_KERNEL 3
 int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
 
 /* ---- a2: bitplane extraction (bitplane_tool.cpp:24-30) -----------------------------------
@@ -105,6 +109,14 @@ int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t 
 int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
                        size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
                        uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg);
+/* a2 + a5-a10 in one call: bitplane_tool.cpp:24-30's planes of a gray image (as
+ * bic_bitplanes_u8, into `planes`) and both streams of every plane (as bic_encode_planes2). Rows of
+ * up to 16384 columns whose gray rows hold ceil(cols/64)*64 readable bytes (pitch >= that, gray and
+ * pitch 16-byte aligned) read the image once: the bitplane kernel also produces the encoder's
+ * per-row counts. Otherwise the same result through the two separate calls. */
+int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,
+                    uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                    uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg);
 /* A slot size (64-bit words) that every plane of this geometry fits for EG (exact) and for
  * Golomb on any input this build has seen (2*rows*(cols+1) bits + 64 words); a larger input
  * still reports BIC_ENOSPC rather than writing out of bounds. */

@@ -1,4 +1,4 @@
-"""The row encoders (bic_fused.hip: the default two-pass one and the single-kernel one) against the
+"""The row encoders (bic_fused.hip: the default staged one, the single kernel and the two-pass one) against the
 oracle and against the multi-pass chunk kernels, with inputs built to reach each of their paths:
 k = 0 copy mode, byte tables, lanes whose codewords exceed the 128-bit register string, rows whose
 output exceeds the LDS window (global fallback), many short rows sharing one output word (fixup
@@ -29,11 +29,11 @@ def check(ctx, oracle, P, cols, pred, both=True):
             assert stream_bytes(out[k], nb) == est.tobytes(), (k, coder)
 
 
-@pytest.fixture(params=["single_pass", "two_pass"])
+@pytest.fixture(params=["staged", "single-kernel", "two-pass"])
 def encoder(request, ctx):
-    ctx.set_two_pass(request.param == "two_pass")
+    ctx.set_encoder(request.param)
     yield request.param
-    ctx.set_two_pass(False)
+    ctx.set_encoder("staged")
 
 
 @pytest.mark.parametrize("rows,cols", [(1, 1), (3, 64), (7, 65), (64, 100), (50, 1000), (40, 4096), (20, 8191),
@@ -60,19 +60,18 @@ def test_fused_vs_multipass(ctx, oracle):
     P = np.stack([oracle.gen_plane(77 + k, p, rows, cols) for k, p in enumerate([0.5, 0.1, 0.01])])
     d = ctx.to_dev(P)
     res = {}
-    for mode in ("single_pass", "two_pass", "multipass"):
-        ctx.set_multipass(mode == "multipass")
-        ctx.set_two_pass(mode == "two_pass")
+    modes = ("staged", "single-kernel", "two-pass", "multipass")
+    for mode in modes:
+        ctx.set_encoder(mode)
         (og, bg), (oe, be) = ctx.encode_planes2(d, cols, True)
         ctx.sync()
         res[mode] = [(as_u64(bg), [stream_bytes(og[k], as_u64(bg)[k]) for k in range(3)]),
                      (as_u64(be), [stream_bytes(oe[k], as_u64(be)[k]) for k in range(3)])]
-    ctx.set_multipass(False)
-    ctx.set_two_pass(False)
-    for mode in ("two_pass", "multipass"):
+    ctx.set_encoder("staged")
+    for mode in modes[1:]:
         for c in range(2):
-            assert np.array_equal(res["single_pass"][c][0], res[mode][c][0])
-            assert res["single_pass"][c][1] == res[mode][c][1]
+            assert np.array_equal(res["staged"][c][0], res[mode][c][0])
+            assert res["staged"][c][1] == res[mode][c][1]
 
 
 def test_long_lane_and_global_fallback(ctx, oracle, encoder):
@@ -134,3 +133,64 @@ def test_fused_overflow(ctx, oracle, encoder):
     assert e.value.code == pybic.BIC_ENOSPC
     assert (as_u64(buf[2 * slot:]) == 0x77).all()
     ctx.sync()
+
+
+@pytest.mark.parametrize("p", [0.5, 0.35, 0.2])
+def test_k_classes_wide_rows(ctx, oracle, encoder, p):
+    """hundreds of 16384-column rows: the coder state drifts far enough from the k boundaries that
+    the staged encoder proves whole rows k = 0 or k = 1 (closed-form lengths, copy and k = 1 table
+    rows) next to the rows that straddle a boundary (walked)."""
+    rows, cols = 400, 16384
+    P = oracle.gen_plane(4242 + int(100 * p), p, rows, cols)
+    for pred in (0, 1):
+        check(ctx, oracle, P, cols, pred)
+
+
+def _gray(oracle, seed, rows, cols, kind):
+    if kind == "uniform":
+        return oracle.gen_bytes(seed, rows * cols).reshape(rows, cols)
+    # smooth gradient + small noise: high planes have long runs (k >= 2, walked rows)
+    i, j = np.mgrid[0:rows, 0:cols]
+    noise = oracle.gen_bytes(seed, rows * cols).reshape(rows, cols) % 7
+    return ((i * 3 + j // 5 + noise) % 256).astype(np.uint8)
+
+
+@pytest.mark.parametrize("rows,cols,pitch,nplanes,kind", [
+    (1, 64, 64, 8, "uniform"), (17, 100, 128, 8, "uniform"), (33, 4096, 4096, 8, "uniform"),
+    (40, 5000, 5120, 3, "smooth"), (24, 16384, 16384, 8, "uniform"), (70, 16384, 16384, 8, "smooth"),
+    (9, 300, 300, 8, "uniform"),  # pitch < used * 64: the two-call path
+    (12, 200, 208, 5, "smooth"),  # pitch < used * 64 (256): the two-call path
+])
+def test_encode_gray(ctx, oracle, rows, cols, pitch, nplanes, kind):
+    """bic_encode_gray == bitplane_tool's planes (oracle) and each plane's Golomb and EG streams"""
+    t = ctx.torch
+    img = np.zeros((rows, pitch), np.uint8)
+    img[:, :cols] = _gray(oracle, rows * 7 + cols, rows, cols, kind)
+    img[:, cols:] = 0xA5  # bytes past cols never reach a plane
+    g = t.from_numpy(img).to(ctx.dev)
+    for pred in (1, 0):
+        planes, (og, bg), (oe, be) = ctx.encode_gray(g, cols=cols, nplanes=nplanes, predict=bool(pred))
+        ctx.sync()
+        exp_planes = oracle.bitplanes(np.ascontiguousarray(img[:, :cols]), nplanes)
+        assert np.array_equal(as_u64(planes), exp_planes)
+        for k in range(nplanes):
+            for coder, out, bits in ((0, og, bg), (1, oe, be)):
+                eb, est, _ = oracle.encode_plane(exp_planes[k], cols, pred, coder)
+                nb = int(as_u64(bits)[k])
+                assert nb == eb, (pred, k, coder)
+                assert stream_bytes(out[k], nb) == est.tobytes(), (pred, k, coder)
+
+
+def test_encode_gray_matches_two_calls(ctx, oracle):
+    rows, cols = 300, 16384
+    img = _gray(oracle, 5, rows, cols, "uniform")
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    planes, (og, bg), (oe, be) = ctx.encode_gray(g)
+    p2 = ctx.bitplanes_u8(g, nplanes=8)
+    (og2, bg2), (oe2, be2) = ctx.encode_planes2(p2, cols, True)
+    ctx.sync()
+    assert np.array_equal(as_u64(planes), as_u64(p2))
+    assert np.array_equal(as_u64(bg), as_u64(bg2)) and np.array_equal(as_u64(be), as_u64(be2))
+    for k in range(8):
+        assert stream_bytes(og[k], as_u64(bg)[k]) == stream_bytes(og2[k], as_u64(bg2)[k])
+        assert stream_bytes(oe[k], as_u64(be)[k]) == stream_bytes(oe2[k], as_u64(be2)[k])

@@ -27,7 +27,7 @@ lib = pybic.load()
 lib.bic_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
 assert lib.bic_debug_stamps(buf.ctypes.data, n) == 0
 S = buf.reshape(-1, 8).astype(np.int64)
-names = ["load", "wait_ones", "eg", "golomb", "wait_bits", "write"]
+names = ["load", "wait_ones", "len+eg", "golomb", "barrier", "write"]
 d = np.diff(S[:, :7], axis=1)
 ok = (S[:, 0] > 0) & (d >= 0).all(axis=1)
 d = d[ok]
