@@ -409,6 +409,7 @@ int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows
   if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
   bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
   fs.counted = true;
+  fs.ns = bic::gray_strips(g);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                       bits_eg, ctx->flags, bic::kEncStaged, st);

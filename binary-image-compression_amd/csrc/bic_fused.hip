@@ -1125,101 +1125,107 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
 // wave walks its rows independently (persistent waves, static row order, no barriers).
 // ==========================================================================================
 
-// Exclusive per-plane scan of per-row values, one 1024-thread workgroup per plane, each thread
-// owning a run of consecutive rows. ONES: the strips' 1-counts (sones) -> row_o[], the ones before each row.
-// Otherwise: glen[] Golomb lengths -> gboff[] absolute bit offsets in the plane's slot, bits_g[]
-// the plane's total; rows past the slot's end get glen = 0 and raise the overflow flag.
 constexpr uint64_t kK0Row = 1ull << 63;  // glen flags: every codeword of the row has k = 0,
 constexpr uint64_t kK1Row = 1ull << 62;  // every codeword of the row has k = 1
 constexpr uint64_t kLenMask = kK1Row - 1;
-template <bool ONES>
-__global__ __launch_bounds__(1024) void k_scan_plane(FusedArgs a) {
-  __shared__ uint64_t tmp[17];
+
+// Golomb length of a row from its sample base O (ones of the plane before it): rows whose k
+// statistics (bic_kstat.h) prove every codeword k = 0 (length cols + 1: the residual row and its
+// end-of-row '1') or k = 1 (2n + (zeros - odd runs) / 2) get their length without being read;
+// returns true for the others (k_row_walk walks them).
+__device__ __forceinline__ bool row_class(const FusedArgs& a, uint64_t id, uint32_t row, uint32_t O) {
   const Geom& g = a.g;
-  const uint32_t plane = blockIdx.x;
-  const uint64_t base = (uint64_t)plane * g.rows;
-  constexpr int kPer = 16;  // rows per thread and pass: all loads in flight before any is used
-  uint64_t carry = 0;
-  for (uint32_t c0 = 0; c0 < g.rows; c0 += 1024 * kPer) {
-    const uint32_t r0 = c0 + threadIdx.x * kPer;
-    uint64_t v[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const uint32_t r = r0 + i;
-      if constexpr (ONES) {
-        uint64_t o = 0;
-        if (r < g.rows)
-          for (uint32_t q = 0; q < a.ns; ++q) o += a.sones[(base + r) * a.ns + q];
-        v[i] = o;
-      } else {
-        v[i] = r < g.rows ? (a.glen[base + r] & kLenMask) : 0;
-      }
-    }
-    uint64_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) sum += v[i];
-    uint64_t tot;
-    uint64_t pre = block_excl_scan<uint64_t>(sum, tmp, tot) + carry;
-    carry += tot;
-    if constexpr (ONES) {
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        if (r0 + i < g.rows) a.row_o[base + r0 + i] = (uint32_t)pre;
-        pre += v[i];
-      }
-    } else {
-      const uint64_t cap = a.slot_g * 64;
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const uint32_t r = r0 + i;
-        if (r < g.rows) {
-          a.gboff[base + r] = (uint64_t)plane * cap + pre;
-          if (pre + v[i] > cap) {
-            a.glen[base + r] = 0;  // overflowed: nothing written, fixup skips
-            atomicOr(&a.flags[0], 1u);
-          }
-        }
-        pre += v[i];
-      }
-    }
+  if (row == 0) return true;  // (the plane's first sample has k = 1 from the fresh state, Golomb.h:18)
+  const RowK rk = row_kstats(a.krec + id * a.ns, a.kpos + id * a.ns, a.ns, g.cols);
+  const int64_t N0 = (int64_t)O + row, A0 = (int64_t)row * g.cols - O;
+  if (A0 - N0 + rk.q0 <= 0) {
+    a.glen[id] = kK0Row | (g.cols + 1);
+    return false;
   }
-  if (!ONES && threadIdx.x == 0) a.bits_g[plane] = carry;
+  if (A0 - 2 * N0 + rk.qh <= 0 && A0 - N0 + rk.ql > 0) {
+    const uint64_t n = rk.ones + 1, zeros = g.cols - rk.ones, odd = n - rk.chg;
+    a.glen[id] = kK1Row | (2 * n + (zeros - odd) / 2);
+    return false;
+  }
+  return true;
 }
 
-// Golomb length of every row from its sample base (ones before it), one lane per row: rows whose k
-// statistics (bic_kstat.h) prove every codeword k = 0 (length cols + 1: the residual row and its
-// end-of-row '1') or k = 1 (2n + (zeros - odd runs) / 2) get their length without being read; the
-// others are appended to a list (k_row_walk).
-__global__ __launch_bounds__(256) void k_row_class(FusedArgs a) {
+// Exclusive per-plane scan of per-row values. Each 1024-thread workgroup owns kScanChunk rows of a
+// plane (kScanPer consecutive rows per thread) and sums the plane's earlier rows itself (coalesced,
+// at most rows / 1024 loads per thread), so no workgroup waits on another and a plane spreads over
+// rows / kScanChunk CUs. ONES: the strips' 1-counts (sones) -> row_o[], the ones before each row;
+// with CLASSIFY each row is also classified (row_class) and the rows to walk are appended to
+// walk_ids. Otherwise: glen[] Golomb lengths -> gboff[] absolute bit offsets in the plane's slot,
+// bits_g[] the plane's total; rows past the slot's end get glen = 0 and raise the overflow flag
+// (a later chunk may then sum a zeroed length: its offsets stay inside the slot, and the call
+// reports BIC_ENOSPC with the stream undefined).
+constexpr uint32_t kScanPer = 2, kScanChunk = 1024 * kScanPer;
+template <bool ONES, bool CLASSIFY>
+__global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
+  __shared__ uint64_t tmp[17];
   const Geom& g = a.g;
-  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  bool walk = false;
-  if (id < nrows) {
-    const uint32_t row = (uint32_t)(id % g.rows);
-    walk = true;
-    if (row > 0) {  // (the plane's first sample has k = 1 from the fresh state, Golomb.h:18)
-      const uint32_t O = a.row_o[id];
-      const RowK rk = row_kstats(a.krec + id * a.ns, a.kpos + id * a.ns, a.ns, g.cols);
-      const int64_t N0 = (int64_t)O + row, A0 = (int64_t)row * g.cols - O;
-      if (A0 - N0 + rk.q0 <= 0) {
-        a.glen[id] = kK0Row | (g.cols + 1);
-        walk = false;
-      } else if (A0 - 2 * N0 + rk.qh <= 0 && A0 - N0 + rk.ql > 0) {
-        const uint64_t n = rk.ones + 1, zeros = g.cols - rk.ones, odd = n - rk.chg;
-        a.glen[id] = kK1Row | (2 * n + (zeros - odd) / 2);
-        walk = false;
-      }
+  const uint32_t nb = (g.rows + kScanChunk - 1) / kScanChunk;
+  const uint32_t plane = blockIdx.x / nb, b = blockIdx.x % nb;
+  const uint64_t base = (uint64_t)plane * g.rows;
+  auto val = [&](uint32_t r) -> uint64_t {
+    if constexpr (ONES) {
+      uint64_t o = 0;
+      for (uint32_t q = 0; q < a.ns; ++q) o += a.sones[(base + r) * a.ns + q];
+      return o;
+    } else {
+      return a.glen[base + r] & kLenMask;
     }
+  };
+  const uint32_t r0 = b * kScanChunk + threadIdx.x * kScanPer;
+  uint64_t v[kScanPer], sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kScanPer; ++i) {
+    v[i] = r0 + i < g.rows ? val(r0 + i) : 0;
+    sum += v[i];
   }
-  // wave-aggregated append to the list of rows to walk
-  const uint64_t m = __ballot(walk);
-  if (!m) return;
-  uint32_t base = 0;
-  const int leader = __builtin_ctzll(m);
-  if (lane_id() == leader) base = atomicAdd(a.counter + 2, (uint32_t)__popcll(m));
-  base = (uint32_t)__shfl((int)base, leader);
-  if (walk) a.walk_ids[base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)id;
+  uint64_t before = 0;  // this thread's share of the plane's rows before the chunk
+  const uint32_t lim = b * kScanChunk;
+#pragma unroll 8
+  for (uint32_t r = threadIdx.x; r < lim; r += 1024) before += val(r);
+  uint64_t tot, btot;
+  uint64_t pre = block_excl_scan<uint64_t>(sum, tmp, tot);
+  (void)block_excl_scan<uint64_t>(before, tmp, btot);
+  pre += btot;
+  if constexpr (ONES) {
+#pragma unroll
+    for (uint32_t i = 0; i < kScanPer; ++i) {
+      const uint32_t r = r0 + i;
+      const bool in = r < g.rows;
+      if (in) a.row_o[base + r] = (uint32_t)pre;
+      if constexpr (CLASSIFY) {
+        const bool walk = in && row_class(a, base + r, r, (uint32_t)pre);
+        const uint64_t m = __ballot(walk);  // wave-aggregated append to the list of rows to walk
+        if (m) {
+          uint32_t wb = 0;
+          const int leader = __builtin_ctzll(m);
+          if (lane_id() == leader) wb = atomicAdd(a.counter + 2, (uint32_t)__popcll(m));
+          wb = (uint32_t)__shfl((int)wb, leader);
+          if (walk) a.walk_ids[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)(base + r);
+        }
+      }
+      pre += v[i];
+    }
+  } else {
+    const uint64_t cap = a.slot_g * 64;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanPer; ++i) {
+      const uint32_t r = r0 + i;
+      if (r < g.rows) {
+        a.gboff[base + r] = (uint64_t)plane * cap + pre;
+        if (pre + v[i] > cap) {
+          a.glen[base + r] = 0;  // overflowed: nothing written, fixup skips
+          atomicOr(&a.flags[0], 1u);
+        }
+      }
+      pre += v[i];
+    }
+    if (b == nb - 1 && threadIdx.x == 0) a.bits_g[plane] = btot + tot;
+  }
 }
 
 // The listed rows' Golomb lengths, one wave per row (codeword walk, word_len); a fixed grid strides
@@ -1261,7 +1267,8 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
 // (k_fixup). One wave per row, 4-wave workgroups, no barriers after the byte tables are staged
 // (XCD-remapped block order: the waves of one XCD hold consecutive rows, the row above is an L2 hit).
 constexpr int kEmitWaves = 4;
-template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+constexpr bool kEmitPrefetch = false;  // the next row's loads in flight (costs 16+ VGPRs: occupancy)
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E, bool REST>
 __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * (kGImg + kEImg)];
   __shared__ uint32_t s_lut[512];
@@ -1276,30 +1283,44 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
   // persistent waves: rows id, id + stride, ... with the next row's loads in flight
   const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
-  uint64_t id = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
+  uint64_t it = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
+  // REST: the rows the main launch listed (counter[3]); otherwise every row
+  const uint64_t nwork =
+      REST ? (uint64_t)__hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : nrows;
+  constexpr bool kPre = kEmitPrefetch && !REST;
   uint64_t np_[WPL], nu_[WPL];
   uint32_t nO = 0;
   uint64_t nLf = 0;
-  if (id < nrows) {
+  if (kPre && it < nwork) {
+    const uint64_t id = it;
     row_load<WPL, PREDICT>(a.planes, g, (uint32_t)(id / g.rows), (uint32_t)(id % g.rows), np_, nu_);
     nO = a.row_o[id];
     nLf = DO_G ? a.glen[id] : 0;
   }
-  for (; id < nrows; id += stride) {
+  for (; it < nwork; it += stride) {
+  const uint64_t id = REST ? (uint64_t)a.walk_ids[it] : it;
   const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
   uint64_t cp_[WPL], cu_[WPL];
+  uint32_t O;
+  uint64_t Lf;
+  if constexpr (kPre) {
 #pragma unroll
-  for (int t = 0; t < WPL; ++t) {
-    cp_[t] = np_[t];
-    cu_[t] = nu_[t];
-  }
-  const uint32_t O = nO;
-  const uint64_t Lf = nLf;
-  if (id + stride < nrows) {
-    const uint64_t id2 = id + stride;
-    row_load<WPL, PREDICT>(a.planes, g, (uint32_t)(id2 / g.rows), (uint32_t)(id2 % g.rows), np_, nu_);
-    nO = a.row_o[id2];
-    nLf = DO_G ? a.glen[id2] : 0;
+    for (int t = 0; t < WPL; ++t) {
+      cp_[t] = np_[t];
+      cu_[t] = nu_[t];
+    }
+    O = nO;
+    Lf = nLf;
+    if (it + stride < nwork) {
+      const uint64_t id2 = it + stride;
+      row_load<WPL, PREDICT>(a.planes, g, (uint32_t)(id2 / g.rows), (uint32_t)(id2 % g.rows), np_, nu_);
+      nO = a.row_o[id2];
+      nLf = DO_G ? a.glen[id2] : 0;
+    }
+  } else {
+    row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
+    O = a.row_o[id];
+    Lf = DO_G ? a.glen[id] : 0;
   }
   const uint64_t L = Lf & kLenMask;
   const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
@@ -1307,7 +1328,11 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
 #ifdef BIC_STAMPS
   if (a.dbg & 1) gen = false;
 #endif
-  if (gen) {  // zero the Golomb image
+  // the main launch leaves the rows with mixed k (per-codeword k) to REST: that path alone costs
+  // ~50 VGPRs, which would halve the main launch's occupancy
+  const bool mixed = gen && !k1;
+  const bool gk1 = !REST && gen && k1, gmix = REST && mixed;
+  if (gk1 || gmix) {  // zero the Golomb image
     uint4* z = reinterpret_cast<uint4*>(gimg);
     for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
   }
@@ -1325,7 +1350,8 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
     f_here = wave_sum_u32(ones) > 0;
     fcol = wave_min(fcol);
   }
-  if (f_here) {  // EG image (~R, pad-masked, EOL '1') of the row holding the plane's first 1 (write_row inserts its '0')
+  if (!REST && lane == 0 && (mixed || f_here)) a.walk_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)id;
+  if (REST && f_here) {  // EG image (~R, pad-masked, EOL '1') of the row holding the plane's first 1 (write_row inserts its '0')
 #pragma unroll
     for (int t = 0; t < WPL; ++t) {
       const uint32_t w = t * 64 + lane;
@@ -1350,24 +1376,27 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
     const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
     const uint64_t cap = a.slot_e * 64;
     const uint64_t Ge = (uint64_t)plane * cap + Ge_rel;
-    if (Ge_rel + Le <= cap) {
-      if (f_here) write_row(eimg, Le, Ge, (int64_t)fcol + 1, a.out_e, a.efrag + 2 * id);
-      else eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
-      if (lane == 0) { a.eboff[id] = Ge; a.elen[id] = Le; }
-    } else if (lane == 0) {
-      a.eboff[id] = Ge;
-      a.elen[id] = 0;
-      atomicOr(&a.flags[0], 1u);
+    if (REST) {
+      if (f_here && Ge_rel + Le <= cap) write_row(eimg, Le, Ge, (int64_t)fcol + 1, a.out_e, a.efrag + 2 * id);
+    } else {
+      if (Ge_rel + Le <= cap) {
+        if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
+        if (lane == 0) { a.eboff[id] = Ge; a.elen[id] = Le; }
+      } else if (lane == 0) {
+        a.eboff[id] = Ge;
+        a.elen[id] = 0;
+        atomicOr(&a.flags[0], 1u);
+      }
+      if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
     }
-    if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
   }
   if constexpr (DO_G) {
-    if (k0 && L) {
+    if (!REST && k0 && L) {
 #ifdef BIC_STAMPS
       if (!(a.dbg & 4))
 #endif
       eg_row_regs<WPL, false>(rr, g, a.gboff[id], L, a.out_g, a.gfrag + 2 * id);
-    } else if (gen && k1) {  // every codeword k = 1: branch-free byte-table words
+    } else if (gk1) {  // every codeword k = 1: branch-free byte-table words
       int jpc = -1;
       uint32_t loc = 0;
 #pragma unroll
@@ -1394,7 +1423,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
-    } else if (gen) {
+    } else if (gmix) {
       StepState st{O + row, -1};
       const uint32_t arow = row * (g.cols + 1);
       uint64_t loc = 0;
@@ -1425,8 +1454,9 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
       __builtin_amdgcn_wave_barrier();
       write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
     }
-    if (lane == 0) {
-      if (k0 || k1) a.glen[id] = L;  // drop the flags: k_fixup reads plain lengths
+    // drop the flags (k_fixup reads plain lengths); a listed row's only after REST has read them
+    if (lane == 0 && (k0 || k1) && f_here == REST) a.glen[id] = L;
+    if (!REST && lane == 0) {
       const bool slow = L && !k0 && !fits;
       a.gslow[id] = slow ? O + row + 1 : 0;  // k_rows_global writes the row
       if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
@@ -1546,18 +1576,19 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   if (mode == kEncStaged) {
     if (stage == kFusedPrefix) {
       if (!fs.counted) launch_row_ones(s, g, planes, predict, fs.sones, fs.krec, fs.kpos);
-      k_scan_plane<true><<<g.nplanes, 1024, 0, s>>>(a);
+      const uint32_t sgrid = (g.rows + kScanChunk - 1) / kScanChunk * g.nplanes;
+      if (dg) k_scan_rows<true, true><<<sgrid, 1024, 0, s>>>(a);
+      else k_scan_rows<true, false><<<sgrid, 1024, 0, s>>>(a);
       if (dg) {
-        k_row_class<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
 #define BIC_WALK(W) \
   if (predict) k_row_walk<W, true><<<kWalkBlocks, 256, 0, s>>>(a); else k_row_walk<W, false><<<kWalkBlocks, 256, 0, s>>>(a)
         if (wpl == 1) { BIC_WALK(1); } else if (wpl == 2) { BIC_WALK(2); } else { BIC_WALK(4); }
 #undef BIC_WALK
-        k_scan_plane<false><<<g.nplanes, 1024, 0, s>>>(a);
+        k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);
       }
       return;
     }
-    // persistent grid: 8 workgroups per CU at most (more rows per wave when the image is larger)
+    // persistent grids (more rows per wave when the image is larger)
     static thread_local int cus = 0;
     if (!cus) {
       int dev = 0;
@@ -1565,10 +1596,13 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (cus <= 0) cus = 256;
     }
-    const uint32_t egrid2 = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 8);
+    // one resident wave set: 4 workgroups per CU (the main launch holds <= 128 VGPRs: 4 waves per SIMD)
+    const uint32_t egrid2 = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 4);
+    const uint32_t rgrid = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 2);
 #define BIC_EMIT1(W, P, DG, DE)                                                                        \
   {                                                                                                  \
-    k_emit_known<W, P, DG, DE><<<egrid2, 64 * kEmitWaves, 0, s>>>(a);                                \
+    k_emit_known<W, P, DG, DE, false><<<egrid2, 64 * kEmitWaves, 0, s>>>(a);                         \
+    k_emit_known<W, P, DG, DE, true><<<rgrid, 64 * kEmitWaves, 0, s>>>(a);                           \
   }
 #define BIC_EMIT(W, P)                                                                                \
   if (dg && de) BIC_EMIT1(W, P, true, true) else if (dg) BIC_EMIT1(W, P, true, false) else BIC_EMIT1(W, P, false, true)

@@ -120,8 +120,10 @@ constexpr int kEncStaged = 0, kEncSingle = 1, kEncTwoPass = 2;
 constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2, kFusedPrefix = 3;
 void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint32_t* sones,
                      int4* krec, uint32_t* kpos);
-// bitplanes + the count pass in one read of the gray image (bic_encode_gray)
+// bitplanes + the count pass in one read of the gray image (bic_encode_gray); gray_strips(g)
+// k statistics records per row (one per 64-word strip)
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes);
+uint32_t gray_strips(const Geom& g);
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos);
 

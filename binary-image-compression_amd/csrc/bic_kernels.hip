@@ -300,12 +300,16 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 }
 
 // From the gray image (bic_encode_gray: bitplane_tool.cpp:24-30 and the count pass in one read):
-// kGrayRows whole rows per wave; lane l loads the 64 * LW pixels of its words (16-byte loads),
-// turns each 64 into one word per plane (K1's 8x8 transposes), stores the plane words, and forms
-// the med residual from the row above (plane words kept in registers) and the left neighbour (the
-// pixel before each word: the lane's own bytes, or lane l - 1's last). The gray rows must hold
-// used * 64 readable bytes (pitch >= used * 64, 16-byte aligned; gray_rows_supported).
+// one wave per strip of 64 plane words (4096 columns) and kGrayRows rows; lane l owns word
+// 64 s + l of strip s: four 16-byte loads give its 64 pixels, K1's 8x8 transposes one word per
+// plane; the plane words are stored and the med residual is formed from the row above (plane
+// words kept in registers) and the pixel left of the word (lane l - 1's last; lane 0 of strip s > 0
+// loads the byte before the strip). One k statistics record per (plane, row, strip) (lanek_store;
+// row_kstats combines a row's strips). The next row's loads are in flight while a row is used.
+// The gray rows must hold used * 64 readable bytes (pitch >= used * 64, 16-byte aligned;
+// gray_rows_supported).
 constexpr int kGrayRows = 8;
+uint32_t gray_strips(const Geom& g) { return (g.used + 63) / 64; }
 
 __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&pw)[8], uint64_t mask) {
   uint64_t T[8];
@@ -323,85 +327,74 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
   }
 }
 
-template <int LW, bool PREDICT>
-__global__ __launch_bounds__(kBlock) void k_gray_rows(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
-                                                      uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
-                                                      int4* __restrict__ krec, uint32_t* __restrict__ kpos) {
+template <bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
+                                                        uint32_t ns, uint64_t* __restrict__ planes,
+                                                        uint32_t* __restrict__ sones, int4* __restrict__ krec,
+                                                        uint32_t* __restrict__ kpos) {
   const int lane = lane_id();
   const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
-  const uint32_t r0 = (uint32_t)gw * kGrayRows;
+  const uint32_t s = (uint32_t)(gw % ns);  // the strips of one row block are neighbouring waves
+  const uint32_t r0 = (uint32_t)(gw / ns) * kGrayRows;
   if (r0 >= g.rows) return;  // whole wave
   const int np = (int)g.nplanes;
-  const uint32_t w0 = LW * lane;
-  auto load = [&](uint32_t row, uint4 (&v)[LW][4]) {
+  const uint32_t w = s * 64 + lane;
+  const bool in = w < g.used;
+  const uint64_t mask = in ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
+  // the word's 64 pixels, and (lane 0 of strips s > 0) the pixel before the strip
+  auto load = [&](uint32_t row, uint4 (&v)[4], uint32_t& lb) {
+    const uint8_t* src = gray + (uint64_t)row * pitch + (uint64_t)w * 64;
 #pragma unroll
-    for (int i = 0; i < LW; ++i) {
-      const uint4* src = reinterpret_cast<const uint4*>(gray + (uint64_t)row * pitch + (uint64_t)(w0 + i) * 64);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[i][q] = (w0 + i < g.used) ? src[q] : make_uint4(0, 0, 0, 0);
-    }
+    for (int q = 0; q < 4; ++q) v[q] = in ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
+    lb = (lane == 0 && s > 0) ? (uint32_t)src[-1] : 0u;
   };
-  // the last pixel of each of the lane's words, packed 8 bits per word
-  auto lasts = [&](const uint4 (&v)[LW][4]) {
-    uint32_t x = 0;
+  uint64_t up[8];
 #pragma unroll
-    for (int i = 0; i < LW; ++i) x |= (v[i][3].w >> 24) << (8 * i);
-    return x;
-  };
-  uint64_t up[LW][8];
-#pragma unroll
-  for (int i = 0; i < LW; ++i)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) up[i][b] = 0;
-  uint32_t ulast = 0;  // lasts() of the row above
-  uint4 cur[LW][4];
+  for (int b = 0; b < 8; ++b) up[b] = 0;
+  uint32_t ulast = 0, ulb = 0;  // the row above's last pixel of the word / pixel before the strip
+  uint4 cur[4];
+  uint32_t clb;
   if (PREDICT && r0) {
-    load(r0 - 1, cur);
-#pragma unroll
-    for (int i = 0; i < LW; ++i) {
-      const uint32_t w = w0 + i;
-      gray_to_planes(cur[i], up[i], w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull);
-    }
-    ulast = lasts(cur);
+    load(r0 - 1, cur, ulb);
+    gray_to_planes(cur, up, mask);
+    ulast = cur[3].w >> 24;
   }
+  load(r0, cur, clb);
   const uint32_t nr = min((uint32_t)kGrayRows, g.rows - r0);
   for (uint32_t r = 0; r < nr; ++r) {
     const uint32_t row = r0 + r;
-    load(row, cur);
-    // D bits of the pixel left of each word (8 planes per byte): own words' last pixels, lane l - 1's
-    // last word for the first
-    const uint32_t cl = lasts(cur);
+    uint4 nxt[4];
+    uint32_t nlb = 0;
+    if (r + 1 < nr) load(row + 1, nxt, nlb);
+    // D bits (8 planes per byte) of the pixel left of the word: lane l - 1's last, or the strip's
+    // preceding pixel for lane 0 (0 at column 0)
+    const uint32_t cl = cur[3].w >> 24;
     const uint32_t dl = (PREDICT && row) ? cl ^ ulast : cl;
-    const uint32_t dprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(dl >> (8 * (LW - 1))), 0x138, 0xf, 0xf, true);
+    uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x138, 0xf, 0xf, true);
+    if (lane == 0) left = (PREDICT && row) ? clb ^ ulb : clb;
     ulast = cl;
-    LaneK k[8];
-#pragma unroll
-    for (int i = 0; i < LW; ++i) {
-      const uint32_t w = w0 + i;
-      const uint64_t mask = w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
-      uint64_t pw[8];
-      gray_to_planes(cur[i], pw, mask);
-      const uint32_t left = i ? (dl >> (8 * (i - 1))) & 0xffu : dprev & 0xffu;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        if (b >= np) break;
-        if (w < g.used) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = pw[b];
-        uint64_t R = pw[b];
-        if constexpr (PREDICT) {
-          const uint64_t D = pw[b] ^ up[i][b];
-          R = (D ^ ((D >> 1) | ((uint64_t)((left >> b) & 1u) << 63))) & mask;
-          if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
-          up[i][b] = pw[b];
-        }
-        lanek_word(k[b], R, (int32_t)(w * 64));
-      }
-    }
+    ulb = clb;
+    uint64_t pw[8];
+    gray_to_planes(cur, pw, mask);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       if (b >= np) break;
-      const uint64_t id = (uint64_t)b * g.rows + row;
-      lanek_store(k[b], krec + id, kpos + id, sones + id);
+      if (in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = pw[b];
+      uint64_t R = pw[b];
+      if constexpr (PREDICT) {
+        const uint64_t D = pw[b] ^ up[b];
+        R = (D ^ ((D >> 1) | ((uint64_t)((left >> b) & 1u) << 63))) & mask;
+        if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+        up[b] = pw[b];
+      }
+      LaneK k;
+      lanek_word(k, R, (int32_t)(w * 64));
+      const uint64_t id = ((uint64_t)b * g.rows + row) * ns + s;
+      lanek_store(k, krec + id, kpos + id, sones + id);
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    clb = nlb;
   }
 }
 
@@ -412,13 +405,11 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
 
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos) {
-  const uint64_t waves = (g.rows + kGrayRows - 1) / kGrayRows;
+  const uint32_t ns = gray_strips(g);
+  const uint64_t waves = (uint64_t)(g.rows + kGrayRows - 1) / kGrayRows * ns;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
-#define BIC_GRAY(LW, P) k_gray_rows<LW, P><<<grid, kBlock, 0, s>>>(gray, pitch, g, planes, sones, krec, kpos)
-  if (g.used <= 64) { if (predict) BIC_GRAY(1, true); else BIC_GRAY(1, false); }
-  else if (g.used <= 128) { if (predict) BIC_GRAY(2, true); else BIC_GRAY(2, false); }
-  else { if (predict) BIC_GRAY(4, true); else BIC_GRAY(4, false); }
-#undef BIC_GRAY
+  if (predict) k_gray_strips<true><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos);
+  else k_gray_strips<false><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos);
 }
 
 void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,

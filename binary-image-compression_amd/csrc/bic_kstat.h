@@ -1,6 +1,6 @@
 // bic_kstat.h -- Golomb k statistics of row strips: the staged row encoder's count pass
-// (bic_kernels.hip k_med_kstat, k_gray_rows) writes one record per (plane, row, strip);
-// k_row_len (bic_fused.hip) combines a row's records (row_kstats) and, from the coder state at the
+// (bic_kernels.hip k_med_kstat, k_gray_strips) writes one record per (plane, row, strip);
+// k_scan_rows (bic_fused.hip) combines a row's records (row_kstats) and, from the coder state at the
 // row's start, proves that every codeword of the row has k = 0 or k = 1, whose lengths then have
 // closed forms (no per-codeword walk). Included by .hip files only (after bic_device.h).
 //
@@ -21,7 +21,8 @@
 namespace bic {
 
 constexpr int32_t kNoOnes = 1 << 30;
-constexpr uint32_t kMaxStrips = 1;  // records per row (the count kernels cover whole rows)
+constexpr uint32_t kMaxStrips = 4;  // records per row: k_med_kstat covers whole rows (1), k_gray_strips
+                                    // one per 64-word strip (<= 4 for rows of <= 256 words)
 
 // Parity changes between consecutive 1s inside a word: with columns MSB-first a 1's predecessor
 // sits at a higher bit; adding S << 1 to ~x ripples each carry up through the zeros and stops at
@@ -58,6 +59,27 @@ __device__ __forceinline__ void lanek_word(LaneK& k, uint64_t x, int32_t c0) {
 // predecessor. Record {q0, qh, ql, ones | chg << 16} and {first | last << 16} (columns < 2^15,
 // -1 = none); lane 0 stores them and the strip's 1-count.
 __device__ __forceinline__ void lanek_store(const LaneK& k, int4* rec, uint32_t* pos, uint32_t* sones) {
+  if (__ballot(k.ones != 0) == ~0ull) {
+    // Every lane holds a 1 (the common case unless the strip is sparse): a lane's predecessor 1 is
+    // lane l - 1's last and the strip's first / last 1 are lane 0's / lane 63's, so one scan of
+    // (ones | chg << 16) (both <= 16384 per strip) and three reductions finish the record.
+    const int32_t before = dpp_or<0x138>(-1, k.last);
+    const uint32_t chg = k.chg + (before >= 0 ? (uint32_t)((before ^ k.first) & 1) : 0u);
+    const uint32_t inc = wave_incl_sum_u32(k.ones | (chg << 16));
+    const int32_t base = (int32_t)((inc & 0xffffu) - k.ones);
+    const int32_t q0 = wave_max(k.q0 - 2 * base);
+    const int32_t qh = wave_max(k.qh - 3 * base);
+    const int32_t ql = wave_min(k.ql - 2 * base);
+    const uint32_t t = lane63_u32(inc), tot = t & 0xffffu;
+    const uint32_t f = (uint32_t)__builtin_amdgcn_readlane(k.first, 0);
+    const uint32_t last = lane63_u32((uint32_t)k.last);
+    if (lane_id() == 0) {
+      *rec = make_int4(q0, qh, ql, (int32_t)(tot | (t >> 16 << 16)));
+      *pos = (f & 0xffffu) | (last << 16);
+      *sones = tot;
+    }
+    return;
+  }
   const uint32_t inc = wave_incl_sum_u32(k.ones);
   const int32_t base = (int32_t)(inc - k.ones);
   const int mx = wave_incl_max(k.last);
