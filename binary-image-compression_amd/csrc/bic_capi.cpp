@@ -25,6 +25,8 @@ struct bic_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
+  hipStream_t aux = nullptr;      // the staged encoder's second stream (REST emit launch), made on first use
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   uint64_t* lut = nullptr;        // device [3][256] byte table of the fused encoder
@@ -100,6 +102,28 @@ int ensure_scratch(bic_ctx* ctx, size_t bytes) {
   }
   ctx->scratch_bytes = want;
   return BIC_OK;
+}
+
+// The staged encoder's second stream and its fork / join events, made on first use; left null
+// (one stream) when HIP cannot make them. Work on it is always joined back into ctx->cur.
+void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
+  if (!ctx->aux) {
+    hipStream_t st = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
+    if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+      if (a) (void)hipEventDestroy(a);
+      (void)hipStreamDestroy(st);
+      return;
+    }
+    ctx->aux = st;
+    ctx->ev_fork = a;
+    ctx->ev_join = b;
+  }
+  fs.aux = ctx->aux;
+  fs.ev_fork = ctx->ev_fork;
+  fs.ev_join = ctx->ev_join;
 }
 
 bool geom_ok(size_t rows, size_t cols, size_t wpr) {
@@ -185,6 +209,9 @@ int bic_ctx_destroy(bic_ctx* ctx) {
   if (ctx->lentab) (void)hipFree(ctx->lentab);
   if (ctx->staging) (void)hipHostFree(ctx->staging);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   delete ctx;
   return BIC_OK;
 }
@@ -346,7 +373,8 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
   if (bic::fused_supported(g) && !ctx->force_multipass) {
     // one pass: residual -> runs -> both streams (bic_fused.hip)
     if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
-    const bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
+    bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
+    set_aux(ctx, fs);
     const int mode = ctx->two_pass ? bic::kEncTwoPass
                      : (ctx->single_kernel || !bic::med_rows_supported(g, planes, nullptr)) ? bic::kEncSingle
                                                                                             : bic::kEncStaged;
@@ -410,6 +438,7 @@ int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows
   bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
   fs.counted = true;
   fs.ns = bic::gray_strips(g);
+  set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                       bits_eg, ctx->flags, bic::kEncStaged, st);

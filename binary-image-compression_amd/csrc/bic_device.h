@@ -86,7 +86,8 @@ __device__ __forceinline__ int wave_incl_max(int x) {
   return x;
 }
 // reductions (wave-uniform results): quad swaps and the two mirrors give every lane its row's
-// total, the four rows are combined from readlanes
+// total (wave_sum_u64: the four rows are combined from readlanes); the 32-bit ones carry the row
+// totals into row 3 with row_bcast:15 / row_bcast:31 and read lane 63 once
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
   x += dpp0_u64<0xB1>(x);
   x += dpp0_u64<0x4E>(x);
@@ -104,24 +105,27 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
   x += dpp0<0x4E>(x);
   x += dpp0<0x141>(x);
   x += dpp0<0x140>(x);
-  return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) + (uint32_t)__builtin_amdgcn_readlane((int)x, 16) +
-         (uint32_t)__builtin_amdgcn_readlane((int)x, 32) + (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+  x += dpp0<0x142, 0xA>(x);
+  x += dpp0<0x143, 0xC>(x);
+  return lane63_u32(x);
 }
 __device__ __forceinline__ int wave_max(int x) {
   x = max(x, dpp_or<0xB1>(x, x));
   x = max(x, dpp_or<0x4E>(x, x));
   x = max(x, dpp_or<0x141>(x, x));
   x = max(x, dpp_or<0x140>(x, x));
-  return max(max(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
-             max(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+  x = max(x, dpp_or<0x142, 0xA>(INT_MIN, x));
+  x = max(x, dpp_or<0x143, 0xC>(INT_MIN, x));
+  return __builtin_amdgcn_readlane(x, 63);
 }
 __device__ __forceinline__ int wave_min(int x) {
   x = min(x, dpp_or<0xB1>(x, x));
   x = min(x, dpp_or<0x4E>(x, x));
   x = min(x, dpp_or<0x141>(x, x));
   x = min(x, dpp_or<0x140>(x, x));
-  return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
-             min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+  x = min(x, dpp_or<0x142, 0xA>(INT_MAX, x));
+  x = min(x, dpp_or<0x143, 0xC>(INT_MAX, x));
+  return __builtin_amdgcn_readlane(x, 63);
 }
 
 // DPP wave reductions: four in-row steps (quad swaps, half-row and row mirrors: a few cycles each,

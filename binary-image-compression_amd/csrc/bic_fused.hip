@@ -489,6 +489,7 @@ struct FusedArgs {
   uint32_t* kpos;
   uint32_t ns;         // strips per row
   uint32_t* walk_ids;  // staged encoder: rows k_row_walk walks (count in counter[2])
+  uint32_t* rest_ids;  // staged encoder: rows the REST emit launch writes (count in counter[3])
   uint32_t* slow_n;    // number of rows k_rows_global must write (zeroed per launch)
   uint64_t* slow_ids;  // their row ids
   uint64_t* out_g;
@@ -1185,8 +1186,15 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
   }
   uint64_t before = 0;  // this thread's share of the plane's rows before the chunk
   const uint32_t lim = b * kScanChunk;
+  if constexpr (ONES) {  // the records of those rows are one contiguous range
+    const uint32_t* so = a.sones + base * a.ns;
+    const uint64_t flat = (uint64_t)lim * a.ns;
 #pragma unroll 8
-  for (uint32_t r = threadIdx.x; r < lim; r += 1024) before += val(r);
+    for (uint64_t i = threadIdx.x; i < flat; i += 1024) before += so[i];
+  } else {
+#pragma unroll 8
+    for (uint32_t r = threadIdx.x; r < lim; r += 1024) before += val(r);
+  }
   uint64_t tot, btot;
   uint64_t pre = block_excl_scan<uint64_t>(sum, tmp, tot);
   (void)block_excl_scan<uint64_t>(before, tmp, btot);
@@ -1197,8 +1205,9 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       const uint32_t r = r0 + i;
       const bool in = r < g.rows;
       if (in) a.row_o[base + r] = (uint32_t)pre;
+      bool walk = false;
       if constexpr (CLASSIFY) {
-        const bool walk = in && row_class(a, base + r, r, (uint32_t)pre);
+        walk = in && row_class(a, base + r, r, (uint32_t)pre);
         const uint64_t m = __ballot(walk);  // wave-aggregated append to the list of rows to walk
         if (m) {
           uint32_t wb = 0;
@@ -1208,6 +1217,9 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
           if (walk) a.walk_ids[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)(base + r);
         }
       }
+      // the row holding the plane's first 1 (EG inserts a '0' after it): listed for REST here unless
+      // walked (k_row_walk lists it)
+      if (in && pre == 0 && v[i] > 0 && !walk) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)(base + r);
       pre += v[i];
     }
   } else {
@@ -1256,7 +1268,11 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
     }
     ll = wave_sum_u32(ll);
     const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);
-    if (lane == 0) a.glen[id] = ll | (!ks ? kK0Row : (!k1s ? kK1Row : 0));
+    if (lane == 0) {
+      a.glen[id] = ll | (!ks ? kK0Row : (!k1s ? kK1Row : 0));
+      // rows with mixed k, and the row holding the plane's first 1, go to the REST emit launch
+      if ((ks && k1s) || (O == 0 && st.n_carry > O + row)) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)id;
+    }
   }
 }
 
@@ -1288,6 +1304,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
   const uint64_t nwork =
       REST ? (uint64_t)__hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : nrows;
   constexpr bool kPre = kEmitPrefetch && !REST;
+  if constexpr (REST) __builtin_amdgcn_s_setprio(3);  // latency-bound rows beside the main launch: issue first
   uint64_t np_[WPL], nu_[WPL];
   uint32_t nO = 0;
   uint64_t nLf = 0;
@@ -1298,7 +1315,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
     nLf = DO_G ? a.glen[id] : 0;
   }
   for (; it < nwork; it += stride) {
-  const uint64_t id = REST ? (uint64_t)a.walk_ids[it] : it;
+  const uint64_t id = REST ? (uint64_t)a.rest_ids[it] : it;
   const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
   uint64_t cp_[WPL], cu_[WPL];
   uint32_t O;
@@ -1350,7 +1367,6 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
     f_here = wave_sum_u32(ones) > 0;
     fcol = wave_min(fcol);
   }
-  if (!REST && lane == 0 && (mixed || f_here)) a.walk_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)id;
   if (REST && f_here) {  // EG image (~R, pad-masked, EOL '1') of the row holding the plane's first 1 (write_row inserts its '0')
 #pragma unroll
     for (int t = 0; t < WPL; ++t) {
@@ -1501,7 +1517,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 2 + 1024;
+  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024;
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -1526,6 +1542,7 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
   fs.sones = fs.kpos + n * kMaxStrips;
   fs.row_o = fs.sones + n * kMaxStrips;
   fs.walk_ids = fs.row_o + n;
+  fs.rest_ids = fs.walk_ids + n;
   fs.ns = 1;
   fs.counted = false;
   fs.slow_n = fs.counter + 1;  // zeroed with the counter
@@ -1550,7 +1567,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   }
   const bool single_pass = mode == kEncSingle;
   FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
-              fs.eboff, fs.elen, fs.efrag, fs.row_o, fs.sones, fs.krec, fs.kpos, fs.counted ? fs.ns : 1u, fs.walk_ids, fs.slow_n, fs.slow_ids, out_g, slot_g, bits_g, out_e, slot_e,
+              fs.eboff, fs.elen, fs.efrag, fs.row_o, fs.sones, fs.krec, fs.kpos, fs.counted ? fs.ns : 1u, fs.walk_ids, fs.rest_ids, fs.slow_n, fs.slow_ids, out_g, slot_g, bits_g, out_e, slot_e,
               bits_e, flags};
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
@@ -1598,11 +1615,17 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     }
     // one resident wave set: 4 workgroups per CU (the main launch holds <= 128 VGPRs: 4 waves per SIMD)
     const uint32_t egrid2 = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 4);
+    // REST (listed rows, latency bound) first, on the aux stream when there is one: it then runs
+    // beside the main launch, which skips the listed rows' REST parts
     const uint32_t rgrid = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 2);
+    hipStream_t rs = s;
+    if (fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
+        hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
+      rs = fs.aux;
 #define BIC_EMIT1(W, P, DG, DE)                                                                        \
   {                                                                                                  \
+    k_emit_known<W, P, DG, DE, true><<<rgrid, 64 * kEmitWaves, 0, rs>>>(a);                          \
     k_emit_known<W, P, DG, DE, false><<<egrid2, 64 * kEmitWaves, 0, s>>>(a);                         \
-    k_emit_known<W, P, DG, DE, true><<<rgrid, 64 * kEmitWaves, 0, s>>>(a);                           \
   }
 #define BIC_EMIT(W, P)                                                                                \
   if (dg && de) BIC_EMIT1(W, P, true, true) else if (dg) BIC_EMIT1(W, P, true, false) else BIC_EMIT1(W, P, false, true)
@@ -1613,6 +1636,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     }
 #undef BIC_EMIT
 #undef BIC_EMIT1
+    if (rs != s && (hipEventRecord(fs.ev_join, rs) != hipSuccess || hipStreamWaitEvent(s, fs.ev_join, 0) != hipSuccess))
+      (void)hipStreamSynchronize(rs);  // no join event: wait on the host rather than race
     return;
   }
   if (stage == kFusedPrefix) return;

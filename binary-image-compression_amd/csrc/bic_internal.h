@@ -98,6 +98,11 @@ struct FusedScratch {
   uint32_t* kpos;
   uint32_t ns;
   uint32_t* walk_ids;  // rows whose Golomb length is walked (k_row_walk)
+  uint32_t* rest_ids;  // rows the REST emit launch writes (mixed k, the plane's first 1; counter[3])
+  // optional second stream for the REST launch (it then runs beside the main emit launch) and
+  // the fork / join events; null: one stream
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool counted;      // the count pass already ran (bic_encode_gray's fused bitplane kernel)
   uint32_t* slow_n;
   uint64_t* slow_ids;
