@@ -443,16 +443,17 @@ __device__ __forceinline__ bool word_complete(uint64_t w, uint64_t G, uint64_t L
   return w * 64 >= G && w * 64 + 64 <= G + L;
 }
 
-// Write a row image of L bits to absolute bit G of out: whole words with plain stores, the
+// Write a row image of L bits to absolute bit G of out (threads tid of nt: a wave's lanes by
+// default): whole words with plain stores, the
 // first/last word (when shared with another row) into frag[0]/frag[1]. Output word t of the row
 // holds image bits [64t - G%64, 64t - G%64 + 64): the bit shift inside the image's u32 words is
 // the same for every t, so the common case (no inserted bit) is three LDS reads and a funnel
 // shift per word, branch-free and independent across iterations.
 __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint64_t G, int64_t ins,
-                                          uint64_t* out, uint64_t* frag) {
+                                          uint64_t* out, uint64_t* frag, uint32_t tid = lane_id(), uint32_t nt = 64) {
   const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6, nw = w1 - w0 + 1;
   if (ins >= 0) {
-    for (uint64_t t = lane_id(); t < nw; t += 64) {
+    for (uint64_t t = tid; t < nw; t += nt) {
       const uint64_t wb = (w0 + t) * 64;
       const uint64_t v = img64(img, (int64_t)wb - (int64_t)G, ins);
       if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
@@ -461,7 +462,7 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
     return;
   }
   const uint32_t g = (uint32_t)(G & 63);
-  for (uint32_t t = lane_id(); t < (uint32_t)nw; t += 64) {
+  for (uint32_t t = tid; t < (uint32_t)nw; t += nt) {
     const int32_t a = (int32_t)(64 * t) - (int32_t)g;  // first image bit of output word t
     const uint32_t b = a < 0 ? 0u : (uint32_t)a;
     const uint32_t i = b >> 5, sh = b & 31;
@@ -1240,164 +1241,143 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
   }
 }
 
-// The listed rows' Golomb lengths, one wave per row (codeword walk, word_len); a fixed grid strides
-// over the list, whose length k_row_class left in counter[2].
-constexpr uint32_t kWalkBlocks = 1024;
-template <int WPL, bool PREDICT>
+// One row across a workgroup of blockDim.x / 64 (<= 4) waves, lane = word 64 v + lane of wave v:
+// the lane's sample base n (samples of the plane before its word's first 1, from nbase = the
+// samples before the row) and jp (the row's last 1 before its word, -1: none), from wave scans
+// and the earlier waves' totals exchanged through LDS (sh: 8 words); ones = the row's 1s.
+struct WideRow {
+  uint32_t n;
+  int jp;
+  uint32_t ones;
+};
+__device__ __forceinline__ WideRow wide_prefix(uint64_t x, uint32_t w, uint32_t nbase, uint32_t* sh) {
+  const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t pc = (uint32_t)__popcll(x), inc = wave_incl_sum_u32(pc);
+  const int mx = wave_incl_max(x ? (int)(w * 64 + 63 - __builtin_ctzll(x)) : -1);
+  if (lane == 63) {
+    sh[v] = inc;
+    sh[4 + v] = (uint32_t)mx;
+  }
+  __syncthreads();
+  uint32_t nb = nbase, tot = 0;
+  int jb = -1;
+  for (int u = 0; u < nw; ++u) {
+    const uint32_t c = sh[u];
+    if (u < v) {
+      nb += c;
+      jb = max(jb, (int)sh[4 + u]);
+    }
+    tot += c;
+  }
+  __syncthreads();  // sh is reused
+  return WideRow{nb + inc - pc, max(jb, dpp_or<0x138>(-1, mx)), tot};
+}
+
+// The listed rows' Golomb lengths (codeword walk, word_len), one workgroup per row and one word
+// per lane, so a row's serial codeword chain is one word long; a fixed grid strides over the
+// list, whose length k_scan_rows left in counter[2]. Rows with mixed k, and the row holding the
+// plane's first 1, are listed for k_emit_rest.
+constexpr uint32_t kWalkBlocks = 2048;
+template <bool PREDICT>
 __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
+  __shared__ uint32_t sh[8], sl[4], sk[4];
   const Geom& g = a.g;
-  const int lane = lane_id();
+  const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t w = 64 * v + lane;
   const uint32_t nlist = __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < nlist; i += kWalkBlocks * 4) {
+  for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
     const uint64_t id = a.walk_ids[i];
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     const uint32_t O = a.row_o[id];
-    uint64_t rr[WPL];
-    resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
-    StepState st{O + row, -1};
-    const uint32_t arow = row * (g.cols + 1);
-    uint32_t ll = 0, kor = 0;
-#pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      const uint32_t w = t * 64 + lane;
-      if (t * 64 >= (int)g.used) break;
-      uint32_t n;
-      int jp;
-      step_prefix(rr[t], w, st, n, jp);
-      ll += word_len(rr[t], w, n, jp, arow, w == g.used - 1, g.cols, kor);
-    }
+    uint64_t rr[1];
+    resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
+    const WideRow p = wide_prefix(rr[0], w, O + row, sh);
+    uint32_t kor = 0;
+    uint32_t ll = word_len(rr[0], w, p.n, p.jp, row * (g.cols + 1), w == g.used - 1, g.cols, kor);
     ll = wave_sum_u32(ll);
-    const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);
+    const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);  // some k != 0 / some k != 1
     if (lane == 0) {
-      a.glen[id] = ll | (!ks ? kK0Row : (!k1s ? kK1Row : 0));
-      // rows with mixed k, and the row holding the plane's first 1, go to the REST emit launch
-      if ((ks && k1s) || (O == 0 && st.n_carry > O + row)) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)id;
+      sl[v] = ll;
+      sk[v] = (ks ? 1u : 0u) | (k1s ? 2u : 0u);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t L = 0, kk = 0;
+      for (int u = 0; u < nw; ++u) {
+        L += sl[u];
+        kk |= sk[u];
+      }
+      a.glen[id] = L | (!(kk & 1u) ? kK0Row : (!(kk & 2u) ? kK1Row : 0));
+      if (kk == 3u || (O == 0 && p.ones > 0)) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)id;
+    }
+    __syncthreads();
   }
 }
 
 // The rows with every prefix known. EG rows, and Golomb rows whose codewords all have k = 0 (the
-// residual row and its '1'), are shifted copies formed in registers. Other Golomb rows: the row
-// image in LDS (encode_word), written with plain stores; rows whose image exceeds the LDS window
-// go to the k_rows_global list. The words shared with neighbouring rows go to the fragment tables
-// (k_fixup). One wave per row, 4-wave workgroups, no barriers after the byte tables are staged
-// (XCD-remapped block order: the waves of one XCD hold consecutive rows, the row above is an L2 hit).
+// residual row and its '1'), are shifted copies formed in registers; Golomb rows whose codewords
+// all have k = 1 go through an LDS row image (byte tables), written with plain stores. Rows whose
+// image exceeds the LDS window go to the k_rows_global list; rows with mixed k and the EG row of
+// the plane's first 1 are k_emit_rest's (their per-codeword path alone costs ~50 VGPRs, which
+// would halve this kernel's occupancy). The words shared with neighbouring rows go to the fragment
+// tables (k_fixup). One wave per row, persistent 4-wave workgroups, no barriers after the byte
+// tables are staged (XCD-remapped block order: the waves of one XCD hold consecutive rows, the
+// row above is an L2 hit).
 constexpr int kEmitWaves = 4;
-constexpr bool kEmitPrefetch = false;  // the next row's loads in flight (costs 16+ VGPRs: occupancy)
-template <int WPL, bool PREDICT, bool DO_G, bool DO_E, bool REST>
-__global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * (kGImg + kEImg)];
+constexpr bool kRestAux = true;  // k_emit_rest on the context's second stream (beside k_emit_known)
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+__global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * kGImg];
   __shared__ uint32_t s_lut[512];
   const Geom& g = a.g;
   const int lane = lane_id(), wave = threadIdx.x >> 6;
-  uint32_t* gimg = lds + wave * (kGImg + kEImg);
-  uint32_t* eimg = gimg + kGImg;
+  uint32_t* gimg = lds + wave * kGImg;
   if (DO_G)
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
   __syncthreads();  // the only workgroup barrier
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
-  // persistent waves: rows id, id + stride, ... with the next row's loads in flight
+  // persistent waves: rows id, id + stride, ...
   const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
-  uint64_t it = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
-  // REST: the rows the main launch listed (counter[3]); otherwise every row
-  const uint64_t nwork =
-      REST ? (uint64_t)__hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : nrows;
-  constexpr bool kPre = kEmitPrefetch && !REST;
-  if constexpr (REST) __builtin_amdgcn_s_setprio(3);  // latency-bound rows beside the main launch: issue first
-  uint64_t np_[WPL], nu_[WPL];
-  uint32_t nO = 0;
-  uint64_t nLf = 0;
-  if (kPre && it < nwork) {
-    const uint64_t id = it;
-    row_load<WPL, PREDICT>(a.planes, g, (uint32_t)(id / g.rows), (uint32_t)(id % g.rows), np_, nu_);
-    nO = a.row_o[id];
-    nLf = DO_G ? a.glen[id] : 0;
-  }
-  for (; it < nwork; it += stride) {
-  const uint64_t id = REST ? (uint64_t)a.rest_ids[it] : it;
-  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
-  uint64_t cp_[WPL], cu_[WPL];
-  uint32_t O;
-  uint64_t Lf;
-  if constexpr (kPre) {
-#pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      cp_[t] = np_[t];
-      cu_[t] = nu_[t];
-    }
-    O = nO;
-    Lf = nLf;
-    if (it + stride < nwork) {
-      const uint64_t id2 = it + stride;
-      row_load<WPL, PREDICT>(a.planes, g, (uint32_t)(id2 / g.rows), (uint32_t)(id2 % g.rows), np_, nu_);
-      nO = a.row_o[id2];
-      nLf = DO_G ? a.glen[id2] : 0;
-    }
-  } else {
+  for (uint64_t id = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave; id < nrows; id += stride) {
+    const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+    uint64_t cp_[WPL], cu_[WPL];
     row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
-    O = a.row_o[id];
-    Lf = DO_G ? a.glen[id] : 0;
-  }
-  const uint64_t L = Lf & kLenMask;
-  const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
-  bool gen = DO_G && L && !k0 && fits;  // Golomb row through the LDS image
+    const uint32_t O = a.row_o[id];
+    const uint64_t Lf = DO_G ? a.glen[id] : 0;
+    const uint64_t L = Lf & kLenMask;
+    const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
+    bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
 #ifdef BIC_STAMPS
-  if (a.dbg & 1) gen = false;
+    if (a.dbg & 1) gk1 = false;
 #endif
-  // the main launch leaves the rows with mixed k (per-codeword k) to REST: that path alone costs
-  // ~50 VGPRs, which would halve the main launch's occupancy
-  const bool mixed = gen && !k1;
-  const bool gk1 = !REST && gen && k1, gmix = REST && mixed;
-  if (gk1 || gmix) {  // zero the Golomb image
-    uint4* z = reinterpret_cast<uint4*>(gimg);
-    for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
-  }
-  uint64_t rr[WPL];
-  row_resid<WPL, PREDICT>(g, row, cp_, cu_, rr);
-  bool f_here = false;  // the plane's first 1 is in this row: EG inserts a '0' after it
-  int fcol = INT_MAX;
-  if (DO_E && O == 0) {
-    uint32_t ones = 0;
-#pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      ones += (uint32_t)__popcll(rr[t]);
-      if (rr[t] && fcol == INT_MAX) fcol = (int)((t * 64 + lane) * 64 + __builtin_clzll(rr[t]));
+    if (gk1) {  // zero the Golomb image
+      uint4* z = reinterpret_cast<uint4*>(gimg);
+      for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
     }
-    f_here = wave_sum_u32(ones) > 0;
-    fcol = wave_min(fcol);
-  }
-  if (REST && f_here) {  // EG image (~R, pad-masked, EOL '1') of the row holding the plane's first 1 (write_row inserts its '0')
+    uint64_t rr[WPL];
+    row_resid<WPL, PREDICT>(g, row, cp_, cu_, rr);
+    bool f_here = false;  // the plane's first 1 is in this row (k_emit_rest writes its EG row)
+    if (DO_E && O == 0) {
+      uint32_t ones = 0;
 #pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      const uint32_t w = t * 64 + lane;
-      if (w < g.used) {
-        const uint64_t v = ~rr[t] & (w == g.used - 1 ? g.trail : ~0ull);
-        eimg[2 * w] = (uint32_t)(v >> 32);
-        eimg[2 * w + 1] = (uint32_t)v;
-      }
+      for (int t = 0; t < WPL; ++t) ones += (uint32_t)__popcll(rr[t]);
+      f_here = wave_sum_u32(ones) > 0;
     }
-    if (lane < kPad + 1) eimg[2 * g.used + lane] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) eimg[g.cols >> 5] |= 0x80000000u >> (g.cols & 31);  // EOL '1'
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
 #ifdef BIC_STAMPS
-  if (!(a.dbg & 2))
+    if (!(a.dbg & 2))
 #endif
-  if constexpr (DO_E) {  // EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1
-    const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
-    const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
-    const uint64_t cap = a.slot_e * 64;
-    const uint64_t Ge = (uint64_t)plane * cap + Ge_rel;
-    if (REST) {
-      if (f_here && Ge_rel + Le <= cap) write_row(eimg, Le, Ge, (int64_t)fcol + 1, a.out_e, a.efrag + 2 * id);
-    } else {
+    if constexpr (DO_E) {  // EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1
+      const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
+      const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
+      const uint64_t cap = a.slot_e * 64;
+      const uint64_t Ge = (uint64_t)plane * cap + Ge_rel;
       if (Ge_rel + Le <= cap) {
         if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
-        if (lane == 0) { a.eboff[id] = Ge; a.elen[id] = Le; }
+        if (lane == 0) {
+          a.eboff[id] = Ge;
+          a.elen[id] = Le;
+        }
       } else if (lane == 0) {
         a.eboff[id] = Ge;
         a.elen[id] = 0;
@@ -1405,81 +1385,138 @@ __global__ __launch_bounds__(64 * kEmitWaves, 8) void k_emit_known(FusedArgs a) 
       }
       if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
     }
-  }
-  if constexpr (DO_G) {
-    if (!REST && k0 && L) {
+    if constexpr (DO_G) {
+      if (k0 && L) {
 #ifdef BIC_STAMPS
-      if (!(a.dbg & 4))
+        if (!(a.dbg & 4))
 #endif
-      eg_row_regs<WPL, false>(rr, g, a.gboff[id], L, a.out_g, a.gfrag + 2 * id);
-    } else if (gk1) {  // every codeword k = 1: branch-free byte-table words
-      int jpc = -1;
-      uint32_t loc = 0;
+        eg_row_regs<WPL, false>(rr, g, a.gboff[id], L, a.out_g, a.gfrag + 2 * id);
+      } else if (gk1) {  // every codeword k = 1: branch-free byte-table words
+        int jpc = -1;
+        uint32_t loc = 0;
 #pragma unroll
-      for (int t = 0; t < WPL; ++t) {
-        if (t * 64 >= (int)g.used) break;
-        const uint32_t w = t * 64 + lane;
-        const uint64_t x = rr[t];
-        const int jp = step_jp(x, w, jpc);
-        const bool eol = w == g.used - 1;
-        const LaneEnc e = encode_word_k1(x, w, jp, eol, g.cols, s_lut);
-        const uint32_t inc = wave_incl_sum_u32(e.len);
-        const uint32_t off = loc + inc - e.len;
-        loc += lane63_u32(inc);
-        if (!e.lng) {
-          place_small(gimg, off, e.head, 1);
-          place128(gimg, off + 1 + e.z, e.t0, e.t1, e.tlen);
-        } else {
-          LdsSink ls{gimg, 0, 0};
-          emit_word_k1(ls, off, x, w, jp, eol, g.cols);
-          ls.flush();
+        for (int t = 0; t < WPL; ++t) {
+          if (t * 64 >= (int)g.used) break;
+          const uint32_t w = t * 64 + lane;
+          const uint64_t x = rr[t];
+          const int jp = step_jp(x, w, jpc);
+          const bool eol = w == g.used - 1;
+          const LaneEnc e = encode_word_k1(x, w, jp, eol, g.cols, s_lut);
+          const uint32_t inc = wave_incl_sum_u32(e.len);
+          const uint32_t off = loc + inc - e.len;
+          loc += lane63_u32(inc);
+          if (!e.lng) {
+            place_small(gimg, off, e.head, 1);
+            place128(gimg, off + 1 + e.z, e.t0, e.t1, e.tlen);
+          } else {
+            LdsSink ls{gimg, 0, 0};
+            emit_word_k1(ls, off, x, w, jp, eol, g.cols);
+            ls.flush();
+          }
         }
+        if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
       }
-      if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
-    } else if (gmix) {
-      StepState st{O + row, -1};
-      const uint32_t arow = row * (g.cols + 1);
-      uint64_t loc = 0;
-#pragma unroll
-      for (int t = 0; t < WPL; ++t) {
-        if (t * 64 >= (int)g.used) break;
-        const uint32_t w = t * 64 + lane;
-        const uint64_t x = rr[t];
-        uint32_t n;
-        int jp;
-        step_prefix(x, w, st, n, jp);
-        const bool eol = w == g.used - 1;
-        const LaneEnc e = encode_word(x, w, n, jp, arow, eol, g.cols, ByteTables{s_lut, a.lut});
-        const uint32_t inc = wave_incl_sum_u32(e.len);
-        const uint64_t off = loc + inc - e.len;
-        loc += lane63_u32(inc);
-        if (!e.lng) {
-          place_small(gimg, (uint32_t)off, e.head, e.k0);
-          place128(gimg, (uint32_t)(off + e.k0 + e.z), e.t0, e.t1, e.tlen);
-        } else {
-          LdsSink ls{gimg, 0, 0};
-          emit_word(ls, (uint32_t)off, x, w, n, jp, arow, eol, g.cols);
-          ls.flush();
-        }
+      if (lane == 0) {
+        // drop the flags (k_fixup reads plain lengths); a first-1 row's only after k_emit_rest read them
+        if ((k0 || k1) && !f_here) a.glen[id] = L;
+        const bool slow = L && !k0 && !fits;
+        a.gslow[id] = slow ? O + row + 1 : 0;  // k_rows_global writes the row
+        if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
       }
-      if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
     }
-    // drop the flags (k_fixup reads plain lengths); a listed row's only after REST has read them
-    if (lane == 0 && (k0 || k1) && f_here == REST) a.glen[id] = L;
-    if (!REST && lane == 0) {
-      const bool slow = L && !k0 && !fits;
-      a.gslow[id] = slow ? O + row + 1 : 0;  // k_rows_global writes the row
-      if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
-    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
+    __builtin_amdgcn_wave_barrier();
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS images
-  __builtin_amdgcn_wave_barrier();
+}
+
+// The rows the prefix kernels listed (counter[3]): Golomb rows with mixed k (per-codeword k,
+// encode_word) and the EG row holding the plane's first 1 (with its inserted '0'). One workgroup
+// per row, one word per lane (wide_prefix), one LDS image per workgroup.
+template <bool PREDICT, bool DO_G, bool DO_E>
+__global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t gimg[kGImg];
+  __shared__ __attribute__((aligned(16))) uint32_t eimg[kEImg];
+  __shared__ uint32_t s_lut[512];
+  __shared__ uint32_t sh[8];
+  __shared__ int sf[4];
+  const Geom& g = a.g;
+  const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t w = 64 * v + lane;
+  if (DO_G)
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+  __syncthreads();
+  constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+  const uint32_t nlist = __hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
+    const uint64_t id = a.rest_ids[i];
+    const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+    const uint32_t O = a.row_o[id];
+    const uint64_t Lf = DO_G ? a.glen[id] : 0;
+    const uint64_t L = Lf & kLenMask;
+    const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0;
+    const bool gmix = DO_G && L && !k0 && !k1 && L <= kCapBits;
+    uint64_t rr[1];
+    resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
+    const uint64_t x = rr[0];
+    const WideRow p = wide_prefix(x, w, O + row, sh);
+    const bool f_here = DO_E && O == 0 && p.ones > 0;
+    if (gmix) {
+      uint4* z = reinterpret_cast<uint4*>(gimg);
+      for (uint32_t j = threadIdx.x; j < kGImg / 4; j += blockDim.x) z[j] = make_uint4(0, 0, 0, 0);
+    }
+    if (f_here) {  // EG image (~R, pad-masked, EOL '1'); write_row inserts the '0' after the first 1
+      const int fc = wave_min(x ? (int)(w * 64 + __builtin_clzll(x)) : INT_MAX);
+      if (lane == 0) sf[v] = fc;
+      if (w < g.used) {
+        const uint64_t e = ~x & (w == g.used - 1 ? g.trail : ~0ull);
+        eimg[2 * w] = (uint32_t)(e >> 32);
+        eimg[2 * w + 1] = (uint32_t)e;
+      }
+      if (threadIdx.x < kPad + 1) eimg[2 * g.used + threadIdx.x] = 0;
+    }
+    __syncthreads();
+    if (f_here) {
+      if (threadIdx.x == 0) eimg[g.cols >> 5] |= 0x80000000u >> (g.cols & 31);  // EOL '1'
+      __syncthreads();
+      int fcol = INT_MAX;
+      for (int u = 0; u < nw; ++u) fcol = min(fcol, sf[u]);
+      const uint64_t Le = (uint64_t)g.cols + 2;
+      const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1);
+      const uint64_t cap = a.slot_e * 64;
+      if (Ge_rel + Le <= cap)
+        write_row(eimg, Le, (uint64_t)plane * cap + Ge_rel, (int64_t)fcol + 1, a.out_e, a.efrag + 2 * id,
+                  threadIdx.x, blockDim.x);
+    }
+    if (gmix) {
+      const uint32_t arow = row * (g.cols + 1);
+      const bool eol = w == g.used - 1;
+      const LaneEnc e = encode_word(x, w, p.n, p.jp, arow, eol, g.cols, ByteTables{s_lut, a.lut});
+      const uint32_t inc = wave_incl_sum_u32(e.len);
+      if (lane == 63) sh[v] = inc;
+      __syncthreads();
+      uint32_t wb = 0, tot = 0;
+      for (int u = 0; u < nw; ++u) {
+        if (u < v) wb += sh[u];
+        tot += sh[u];
+      }
+      const uint32_t off = wb + inc - e.len;
+      if (!e.lng) {
+        place_small(gimg, off, e.head, e.k0);
+        place128(gimg, off + e.k0 + e.z, e.t0, e.t1, e.tlen);
+      } else {
+        LdsSink ls{gimg, 0, 0};
+        emit_word(ls, off, x, w, p.n, p.jp, arow, eol, g.cols);
+        ls.flush();
+      }
+      __syncthreads();
+      if (threadIdx.x == 0 && tot != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id, threadIdx.x, blockDim.x);
+    }
+    if (DO_G && threadIdx.x == 0 && (k0 || k1) && f_here) a.glen[id] = L;  // drop the flags (k_fixup)
+    __syncthreads();  // the images and sh are reused by the next row
   }
 }
 
@@ -1597,10 +1634,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       if (dg) k_scan_rows<true, true><<<sgrid, 1024, 0, s>>>(a);
       else k_scan_rows<true, false><<<sgrid, 1024, 0, s>>>(a);
       if (dg) {
-#define BIC_WALK(W) \
-  if (predict) k_row_walk<W, true><<<kWalkBlocks, 256, 0, s>>>(a); else k_row_walk<W, false><<<kWalkBlocks, 256, 0, s>>>(a)
-        if (wpl == 1) { BIC_WALK(1); } else if (wpl == 2) { BIC_WALK(2); } else { BIC_WALK(4); }
-#undef BIC_WALK
+        const uint32_t nwv = (g.used + 63) / 64;  // one workgroup per row, one word per lane
+        if (predict) k_row_walk<true><<<kWalkBlocks, 64 * nwv, 0, s>>>(a);
+        else k_row_walk<false><<<kWalkBlocks, 64 * nwv, 0, s>>>(a);
         k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);
       }
       return;
@@ -1615,17 +1651,18 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     }
     // one resident wave set: 4 workgroups per CU (the main launch holds <= 128 VGPRs: 4 waves per SIMD)
     const uint32_t egrid2 = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 4);
-    // REST (listed rows, latency bound) first, on the aux stream when there is one: it then runs
-    // beside the main launch, which skips the listed rows' REST parts
-    const uint32_t rgrid = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 2);
+    // k_emit_rest (listed rows, latency bound: few workgroups) first, on the aux stream when there
+    // is one, so that it can overlap the main launch, which skips the listed rows' parts
+    const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
+    const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 4);
     hipStream_t rs = s;
-    if (fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
+    if (kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
         hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
       rs = fs.aux;
 #define BIC_EMIT1(W, P, DG, DE)                                                                        \
   {                                                                                                  \
-    k_emit_known<W, P, DG, DE, true><<<rgrid, 64 * kEmitWaves, 0, rs>>>(a);                          \
-    k_emit_known<W, P, DG, DE, false><<<egrid2, 64 * kEmitWaves, 0, s>>>(a);                         \
+    k_emit_rest<P, DG, DE><<<rgrid, 64 * nwv, 0, rs>>>(a);                                           \
+    k_emit_known<W, P, DG, DE><<<egrid2, 64 * kEmitWaves, 0, s>>>(a);                                \
   }
 #define BIC_EMIT(W, P)                                                                                \
   if (dg && de) BIC_EMIT1(W, P, true, true) else if (dg) BIC_EMIT1(W, P, true, false) else BIC_EMIT1(W, P, false, true)
