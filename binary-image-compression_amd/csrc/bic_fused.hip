@@ -1189,9 +1189,18 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
   const uint32_t lim = b * kScanChunk;
   if constexpr (ONES) {  // the records of those rows are one contiguous range
     const uint32_t* so = a.sones + base * a.ns;
-    const uint64_t flat = (uint64_t)lim * a.ns;
+    const uint64_t flat = (uint64_t)lim * a.ns;  // a multiple of 4 (lim is one of kScanChunk)
+    if ((base * a.ns) % 4 == 0) {  // 16-byte loads
+      const uint4* s4 = reinterpret_cast<const uint4*>(so);
 #pragma unroll 8
-    for (uint64_t i = threadIdx.x; i < flat; i += 1024) before += so[i];
+      for (uint64_t i = threadIdx.x; i < flat / 4; i += 1024) {
+        const uint4 q = s4[i];
+        before += (uint64_t)q.x + q.y + q.z + q.w;
+      }
+    } else {
+#pragma unroll 8
+      for (uint64_t i = threadIdx.x; i < flat; i += 1024) before += so[i];
+    }
   } else {
 #pragma unroll 8
     for (uint32_t r = threadIdx.x; r < lim; r += 1024) before += val(r);
@@ -1201,14 +1210,21 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
   (void)block_excl_scan<uint64_t>(before, tmp, btot);
   pre += btot;
   if constexpr (ONES) {
+    bool walks[kScanPer];  // classify every row of the thread first: their record loads overlap
+#pragma unroll
+    for (uint32_t i = 0; i < kScanPer; ++i) {
+      const uint32_t r = r0 + i;
+      const uint64_t p = pre + (i ? v[0] : 0) + (i > 1 ? v[1] : 0);
+      static_assert(kScanPer <= 2, "prefix above covers two rows");
+      walks[i] = CLASSIFY && r < g.rows && row_class(a, base + r, r, (uint32_t)p);
+    }
 #pragma unroll
     for (uint32_t i = 0; i < kScanPer; ++i) {
       const uint32_t r = r0 + i;
       const bool in = r < g.rows;
       if (in) a.row_o[base + r] = (uint32_t)pre;
-      bool walk = false;
+      const bool walk = walks[i];
       if constexpr (CLASSIFY) {
-        walk = in && row_class(a, base + r, r, (uint32_t)pre);
         const uint64_t m = __ballot(walk);  // wave-aggregated append to the list of rows to walk
         if (m) {
           uint32_t wb = 0;

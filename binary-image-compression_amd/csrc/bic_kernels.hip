@@ -304,8 +304,8 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 // 64 s + l of strip s: four 16-byte loads give its 64 pixels, K1's 8x8 transposes one word per
 // plane; the plane words are stored and the med residual is formed from the row above (plane
 // words kept in registers) and the pixel left of the word (lane l - 1's last; lane 0 of strip s > 0
-// loads the byte before the strip). One k statistics record per (plane, row, strip) (lanek_store;
-// row_kstats combines a row's strips). The next row's loads are in flight while a row is used.
+// loads the byte before the strip). One k statistics record per (plane, row, strip) (all planes'
+// records in one transposed pass, strip_records; row_kstats combines a row's strips). The next row's loads are in flight while a row is used.
 // The gray rows must hold used * 64 readable bytes (pitch >= used * 64, 16-byte aligned;
 // gray_rows_supported).
 constexpr int kGrayRows = 8;
@@ -332,7 +332,9 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
                                                         uint32_t ns, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
                                                         uint32_t* __restrict__ kpos) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
   const int lane = lane_id();
+  uint32_t* tw = tab[threadIdx.x >> 6];
   const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
   const uint32_t s = (uint32_t)(gw % ns);  // the strips of one row block are neighbouring waves
   const uint32_t r0 = (uint32_t)(gw / ns) * kGrayRows;
@@ -387,11 +389,13 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
         if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
         up[b] = pw[b];
       }
-      LaneK k;
-      lanek_word(k, R, (int32_t)(w * 64));
-      const uint64_t id = ((uint64_t)b * g.rows + row) * ns + s;
-      lanek_store(k, krec + id, kpos + id, sones + id);
+      strip_word_put(tw, b, R, (int32_t)(w * 64));
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    strip_records(tw, np, krec, kpos, sones, (uint64_t)row * ns + s, (uint64_t)g.rows * ns);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row rewrites the table
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
     clb = nlb;

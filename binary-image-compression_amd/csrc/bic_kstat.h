@@ -104,25 +104,123 @@ __device__ __forceinline__ void lanek_store(const LaneK& k, int4* rec, uint32_t*
   }
 }
 
-// A row's statistics from its ns strip records (the strips' local 1 counts rebased).
+// The strip records of up to 8 planes at once, for waves whose lanes hold ONE residual word per
+// plane (k_gray_strips): strip_word_put leaves lane l's (m | chg << 8, pf | pl << 16) of plane b
+// in the wave's LDS table t (1024 words); after a wave fence, strip_records lets lane
+// L = 8 p + j combine lanes 8j..8j+7 of plane p in column order, then the eight parts of a plane
+// are combined with 8-lane DPP scans (ones before the part, last 1 before it) and reductions;
+// lane 8p stores plane p's record (the same record lanek_word + lanek_store make). One transposed
+// pass instead of eight wave-wide scan-and-reduce chains.
+__device__ __forceinline__ void strip_word_put(uint32_t* t, int b, uint64_t x, int32_t c0) {
+  const int lane = lane_id();
+  uint32_t m = 0, c = 0;
+  if (x) {
+    m = (uint32_t)__popcll(x) | (parity_changes(x) << 8);
+    c = (uint32_t)(c0 + __builtin_clzll(x)) | ((uint32_t)(c0 + 63 - __builtin_ctzll(x)) << 16);
+  }
+  t[b * 64 + lane] = m;
+  t[512 + b * 64 + lane] = c;
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_same(int v) {  // every source lane valid (quad perms, mirrors)
+  return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ void strip_records(const uint32_t* t, int np, int4* krec, uint32_t* kpos, uint32_t* sones,
+                                              uint64_t id0, uint64_t pstride) {
+  const int L = lane_id(), p = L >> 3, j = L & 7;
+  const uint4 a0 = *reinterpret_cast<const uint4*>(t + p * 64 + 8 * j);
+  const uint4 a1 = *reinterpret_cast<const uint4*>(t + p * 64 + 8 * j + 4);
+  const uint4 c0 = *reinterpret_cast<const uint4*>(t + 512 + p * 64 + 8 * j);
+  const uint4 c1 = *reinterpret_cast<const uint4*>(t + 512 + p * 64 + 8 * j + 4);
+  const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const uint32_t cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  uint32_t ones = 0, chg = 0;
+  int32_t first = -1, last = -1, q0 = -kNoOnes, qh = -kNoOnes, ql = kNoOnes;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int32_t m = (int32_t)(av[i] & 0xffu);
+    if (m) {
+      const int32_t pf = (int32_t)(cv[i] & 0xffffu), pl = (int32_t)(cv[i] >> 16), o = (int32_t)ones;
+      chg += (av[i] >> 8) + (last >= 0 ? (uint32_t)((last ^ pf) & 1) : 0u);
+      q0 = max(q0, pl - m - 2 * o);
+      qh = max(qh, pl - m - 1 - 3 * o);
+      ql = min(ql, pf - m - 2 * o);
+      if (first < 0) first = pf;
+      last = pl;
+      ones += (uint32_t)m;
+    }
+  }
+  // inclusive 8-lane scans (row_shr inside the 16-lane row, masked to the part's group)
+  uint32_t inc = ones;
+  int32_t lmax = last;
+#pragma unroll
+  for (int d = 1; d < 8; d <<= 1) {
+    const uint32_t o = d == 1 ? (uint32_t)dpp_or<0x111>(0, (int)inc) : d == 2 ? (uint32_t)dpp_or<0x112>(0, (int)inc)
+                                                                             : (uint32_t)dpp_or<0x114>(0, (int)inc);
+    const int32_t lm = d == 1 ? dpp_or<0x111>(-1, lmax) : d == 2 ? dpp_or<0x112>(-1, lmax) : dpp_or<0x114>(-1, lmax);
+    if (j >= d) {
+      inc += o;
+      lmax = max(lmax, lm);
+    }
+  }
+  const int32_t lprev = dpp_or<0x111>(-1, lmax);  // DPP outside any branch: every source lane active
+  const int32_t before = j ? lprev : -1;           // the last 1 of the parts before
+  const int32_t B = (int32_t)(inc - ones);
+  if (ones) {
+    if (before >= 0) chg += (uint32_t)((before ^ first) & 1);
+    q0 -= 2 * B;
+    qh -= 3 * B;
+    ql -= 2 * B;
+  }
+  int32_t f = ones ? first : INT_MAX;
+  uint32_t tot = ones;
+  // 8-lane reductions: quad swaps, then the half-row mirror pairs the group's two quads
+#define BIC_RED8(CTRL)                          \
+  q0 = max(q0, dpp_same<CTRL>(q0));             \
+  qh = max(qh, dpp_same<CTRL>(qh));             \
+  ql = min(ql, dpp_same<CTRL>(ql));             \
+  f = min(f, dpp_same<CTRL>(f));                \
+  last = max(last, dpp_same<CTRL>(last));       \
+  chg += (uint32_t)dpp_same<CTRL>((int)chg);    \
+  tot += (uint32_t)dpp_same<CTRL>((int)tot);
+  BIC_RED8(0xB1)
+  BIC_RED8(0x4E)
+  BIC_RED8(0x141)
+#undef BIC_RED8
+  if (j == 0 && p < np) {
+    const uint64_t id = id0 + (uint64_t)p * pstride;
+    krec[id] = make_int4(q0, qh, ql, (int32_t)(tot | (chg << 16)));
+    kpos[id] = ((uint32_t)(f == INT_MAX ? -1 : f) & 0xffffu) | ((uint32_t)last << 16);
+    sones[id] = tot;
+  }
+}
+
+// A row's statistics from its ns (<= kMaxStrips) strip records (the strips' local 1 counts
+// rebased). Every record is loaded before any is used.
 struct RowK {
   int32_t q0, qh, ql;
   uint32_t ones, chg;
 };
 __device__ __forceinline__ RowK row_kstats(const int4* rec, const uint32_t* pos, uint32_t ns, uint32_t cols) {
+  int4 v[kMaxStrips];
+  uint32_t pp[kMaxStrips];
+#pragma unroll
+  for (uint32_t s = 0; s < kMaxStrips; ++s) {
+    v[s] = s < ns ? rec[s] : make_int4(0, 0, 0, 0);
+    pp[s] = s < ns ? pos[s] : 0u;
+  }
   RowK r{0, 0, 0, 0, 0};
   int32_t last = -1;
-  for (uint32_t s = 0; s < ns; ++s) {
-    const int4 v = rec[s];
-    const uint32_t o = (uint32_t)v.w & 0xffffu;
+#pragma unroll
+  for (uint32_t s = 0; s < kMaxStrips; ++s) {
+    const uint32_t o = (uint32_t)v[s].w & 0xffffu;
     if (!o) continue;
-    const uint32_t p = pos[s];
-    r.q0 = max(r.q0, v.x - 2 * (int32_t)r.ones);
-    r.qh = max(r.qh, v.y - 3 * (int32_t)r.ones);
-    r.ql = min(r.ql, v.z - 2 * (int32_t)r.ones);
-    r.chg += ((uint32_t)v.w >> 16) + (uint32_t)((last ^ (int32_t)(int16_t)(p & 0xffffu)) & 1);
+    r.q0 = max(r.q0, v[s].x - 2 * (int32_t)r.ones);
+    r.qh = max(r.qh, v[s].y - 3 * (int32_t)r.ones);
+    r.ql = min(r.ql, v[s].z - 2 * (int32_t)r.ones);
+    r.chg += ((uint32_t)v[s].w >> 16) + (uint32_t)((last ^ (int32_t)(int16_t)(pp[s] & 0xffffu)) & 1);
     r.ones += o;
-    last = (int16_t)(p >> 16);
+    last = (int16_t)(pp[s] >> 16);
   }
   r.chg += (uint32_t)((last ^ (int32_t)cols) & 1);  // the end-of-row sample at column cols
   return r;

@@ -55,9 +55,11 @@ def main():
                              "hbm_bytes_per_launch": int(hbm) if hbm is not None else None}
     # bench.py times launch sequences (bic_prof_* names); their HBM bytes per launch are the sums
     # over the kernels each sequence runs, per launch of its main kernel
-    timers = {"encode_rows_golomb_eg": ["k_encode_rows", "k_len_rows", "k_emit_rows"],
-              "encode_rows_golomb": ["k_encode_rows", "k_len_rows", "k_emit_rows"],
-              "encode_rows_eg": ["k_encode_rows", "k_len_rows", "k_emit_rows"],
+    # (the first kernel of each list runs once per launch of the sequence: it gives the count)
+    rows = ["k_emit_known", "k_emit_rest", "k_encode_rows", "k_len_rows", "k_emit_rows"]
+    timers = {"encode_rows_golomb_eg": rows, "encode_rows_golomb": rows, "encode_rows_eg": rows,
+              "encode_prefix": ["k_row_walk", "k_scan_rows", "k_med_kstat"],
+              "bitplanes_count": ["k_gray_strips"],
               "encode_finish": ["k_rows_global", "k_fixup"],
               "bitplanes_u8": ["k_bitplanes_u8"], "med_count": ["k_med_rows", "k_count", "k_plane_weight"],
               "tiles": ["k_tiles_aligned", "k_tiles"], "golomb_samples": ["k_samp_scan", "k_samp_emit"],
