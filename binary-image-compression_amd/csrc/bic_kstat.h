@@ -118,8 +118,12 @@ __device__ __forceinline__ void strip_word_put(uint32_t* t, int b, uint64_t x, i
     m = (uint32_t)__popcll(x) | (parity_changes(x) << 8);
     c = (uint32_t)(c0 + __builtin_clzll(x)) | ((uint32_t)(c0 + 63 - __builtin_ctzll(x)) << 16);
   }
-  t[b * 64 + lane] = m;
-  t[512 + b * 64 + lane] = c;
+  // lane l's value is value i = l & 7 of part 8b + (l >> 3): stored at word (i >> 2) * 256 +
+  // 4 * part + (i & 3), so that strip_records' 16-byte reads (lane L: words 4L..4L+3 of each
+  // quarter) are bank-conflict free
+  const uint32_t idx = ((uint32_t)(lane & 7) >> 2) * 256 + 32 * b + 4 * (lane >> 3) + (lane & 3);
+  t[idx] = m;
+  t[512 + idx] = c;
 }
 template <int CTRL>
 __device__ __forceinline__ int dpp_same(int v) {  // every source lane valid (quad perms, mirrors)
@@ -128,10 +132,10 @@ __device__ __forceinline__ int dpp_same(int v) {  // every source lane valid (qu
 __device__ __forceinline__ void strip_records(const uint32_t* t, int np, int4* krec, uint32_t* kpos, uint32_t* sones,
                                               uint64_t id0, uint64_t pstride) {
   const int L = lane_id(), p = L >> 3, j = L & 7;
-  const uint4 a0 = *reinterpret_cast<const uint4*>(t + p * 64 + 8 * j);
-  const uint4 a1 = *reinterpret_cast<const uint4*>(t + p * 64 + 8 * j + 4);
-  const uint4 c0 = *reinterpret_cast<const uint4*>(t + 512 + p * 64 + 8 * j);
-  const uint4 c1 = *reinterpret_cast<const uint4*>(t + 512 + p * 64 + 8 * j + 4);
+  const uint4 a0 = *reinterpret_cast<const uint4*>(t + 4 * L);
+  const uint4 a1 = *reinterpret_cast<const uint4*>(t + 256 + 4 * L);
+  const uint4 c0 = *reinterpret_cast<const uint4*>(t + 512 + 4 * L);
+  const uint4 c1 = *reinterpret_cast<const uint4*>(t + 768 + 4 * L);
   const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
   const uint32_t cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
   uint32_t ones = 0, chg = 0;
