@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=16384, help="rows per plane in the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="repeat the CPU baseline sample until this much CPU time has been measured")
-    ap.add_argument("--encoder", default="staged", choices=["staged", "single-kernel", "two-pass", "multipass"],
+    ap.add_argument("--encoder", default="auto", choices=["auto", "staged", "single-kernel", "two-pass", "multipass"],
                     help="row encoder for rows <= 16384 columns (bic_ctx_set_option)")
     ap.add_argument("--separate", action="store_true",
                     help="c3: bic_bitplanes_u8 then bic_encode_planes2 instead of the one-call bic_encode_gray")

@@ -46,6 +46,7 @@ struct bic_ctx {
   bool force_multipass = false;
   bool two_pass = false;       // BIC_OPT_TWO_PASS: the two-pass row encoder instead of the staged one
   bool single_kernel = false;  // BIC_OPT_SINGLE_KERNEL: the single kernel with decoupled look-backs
+  bool force_staged = false;   // BIC_OPT_STAGED: the staged encoder whatever the batch size
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -124,6 +125,14 @@ void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
   fs.aux = ctx->aux;
   fs.ev_fork = ctx->ev_fork;
   fs.ev_join = ctx->ev_join;
+}
+
+// The staged encoder's ~8 dependent launches cost more than the single kernel's look-back waits
+// on small batches (C2, one 4096^2 plane: 92 vs 25 us); from kStagedMinRows rows (all planes) on
+// it is the faster one (C3: 131,072 rows). BIC_OPT_STAGED forces it.
+constexpr uint64_t kStagedMinRows = 32768;
+bool staged_pays(const bic_ctx* ctx, const bic::Geom& g) {
+  return ctx->force_staged || (uint64_t)g.rows * g.nplanes >= kStagedMinRows;
 }
 
 bool geom_ok(size_t rows, size_t cols, size_t wpr) {
@@ -308,6 +317,10 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
     ctx->single_kernel = value != 0;
     return BIC_OK;
   }
+  if (option == BIC_OPT_STAGED) {
+    ctx->force_staged = value != 0;
+    return BIC_OK;
+  }
   return BIC_EINVAL;
 }
 
@@ -376,7 +389,8 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
     bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
     set_aux(ctx, fs);
     const int mode = ctx->two_pass ? bic::kEncTwoPass
-                     : (ctx->single_kernel || !bic::med_rows_supported(g, planes, nullptr)) ? bic::kEncSingle
+                     : (ctx->single_kernel || !staged_pays(ctx, g) || !bic::med_rows_supported(g, planes, nullptr))
+                         ? bic::kEncSingle
                                                                                             : bic::kEncStaged;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
@@ -427,6 +441,7 @@ int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows
   if (rows && (!gray || !planes)) return BIC_EINVAL;
   const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
   const bool fuse = rows && bic::fused_supported(g) && !ctx->force_multipass && !ctx->two_pass && !ctx->single_kernel &&
+                    staged_pays(ctx, g) &&
                     bic::med_rows_supported(g, planes, nullptr) && bic::gray_rows_supported(g, gray, pitch, planes);
   if (!fuse) {  // the same result through the two separate calls
     if ((rc = bic_bitplanes_u8(ctx, gray, pitch, rows, cols, nplanes, planes, wpr))) return rc;

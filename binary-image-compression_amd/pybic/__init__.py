@@ -272,10 +272,12 @@ class Context:
         return planes, ((og, bg) if golomb else None), ((oe, be) if eg else None)
 
     def set_encoder(self, name):
-        """row encoder for rows <= 16384 columns: "staged" (default), "single-kernel", "two-pass",
-        "multipass" (bic_ctx_set_option)"""
-        assert name in ("staged", "single-kernel", "two-pass", "multipass"), name
+        """row encoder for rows <= 16384 columns: "auto" (default: staged from 32768 rows on, the
+        single kernel below), "staged" (forced), "single-kernel", "two-pass", "multipass"
+        (bic_ctx_set_option)"""
+        assert name in ("auto", "staged", "single-kernel", "two-pass", "multipass"), name
         self.set_multipass(name == "multipass")
+        self._chk(self.lib.bic_ctx_set_option(self.h, 4, int(name == "staged")), "bic_ctx_set_option")
         self._chk(self.lib.bic_ctx_set_option(self.h, 2, int(name == "two-pass")), "bic_ctx_set_option")
         self._chk(self.lib.bic_ctx_set_option(self.h, 3, int(name == "single-kernel")), "bic_ctx_set_option")
 

@@ -72,12 +72,14 @@ int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
 #define BIC_OPT_MULTIPASS 1
 /* Row encoders (same output; the alternatives are kept as cross-checks and for comparison).
  * Default: the staged encoder -- per-row sample counts, per-plane scans and per-row Golomb
- * lengths first, then every row written independently (planes 16-byte aligned, even row pitch;
- * otherwise the single kernel is used). BIC_OPT_TWO_PASS = 1: lengths and offsets found by
- * decoupled look-backs, then every row written. BIC_OPT_SINGLE_KERNEL = 1: one kernel, rows staged
- * in LDS until decoupled look-backs give their offsets. */
+ * lengths first, then every row written independently -- for batches of >= 32768 rows (all
+ * planes; planes 16-byte aligned, even row pitch), the single kernel below that (fewer launches).
+ * BIC_OPT_STAGED = 1: the staged encoder for every batch size. BIC_OPT_TWO_PASS = 1: lengths and
+ * offsets found by decoupled look-backs, then every row written. BIC_OPT_SINGLE_KERNEL = 1: one
+ * kernel, rows staged in LDS until decoupled look-backs give their offsets. */
 #define BIC_OPT_TWO_PASS 2
 #define BIC_OPT_SINGLE_KERNEL 3
+#define BIC_OPT_STAGED 4
 int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
 
 /* ---- a2: bitplane extraction (bitplane_tool.cpp:24-30) -----------------------------------

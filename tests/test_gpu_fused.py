@@ -33,7 +33,7 @@ def check(ctx, oracle, P, cols, pred, both=True):
 def encoder(request, ctx):
     ctx.set_encoder(request.param)
     yield request.param
-    ctx.set_encoder("staged")
+    ctx.set_encoder("auto")
 
 
 @pytest.mark.parametrize("rows,cols", [(1, 1), (3, 64), (7, 65), (64, 100), (50, 1000), (40, 4096), (20, 8191),
@@ -67,7 +67,7 @@ def test_fused_vs_multipass(ctx, oracle):
         ctx.sync()
         res[mode] = [(as_u64(bg), [stream_bytes(og[k], as_u64(bg)[k]) for k in range(3)]),
                      (as_u64(be), [stream_bytes(oe[k], as_u64(be)[k]) for k in range(3)])]
-    ctx.set_encoder("staged")
+    ctx.set_encoder("auto")
     for mode in modes[1:]:
         for c in range(2):
             assert np.array_equal(res["staged"][c][0], res[mode][c][0])
@@ -155,13 +155,22 @@ def _gray(oracle, seed, rows, cols, kind):
     return ((i * 3 + j // 5 + noise) % 256).astype(np.uint8)
 
 
+@pytest.fixture
+def staged(ctx):
+    """the staged encoder (and bic_encode_gray's fused count pass) at test sizes, which the
+    automatic choice would give to the single kernel"""
+    ctx.set_encoder("staged")
+    yield
+    ctx.set_encoder("auto")
+
+
 @pytest.mark.parametrize("rows,cols,pitch,nplanes,kind", [
     (1, 64, 64, 8, "uniform"), (17, 100, 128, 8, "uniform"), (33, 4096, 4096, 8, "uniform"),
     (40, 5000, 5120, 3, "smooth"), (24, 16384, 16384, 8, "uniform"), (70, 16384, 16384, 8, "smooth"),
     (9, 300, 300, 8, "uniform"),  # pitch < used * 64: the two-call path
     (12, 200, 208, 5, "smooth"),  # pitch < used * 64 (256): the two-call path
 ])
-def test_encode_gray(ctx, oracle, rows, cols, pitch, nplanes, kind):
+def test_encode_gray(ctx, oracle, staged, rows, cols, pitch, nplanes, kind):
     """bic_encode_gray == bitplane_tool's planes (oracle) and each plane's Golomb and EG streams"""
     t = ctx.torch
     img = np.zeros((rows, pitch), np.uint8)
@@ -181,7 +190,7 @@ def test_encode_gray(ctx, oracle, rows, cols, pitch, nplanes, kind):
                 assert stream_bytes(out[k], nb) == est.tobytes(), (pred, k, coder)
 
 
-def test_encode_gray_matches_two_calls(ctx, oracle):
+def test_encode_gray_matches_two_calls(ctx, oracle, staged):
     rows, cols = 300, 16384
     img = _gray(oracle, 5, rows, cols, "uniform")
     g = ctx.torch.from_numpy(img).to(ctx.dev)
