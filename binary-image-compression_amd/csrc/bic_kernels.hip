@@ -311,6 +311,16 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 constexpr int kGrayRows = 8;
 uint32_t gray_strips(const Geom& g) { return (g.used + 63) / 64; }
 
+// out[b] = bytes b of w0..w3, w0's in the most significant byte (a 4x4 byte transpose)
+__device__ __forceinline__ void perm_t4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t (&out)[4]) {
+  const uint32_t a01 = __builtin_amdgcn_perm(w0, w1, 0x04000501u), b01 = __builtin_amdgcn_perm(w0, w1, 0x06020703u);
+  const uint32_t a23 = __builtin_amdgcn_perm(w2, w3, 0x04000501u), b23 = __builtin_amdgcn_perm(w2, w3, 0x06020703u);
+  out[0] = __builtin_amdgcn_perm(a01, a23, 0x07060302u);
+  out[1] = __builtin_amdgcn_perm(a01, a23, 0x05040100u);
+  out[2] = __builtin_amdgcn_perm(b01, b23, 0x07060302u);
+  out[3] = __builtin_amdgcn_perm(b01, b23, 0x05040100u);
+}
+
 __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&pw)[8], uint64_t mask) {
   uint64_t T[8];
 #pragma unroll
@@ -318,12 +328,16 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
     T[2 * i] = transpose8x8(bswap64((uint64_t)v[i].x | ((uint64_t)v[i].y << 32)));
     T[2 * i + 1] = transpose8x8(bswap64((uint64_t)v[i].z | ((uint64_t)v[i].w << 32)));
   }
+  // byte b of T[g8] -> byte 7 - g8 of pw[b]: four 4x4 byte transposes, 8 v_perm_b32 each
+  uint32_t XL[4], YL[4], XH[4], YH[4];
+  perm_t4((uint32_t)T[0], (uint32_t)T[1], (uint32_t)T[2], (uint32_t)T[3], XL);
+  perm_t4((uint32_t)T[4], (uint32_t)T[5], (uint32_t)T[6], (uint32_t)T[7], YL);
+  perm_t4((uint32_t)(T[0] >> 32), (uint32_t)(T[1] >> 32), (uint32_t)(T[2] >> 32), (uint32_t)(T[3] >> 32), XH);
+  perm_t4((uint32_t)(T[4] >> 32), (uint32_t)(T[5] >> 32), (uint32_t)(T[6] >> 32), (uint32_t)(T[7] >> 32), YH);
 #pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    uint64_t x = 0;
-#pragma unroll
-    for (int g8 = 0; g8 < 8; ++g8) x |= ((T[g8] >> (8 * b)) & 0xffull) << (56 - 8 * g8);
-    pw[b] = x & mask;
+  for (int b = 0; b < 4; ++b) {
+    pw[b] = (((uint64_t)XL[b] << 32) | YL[b]) & mask;
+    pw[4 + b] = (((uint64_t)XH[b] << 32) | YH[b]) & mask;
   }
 }
 
