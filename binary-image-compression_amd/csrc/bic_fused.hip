@@ -1293,7 +1293,7 @@ __device__ __forceinline__ WideRow wide_prefix(uint64_t x, uint32_t w, uint32_t 
 // per lane, so a row's serial codeword chain is one word long; a fixed grid strides over the
 // list, whose length k_scan_rows left in counter[2]. Rows with mixed k, and the row holding the
 // plane's first 1, are listed for k_emit_rest.
-constexpr uint32_t kWalkBlocks = 2048;
+constexpr uint32_t kWalkWaves = 8192;  // the walk grid in waves (32 per CU), whatever the row width
 template <bool PREDICT>
 __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
   __shared__ uint32_t sh[8], sl[4], sk[4];
@@ -1651,8 +1651,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       else k_scan_rows<true, false><<<sgrid, 1024, 0, s>>>(a);
       if (dg) {
         const uint32_t nwv = (g.used + 63) / 64;  // one workgroup per row, one word per lane
-        if (predict) k_row_walk<true><<<kWalkBlocks, 64 * nwv, 0, s>>>(a);
-        else k_row_walk<false><<<kWalkBlocks, 64 * nwv, 0, s>>>(a);
+        if (predict) k_row_walk<true><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
+        else k_row_walk<false><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
         k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);
       }
       return;
@@ -1670,7 +1670,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     // k_emit_rest (listed rows, latency bound: few workgroups) first, on the aux stream when there
     // is one, so that it can overlap the main launch, which skips the listed rows' parts
     const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
-    const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 4);
+    const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 16 / nwv);  // 16 waves per CU
     hipStream_t rs = s;
     if (kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
         hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
