@@ -460,7 +460,7 @@ int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows
   };
   stage(bic::kFusedPrep);
   timed(ctx, "bitplanes_count", [&] {
-    bic::launch_gray_rows(ctx->cur, gray, pitch, g, pr, planes, fs.sones, fs.krec, fs.kpos);
+    bic::launch_gray_rows(ctx->cur, gray, pitch, g, pr, planes, fs.sones, fs.krec, fs.kpos, fs.counter);
   });
   timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
   timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",

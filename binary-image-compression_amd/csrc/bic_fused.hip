@@ -1615,7 +1615,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
                   uint64_t* out_g, uint64_t slot_g, uint64_t* bits_g, uint64_t* out_e, uint64_t slot_e,
                   uint64_t* bits_e, uint32_t* flags, int mode, int stage) {
   if (stage == kFusedPrep) {
-    (void)hipMemsetAsync(fs.counter, 0, mode == kEncStaged ? 256 : fs.zero_bytes, s);
+    // the staged encoder's count pass zeroes its counters itself (kZeroWords, launch_row_ones /
+    // launch_gray_rows)
+    if (mode != kEncStaged) (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
     return;
   }
   const bool single_pass = mode == kEncSingle;
@@ -1645,7 +1647,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
   if (mode == kEncStaged) {
     if (stage == kFusedPrefix) {
-      if (!fs.counted) launch_row_ones(s, g, planes, predict, fs.sones, fs.krec, fs.kpos);
+      if (!fs.counted) launch_row_ones(s, g, planes, predict, fs.sones, fs.krec, fs.kpos, fs.counter);
       const uint32_t sgrid = (g.rows + kScanChunk - 1) / kScanChunk * g.nplanes;
       if (dg) k_scan_rows<true, true><<<sgrid, 1024, 0, s>>>(a);
       else k_scan_rows<true, false><<<sgrid, 1024, 0, s>>>(a);

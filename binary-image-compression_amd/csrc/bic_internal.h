@@ -123,14 +123,16 @@ constexpr int kEncStaged = 0, kEncSingle = 1, kEncTwoPass = 2;
 // launch_fused stages: zero the tickets and records; the staged encoder's prefix kernels (counts,
 // scans, lengths); the row kernel(s); the LDS-overflow rows and the words adjacent rows share
 constexpr int kFusedPrep = 0, kFusedRows = 1, kFusedFinish = 2, kFusedPrefix = 3;
+// the staged encoder's count passes also zero its kZeroWords counters (no separate fill launch)
+constexpr uint32_t kZeroWords = 64;
 void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint32_t* sones,
-                     int4* krec, uint32_t* kpos);
+                     int4* krec, uint32_t* kpos, uint32_t* zero);
 // bitplanes + the count pass in one read of the gray image (bic_encode_gray); gray_strips(g)
 // k statistics records per row (one per 64-word strip)
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes);
 uint32_t gray_strips(const Geom& g);
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
-                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos);
+                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero);
 
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
                          uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd);

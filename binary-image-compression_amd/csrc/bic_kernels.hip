@@ -231,7 +231,8 @@ __global__ __launch_bounds__(kBlock) void k_med_rows(Geom g, const uint64_t* __r
 template <int LW, int RPW, bool PREDICT>
 __global__ __launch_bounds__(kBlock) void k_med_kstat(Geom g, const uint64_t* __restrict__ planes,
                                                       uint32_t* __restrict__ sones, int4* __restrict__ krec,
-                                                      uint32_t* __restrict__ kpos) {
+                                                      uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
+  if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   const int lane = lane_id();
   const uint32_t wpp = (g.rows + RPW - 1) / RPW;  // waves per plane
   const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
@@ -288,11 +289,11 @@ __global__ __launch_bounds__(kBlock) void k_med_kstat(Geom g, const uint64_t* __
 }
 
 void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint32_t* sones,
-                     int4* krec, uint32_t* kpos) {
+                     int4* krec, uint32_t* kpos, uint32_t* zero) {
   constexpr int RPW = 8;
   const uint32_t wpp = (g.rows + RPW - 1) / RPW;
   const uint32_t grid = (uint32_t)(((uint64_t)wpp * g.nplanes + kWaves - 1) / kWaves);
-#define BIC_KST(LW, P) k_med_kstat<LW, RPW, P><<<grid, kBlock, 0, s>>>(g, planes, sones, krec, kpos)
+#define BIC_KST(LW, P) k_med_kstat<LW, RPW, P><<<grid, kBlock, 0, s>>>(g, planes, sones, krec, kpos, zero)
   if (g.used <= 64) { if (predict) BIC_KST(1, true); else BIC_KST(1, false); }
   else if (g.used <= 128) { if (predict) BIC_KST(2, true); else BIC_KST(2, false); }
   else { if (predict) BIC_KST(4, true); else BIC_KST(4, false); }
@@ -345,8 +346,9 @@ template <bool PREDICT>
 __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
                                                         uint32_t ns, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
-                                                        uint32_t* __restrict__ kpos) {
+                                                        uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
+  if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   const int lane = lane_id();
   uint32_t* tw = tab[threadIdx.x >> 6];
   const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
@@ -422,12 +424,12 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
 }
 
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
-                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos) {
+                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero) {
   const uint32_t ns = gray_strips(g);
   const uint64_t waves = (uint64_t)(g.rows + kGrayRows - 1) / kGrayRows * ns;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
-  if (predict) k_gray_strips<true><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos);
-  else k_gray_strips<false><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos);
+  if (predict) k_gray_strips<true><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos, zero);
+  else k_gray_strips<false><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos, zero);
 }
 
 void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,
