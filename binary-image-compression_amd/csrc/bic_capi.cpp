@@ -43,6 +43,7 @@ struct bic_ctx {
   unsigned match_parts = 0;       // bic_set_match_parts: workgroups per tile (0 = by region size)
   // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
   bool prof_on = false;
+  std::string prof_only;  // bic_prof_only: bracket only launches of this name ("" = all)
   bool force_multipass = false;
   bool two_pass = false;       // BIC_OPT_TWO_PASS: the two-pass row encoder instead of the staged one
   bool single_kernel = false;  // BIC_OPT_SINGLE_KERNEL: the single kernel with decoupled look-backs
@@ -73,7 +74,7 @@ hipEvent_t take_event(bic_ctx* ctx) {
 // Runs one launch, bracketed by events when profiling is on.
 template <typename F>
 void timed(bic_ctx* ctx, const char* name, F&& launch) {
-  if (!ctx->prof_on) {
+  if (!ctx->prof_on || (!ctx->prof_only.empty() && ctx->prof_only != name)) {
     launch();
     return;
   }
@@ -702,6 +703,12 @@ int bic_tile_lentab(unsigned W, uint64_t* lentab) {
 int bic_prof_enable(bic_ctx* ctx, int on) {
   if (!ctx) return BIC_EINVAL;
   ctx->prof_on = on != 0;
+  return BIC_OK;
+}
+
+int bic_prof_only(bic_ctx* ctx, const char* name) {
+  if (!ctx) return BIC_EINVAL;
+  ctx->prof_only = name ? name : "";
   return BIC_OK;
 }
 

@@ -24,7 +24,7 @@ EXPORTS = [
     "bic_sync",
     "bic_strerror", "bic_device_count", "bic_reserve", "bic_bitplanes_u8", "bic_med_residual",
     "bic_encode_planes", "bic_encode_planes2", "bic_ctx_set_option", "bic_encode_slot_words", "bic_golomb_encode_samples", "bic_patch_encode",
-    "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_enum_codelength", "bic_tile_lentab",
+    "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_prof_only", "bic_enum_codelength", "bic_tile_lentab",
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
 ]
@@ -80,6 +80,7 @@ def load(path=LIB_PATH):
     sig("bic_pack_streams", i32, [vp, vp, i32, sz, vp, vp, vp])
     sig("bic_prof_enable", i32, [vp, i32])
     sig("bic_prof_collect", i32, [vp, C.c_char_p, sz])
+    sig("bic_prof_only", i32, [vp, C.c_char_p])
     sig("bic_enum_codelength", C.c_double, [u32, u32])
     sig("bic_tile_lentab", i32, [u32, vp])
     sig("bic_malloc", i32, [vp, sz, C.POINTER(vp)])
@@ -172,6 +173,10 @@ class Context:
 
     def prof_enable(self, on=True):
         self._chk(self.lib.bic_prof_enable(self.h, int(on)), "bic_prof_enable")
+
+    def prof_only(self, name=None):
+        """bracket only launches recorded as `name` (None = all; bic_prof_only)"""
+        self._chk(self.lib.bic_prof_only(self.h, name.encode() if name else None), "bic_prof_only")
 
     def prof_collect(self):
         """-> {kernel name: (launches, total_ms)} since the last collect (syncs)."""

@@ -210,6 +210,10 @@ int bic_pbm_pack(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, 
  * and clears the records. */
 int bic_prof_enable(bic_ctx* ctx, int on);
 int bic_prof_collect(bic_ctx* ctx, char* buf, size_t cap);
+/* Restrict the bracketing to launches recorded under `name` (NULL or "" = every launch). Each
+ * event pair costs the step a few microseconds of pipeline drain, so a timed region that needs
+ * one kernel's duration brackets only that kernel. */
+int bic_prof_only(bic_ctx* ctx, const char* name);
 
 #ifdef __cplusplus
 }
