@@ -194,14 +194,20 @@ class C3:
                 "frac": round(byts / avg_s / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 2)}
 
     def check(self, oracle):
-        """plane 0 of the last step: Golomb and EG streams == the oracle's."""
-        P = self.pybic.as_u64(self.planes[0])
+        """every plane of the last step: the planes == the oracle's bitplanes of the gray image,
+        and each plane's Golomb and EG streams == the oracle's (host threads)"""
+        P = self.pybic.as_u64(self.planes)
+        gray = self.gray[(self.k - 1) & 1].cpu().numpy()
+        if not np.array_equal(P, oracle.bitplanes_par(gray, self.nplanes)):
+            return False
+        exp = oracle.encode_planes_par(P, self.cols, 1)
         ok = True
         for coder, out, bits in ((0, self.out_g, self.bits_g), (1, self.out_e, self.bits_e)):
-            eb, est, _ = oracle.encode_plane(P, self.cols, 1, coder)
-            nb = int(self.pybic.as_u64(bits)[0])
-            ok &= (nb == eb) and self.pybic.stream_bytes(out[0], nb) == est.tobytes()
-        return ok
+            B = self.pybic.as_u64(bits)
+            for k in range(self.nplanes):
+                eb, est = exp[(k, coder)]
+                ok &= int(B[k]) == eb and self.pybic.stream_bytes(out[k], eb) == est.tobytes()
+        return bool(ok)
 
 
 class C2(C3):

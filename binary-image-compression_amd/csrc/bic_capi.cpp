@@ -48,6 +48,7 @@ struct bic_ctx {
   bool two_pass = false;       // BIC_OPT_TWO_PASS: the two-pass row encoder instead of the staged one
   bool single_kernel = false;  // BIC_OPT_SINGLE_KERNEL: the single kernel with decoupled look-backs
   bool force_staged = false;   // BIC_OPT_STAGED: the staged encoder whatever the batch size
+  bool one_stream = false;     // BIC_OPT_ONE_STREAM: no second stream for the staged encoder's emission
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -109,6 +110,11 @@ int ensure_scratch(bic_ctx* ctx, size_t bytes) {
 // The staged encoder's second stream and its fork / join events, made on first use; left null
 // (one stream) when HIP cannot make them. Work on it is always joined back into ctx->cur.
 void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
+  if (ctx->one_stream) {
+    fs.aux = nullptr;
+    fs.ev_fork = fs.ev_join = nullptr;
+    return;
+  }
   if (!ctx->aux) {
     hipStream_t st = nullptr;
     hipEvent_t a = nullptr, b = nullptr;
@@ -320,6 +326,10 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
   }
   if (option == BIC_OPT_STAGED) {
     ctx->force_staged = value != 0;
+    return BIC_OK;
+  }
+  if (option == BIC_OPT_ONE_STREAM) {
+    ctx->one_stream = value != 0;
     return BIC_OK;
   }
   return BIC_EINVAL;

@@ -475,6 +475,12 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
   }
 }
 
+// glen[] flags of the staged encoder (set by the prefix kernels, read-only afterwards: every
+// consumer masks them off, so the two emission launches never write glen)
+constexpr uint64_t kK0Row = 1ull << 63;  // every codeword of the row has k = 0
+constexpr uint64_t kK1Row = 1ull << 62;  // every codeword of the row has k = 1
+constexpr uint64_t kLenMask = kK1Row - 1;
+
 struct FusedArgs {
   Geom g;
   const uint64_t* planes;
@@ -557,7 +563,7 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
   const Geom& g = a.g;
   const uint64_t slow = a.gslow[id];
   const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
-  const uint64_t G = a.gboff[id], L = a.glen[id];
+  const uint64_t G = a.gboff[id], L = a.glen[id] & kLenMask;
   uint64_t* frag = a.gfrag + 2 * id;
   const uint64_t wh = G >> 6, wt = (G + L - 1) >> 6;
   const bool hpart = !word_complete(wh, G, L);
@@ -1127,10 +1133,6 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
 // wave walks its rows independently (persistent waves, static row order, no barriers).
 // ==========================================================================================
 
-constexpr uint64_t kK0Row = 1ull << 63;  // glen flags: every codeword of the row has k = 0,
-constexpr uint64_t kK1Row = 1ull << 62;  // every codeword of the row has k = 1
-constexpr uint64_t kLenMask = kK1Row - 1;
-
 // Golomb length of a row from its sample base O (ones of the plane before it): rows whose k
 // statistics (bic_kstat.h) prove every codeword k = 0 (length cols + 1: the residual row and its
 // end-of-row '1') or k = 1 (2n + (zeros - odd runs) / 2) get their length without being read;
@@ -1436,8 +1438,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
         write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
       }
       if (lane == 0) {
-        // drop the flags (k_fixup reads plain lengths); a first-1 row's only after k_emit_rest read them
-        if ((k0 || k1) && !f_here) a.glen[id] = L;
+        // glen keeps its flags: k_emit_rest (on the other stream) reads them too
         const bool slow = L && !k0 && !fits;
         a.gslow[id] = slow ? O + row + 1 : 0;  // k_rows_global writes the row
         if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
@@ -1531,7 +1532,6 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
       if (threadIdx.x == 0 && tot != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
       write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id, threadIdx.x, blockDim.x);
     }
-    if (DO_G && threadIdx.x == 0 && (k0 || k1) && f_here) a.glen[id] = L;  // drop the flags (k_fixup)
     __syncthreads();  // the images and sh are reused by the next row
   }
 }
@@ -1552,7 +1552,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
   }
   const uint64_t id = (uint64_t)(blockIdx.x >= second ? blockIdx.x - second : blockIdx.x) * 256 + threadIdx.x;
   if (id >= nrows) return;
-  const uint64_t G = boff[id], L = len[id];
+  const uint64_t G = boff[id], L = len[id] & kLenMask;  // (the staged encoder's glen carries row flags)
   if (L == 0) return;
   const uint64_t wt = (G + L - 1) >> 6, wh = G >> 6;
   const uint64_t wb = wt * 64;
@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
   uint64_t v = (wh == wt) ? frag[2 * id] : frag[2 * id + 1];
   const uint64_t pend = (id / rows + 1) * (uint64_t)rows;
   for (uint64_t r2 = id + 1; r2 < pend; ++r2) {
-    if (len[r2] == 0 || boff[r2] >= wb + 64) break;
+    if ((len[r2] & kLenMask) == 0 || boff[r2] >= wb + 64) break;
     v |= frag[2 * r2];
   }
   out[wt] = bswap64(v);

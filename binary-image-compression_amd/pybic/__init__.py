@@ -286,6 +286,11 @@ class Context:
         self._chk(self.lib.bic_ctx_set_option(self.h, 2, int(name == "two-pass")), "bic_ctx_set_option")
         self._chk(self.lib.bic_ctx_set_option(self.h, 3, int(name == "single-kernel")), "bic_ctx_set_option")
 
+    def set_one_stream(self, on=True):
+        """the staged encoder's two emission launches one after the other on the ctx stream
+        (BIC_OPT_ONE_STREAM) instead of side by side on a second stream"""
+        self._chk(self.lib.bic_ctx_set_option(self.h, 5, int(on)), "bic_ctx_set_option")
+
     def set_multipass(self, on=True):
         self._chk(self.lib.bic_ctx_set_option(self.h, 1, int(on)), "bic_ctx_set_option")
 

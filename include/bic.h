@@ -80,6 +80,10 @@ int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
 #define BIC_OPT_TWO_PASS 2
 #define BIC_OPT_SINGLE_KERNEL 3
 #define BIC_OPT_STAGED 4
+/* BIC_OPT_ONE_STREAM = 1: the staged encoder's two emission launches run one after the other on
+ * the ctx stream instead of side by side on a second stream (same output; a test hook for the
+ * launch ordering). */
+#define BIC_OPT_ONE_STREAM 5
 int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
 
 /* ---- a2: bitplane extraction (bitplane_tool.cpp:24-30) -----------------------------------

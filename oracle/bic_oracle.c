@@ -520,11 +520,17 @@ uint64_t bo_baseline_planes(const uint64_t* planes, int nplanes, size_t rows, si
  * unsigned difference is negative for i0 < W, so the first loop is skipped). */
 void bo_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
                      uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+    bo_patch_search_rows(I, rows, cols, wpr, W, 0, (W - 1 + rows) / W, besti, bestj, bestd);
+}
+
+void bo_patch_search_rows(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                          size_t tr0, size_t tr1, uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
     const size_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
     const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
     uint64_t P[64], P2[64];
-    size_t li = 0;
-    for (size_t i = 0; i < Ny; i++)
+    if (tr1 > Ny) tr1 = Ny;
+    size_t li = tr0 * Nx;
+    for (size_t i = tr0; i < tr1; i++)
         for (size_t j = 0; j < Nx; j++, li++) {
             const size_t i0 = i * W, j0 = j * W;
             bo_get_submatrix(I, rows, cols, wpr, i0, i0 + W, j0, j0 + W, P, 1);

@@ -150,6 +150,11 @@ int64_t bo_patch_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsig
  * early exit at a perfect match; (0, 0, W*W) when nothing beats W*W. */
 void bo_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
                      uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
+/* The same search for the tiles of tile rows [tr0, tr1) only (every tile's search is independent
+ * of the others' results), written at their raster indices of the full arrays: lets the tests
+ * split the checker over host threads. */
+void bo_patch_search_rows(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                          size_t tr0, size_t tr1, uint32_t* besti, uint32_t* bestj, uint32_t* bestd);
 
 /* compress7_test.cpp:117-275 with search window R and match threshold T (rows, cols multiples
  * of W): per tile the causal search over the image as modified by the residual write-back of

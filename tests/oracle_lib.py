@@ -50,6 +50,7 @@ class Oracle:
              [u64p, sz, sz, sz, C.c_uint, u64p, u32p, u32p, C.c_char_p, u64p, u8p, sz])
         _sig(L, "bo_baseline_planes", C.c_uint64, [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, C.POINTER(C.c_int)])
         _sig(L, "bo_patch_search", None, [u64p, sz, sz, sz, C.c_uint, u32p, u32p, u32p])
+        _sig(L, "bo_patch_search_rows", None, [u64p, sz, sz, sz, C.c_uint, sz, sz, u32p, u32p, u32p])
         _sig(L, "bo_match_encode", C.c_int,
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p,
               u8p, u8p, sz])
@@ -174,6 +175,41 @@ class Oracle:
         bi, bj, bd = (np.zeros(n, np.uint32) for _ in range(3))
         self.lib.bo_patch_search(ptr(I, u64p), rows, cols, wpr, W, ptr(bi, u32p), ptr(bj, u32p), ptr(bd, u32p))
         return bi, bj, bd
+
+    def patch_search_par(self, I, cols, W, threads=None):
+        """patch_search split by tile rows over host threads (ctypes drops the GIL); the later
+        tile rows search more windows, so the rows are dealt out round-robin"""
+        I = np.ascontiguousarray(I)
+        rows, wpr = I.shape
+        ny, nx = (rows + W - 1) // W, (cols + W - 1) // W
+        bi, bj, bd = (np.zeros(ny * nx, np.uint32) for _ in range(3))
+
+        def one(tr):
+            self.lib.bo_patch_search_rows(ptr(I, u64p), rows, cols, wpr, W, tr, tr + 1, ptr(bi, u32p),
+                                          ptr(bj, u32p), ptr(bd, u32p))
+        pool_map(one, list(range(ny - 1, -1, -1)), threads)
+        return bi, bj, bd
+
+    def bitplanes_par(self, gray, nplanes, threads=None, band=512):
+        """bitplanes over bands of rows on host threads"""
+        gray = np.ascontiguousarray(gray)
+        rows, cols = gray.shape
+        out = np.zeros((nplanes, rows, (cols + 63) // 64), np.uint64)
+
+        def one(r0):
+            out[:, r0:r0 + band] = self.bitplanes(gray[r0:r0 + band], nplanes)
+        pool_map(one, list(range(0, rows, band)), threads)
+        return out
+
+    def encode_planes_par(self, planes, cols, predict, coders=(0, 1), threads=None):
+        """{(plane, coder): (nbits, stream bytes)} for every plane and coder, on host threads"""
+        jobs = [(k, c) for k in range(planes.shape[0]) for c in coders]
+
+        def one(job):
+            k, c = job
+            b, st, _ = self.encode_plane(planes[k], cols, predict, c)
+            return job, (b, st)
+        return dict(pool_map(one, jobs, threads))
 
     def enum_table(self, W):
         """enumL(W*W, w) for w = 0..W*W (the double table the match loop takes)."""
@@ -316,6 +352,23 @@ class Ref:
 
 def have_ref():
     return os.path.exists(REF_SO)
+
+
+def host_threads():
+    """worker threads for the checker: the box's CPU share (OMP_NUM_THREADS is set to it there;
+    os.cpu_count() reports the whole machine)"""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(16, n or os.cpu_count() or 1))
+
+
+def pool_map(fn, items, threads=None):
+    """fn over items on a thread pool, results in order (the oracle's ctypes calls drop the GIL)"""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=threads or host_threads()) as ex:
+        return list(ex.map(fn, items))
 
 
 def pack_rows(bits):

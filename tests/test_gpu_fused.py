@@ -146,6 +146,36 @@ def test_k_classes_wide_rows(ctx, oracle, encoder, p):
         check(ctx, oracle, P, cols, pred)
 
 
+@pytest.mark.parametrize("one_stream", [False, True])
+@pytest.mark.parametrize("cols", [16384, 1000, 64])
+def test_first_one_row_with_k_flags(ctx, oracle, one_stream, cols):
+    """The row holding a plane's first 1 is written by both emission launches (the REST one writes
+    its EG row, the main one its Golomb row when every codeword there has k = 1). Row 0's residual
+    "001001..." gives codewords of k = 1 only (s = 2 from the fresh k = 1 state keeps k = 1), so
+    that row is flagged k = 1 AND holds the first 1, in every plane; the two launches run side by
+    side on two streams or one after the other (BIC_OPT_ONE_STREAM), and neither may depend on
+    what the other does with the row's length flags."""
+    ctx.set_encoder("staged")
+    ctx.set_one_stream(one_stream)
+    try:
+        rows, n = 48, 4
+        wpr = (cols + 63) // 64
+        R0 = np.zeros(cols, bool)
+        R0[2::3] = True
+        P0 = np.cumsum(R0) % 2 == 1  # row 0's med residual is P[j] ^ P[j-1]: invert by a prefix xor
+        from oracle_lib import pack_rows
+        P = np.zeros((n, rows, wpr), np.uint64)
+        for k in range(n):
+            P[k] = oracle.gen_plane(700 + k, (0.5, 0.3, 0.1, 0.02)[k], rows, cols)
+            P[k, 0] = pack_rows(P0[None])[0]
+        R = oracle.med(P[0], cols)
+        assert np.array_equal(R[0], pack_rows(R0[None])[0])
+        check(ctx, oracle, P, cols, 1)
+    finally:
+        ctx.set_one_stream(False)
+        ctx.set_encoder("auto")
+
+
 def _gray(oracle, seed, rows, cols, kind):
     if kind == "uniform":
         return oracle.gen_bytes(seed, rows * cols).reshape(rows, cols)
