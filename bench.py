@@ -40,6 +40,10 @@ def parse():
                     help="repeat the CPU baseline sample until this much CPU time has been measured")
     ap.add_argument("--encoder", default="auto", choices=["auto", "staged", "single-kernel", "two-pass", "multipass"],
                     help="row encoder for rows <= 16384 columns (bic_ctx_set_option)")
+    ap.add_argument("--shard", default="images", choices=["images", "planes"],
+                    help="c3 at N GPUs: one image per GPU (weak scaling, no exchange) or the 8 planes of ONE "
+                         "image split over the GPUs, every rank's packed streams gathered to rank 0 over RCCL "
+                         "(strong scaling; the gather is in the timed step)")
     ap.add_argument("--separate", action="store_true",
                     help="c3: bic_bitplanes_u8 then bic_encode_planes2 instead of the one-call bic_encode_gray")
     ap.add_argument("--no-cpu", action="store_true")
@@ -208,6 +212,113 @@ class C3:
                 eb, est = exp[(k, coder)]
                 ok &= int(B[k]) == eb and self.pybic.stream_bytes(out[k], eb) == est.tobytes()
         return bool(ok)
+
+
+class C3Planes(C3):
+    """C3 sharded by planes (SURVEY.md §8 e: "8 planes -> 1 per GPU"): every rank holds the same
+    gray image and encodes planes [8r/N, 8(r+1)/N) of it (bic_encode_gray_range), packs each
+    coder's streams word-aligned (bic_pack_streams) and sends them to rank 0 (gather_streams: one
+    all-gather of sizes, point-to-point RCCL transfers over xGMI), which ends the step holding the
+    whole image's streams in plane order. Strong scaling: one image per step whatever N."""
+
+    def __init__(self, ctx, args, rank, world):
+        import pybic
+        t = ctx.torch
+        self.ctx, self.pybic, self.rank, self.world = ctx, pybic, rank, world
+        self.rows = args.rows or 16384
+        self.cols = args.cols or 16384
+        self.lo, self.hi = rank * 8 // world, (rank + 1) * 8 // world
+        self.nplanes = self.hi - self.lo
+        g = t.Generator(device=ctx.dev)
+        g.manual_seed(0x5EED0000)  # the same image on every rank
+        self.gray = [t.randint(0, 256, (self.rows, self.cols), dtype=t.uint8, device=ctx.dev, generator=g)
+                     for _ in range(2)]
+        self.wpr = (self.cols + 63) // 64
+        self.planes = ctx.empty_i64(max(1, self.nplanes), self.rows, self.wpr)
+        self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
+        self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
+        n = max(1, self.nplanes)
+        self.out_g, self.out_e = ctx.empty_i64(n, self.slot_g), ctx.empty_i64(n, self.slot_e)
+        self.bits_g, self.bits_e = ctx.empty_i64(n), ctx.empty_i64(n)
+        self.gathered = (None, None)
+        ctx.reserve(n, self.rows, self.cols)
+        self.k = 0
+        self.separate = False
+        self.pixels = self.rows * self.cols * self.nplanes
+        self.workload = (f"c3 sharded by planes: one {self.rows}x{self.cols} 8-bit gray image per step, its 8 "
+                         f"planes split over {world} GPU(s) -> med -> Golomb + EG, packed streams gathered to "
+                         f"rank 0")
+
+    def step(self):
+        from pybic.parallel import gather_streams
+        c = self.ctx
+        if self.nplanes:
+            c.encode_gray(self.gray[self.k & 1], nplanes=self.nplanes, plane0=self.lo, planes=self.planes,
+                          slots=(self.slot_g, self.slot_e), outs=(self.out_g, self.out_e),
+                          bits=(self.bits_g, self.bits_e))
+        got = []
+        for out, bits in ((self.out_g, self.bits_g), (self.out_e, self.bits_e)):
+            packed, off = c.pack_streams(out[:self.nplanes], bits[:self.nplanes])
+            if self.world > 1:
+                got.append(gather_streams(packed, off[-1:], self.world, self.rank))
+            else:
+                got.append((packed, [0, int(off[-1].item())]))
+        self.gathered = tuple(got)
+        self.k += 1
+
+    def collect(self):
+        """every rank's per-plane bit counts on every rank (collective, after the timed steps)"""
+        import torch
+        res = []
+        for bits in (self.bits_g, self.bits_e):
+            t = torch.zeros(8, dtype=torch.int64)
+            t[:self.nplanes] = bits[:self.nplanes].cpu()
+            if self.world > 1:
+                import torch.distributed as dist
+                host = dist.get_backend() == "gloo"
+                t = t if host else t.to(self.ctx.dev)
+                outs = [torch.zeros_like(t) for _ in range(self.world)]
+                dist.all_gather(outs, t)
+                res.append([o.cpu().numpy().view(np.uint64) for o in outs])
+            else:
+                res.append([t.numpy().view(np.uint64)])
+        self.allbits = res
+
+    def out_bytes(self):
+        b = self.pybic.as_u64(self.bits_g[:self.nplanes]).astype(np.int64).sum() + \
+            self.pybic.as_u64(self.bits_e[:self.nplanes]).astype(np.int64).sum()
+        return int(b) / 8.0
+
+    def host_planes(self, rows):
+        return self.pybic.as_u64(self.planes[:self.nplanes, :rows])
+
+    def check(self, oracle):
+        """rank 0, after collect(): the gathered streams of all 8 planes == the oracle's streams of
+        bitplane_tool's planes of the last step's image"""
+        gray = self.gray[(self.k - 1) & 1].cpu().numpy()
+        exp_planes = oracle.bitplanes_par(gray, 8)
+        exp = oracle.encode_planes_par(exp_planes, self.cols, 1)
+        ok = True
+        for coder in (0, 1):
+            words, offs = self.gathered[coder]
+            W = self.pybic.as_u64(words)
+            for r in range(self.world):
+                a, b = r * 8 // self.world, (r + 1) * 8 // self.world
+                o = offs[r]
+                for k in range(a, b):
+                    nb = int(self.allbits[coder][r][k - a])
+                    nw = (nb + 63) // 64
+                    eb, est = exp[(k, coder)]
+                    ok &= nb == eb and W[o:o + nw].tobytes() == est.tobytes()
+                    o += nw
+                ok &= o == offs[r + 1]
+        return bool(ok)
+
+    def kernel_bytes(self):
+        plane_b = self.nplanes * self.rows * self.wpr * 8
+        g = int(self.pybic.as_u64(self.bits_g[:self.nplanes]).astype(np.int64).sum()) // 8
+        e = int(self.pybic.as_u64(self.bits_e[:self.nplanes]).astype(np.int64).sum()) // 8
+        return {"bitplanes_count": self.rows * self.cols + plane_b, "encode_rows_golomb_eg": plane_b + g + e}
 
 
 class C2(C3):
@@ -510,7 +621,7 @@ def cpu_baseline(wl, args):
         return None
     nplanes = planes.shape[0]
     threads = max(1, min(nplanes, int(os.environ.get("OMP_NUM_THREADS", "8") or 8)))
-    do_eg = 1 if isinstance(wl, C3) and type(wl) is C3 else 0
+    do_eg = 1 if type(wl) in (C3, C3Planes) else 0
     predict = 0 if isinstance(wl, C2) else 1
     reps, dt, used = 0, 0.0, 0
     while reps == 0 or (dt < args.cpu_seconds and reps < 32):
@@ -541,7 +652,9 @@ def main():
     import pybic
     ctx = pybic.Context(local)
     ctx.set_encoder(args.encoder)
-    if args.workload == "c3":
+    if args.workload == "c3" and args.shard == "planes":
+        wl = C3Planes(ctx, args, rank, world)
+    elif args.workload == "c3":
         wl = C3(ctx, args, rank)
     elif args.workload == "c2":
         wl = C2(ctx, args, rank)
@@ -600,6 +713,8 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc(args.workload, dom), "kernel": dom,
                 "algorithmic_bytes_per_launch": kb[dom], "avg_launch_us": round(avg_s * 1e6, 2)}
     pred_pass = wl.predictor_pass(max(args.steps, 5)) if hasattr(wl, "predictor_pass") and type(wl) is C3 else None
+    if hasattr(wl, "collect"):
+        wl.collect()
     ok = None
     cpu = None
     if rank == 0 and not args.no_check:
@@ -611,11 +726,12 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong" if args.workload in ("c4", "c5") else "weak", "vs_baseline": None, "dtype": "u64",
+            "scaling": "strong" if args.workload in ("c4", "c5") or isinstance(wl, C3Planes) else "weak", "vs_baseline": None, "dtype": "u64",
             "data": ("synthetic text-like page (seeded glyph alphabet), device-resident" if args.workload == "c1m"
                      else "synthetic (seeded uniform bytes / Bernoulli(0.5) words, device-resident)"),
             "config": {"workload": wl.workload, "rows": wl.rows, "cols": wl.cols, "planes_per_gpu": wl.nplanes,
-                       "parallelism": {"c4": f"dp{world} (64 frames sharded)",
+                       "parallelism": f"dp{world} (planes of one image sharded, streams gathered to rank 0)"
+                       if isinstance(wl, C3Planes) else {"c4": f"dp{world} (64 frames sharded)",
                                        "c5": f"dp{world} (tile-row bands, coder state exchanged)"}.get(
                                            args.workload, f"dp{world} (independent images per GPU)")},
             "mb_per_s_out": round(out_all / dt_max / 1e6, 1),

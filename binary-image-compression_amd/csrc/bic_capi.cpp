@@ -335,19 +335,25 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
   return BIC_EINVAL;
 }
 
-int bic_bitplanes_u8(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols,
-                     int nplanes, uint64_t* planes, size_t wpr) {
+int bic_bitplanes_u8_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                           int nplanes, uint64_t* planes, size_t wpr) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if (nplanes < 1 || nplanes > 8 || pitch < cols || (rows && (!gray || !planes))) return BIC_EINVAL;
+  if (plane0 < 0 || nplanes < 1 || plane0 + nplanes > 8 || pitch < cols || (rows && (!gray || !planes)))
+    return BIC_EINVAL;
   if (!geom_ok(rows, cols, wpr)) return BIC_EINVAL;
   if (rows == 0) return BIC_OK;
   timed(ctx, "bitplanes_u8", [&] {
-    bic::launch_bitplanes_u8(ctx->cur, gray, pitch, (uint32_t)rows, (uint32_t)cols, nplanes, planes,
+    bic::launch_bitplanes_u8(ctx->cur, gray, pitch, (uint32_t)rows, (uint32_t)cols, plane0, nplanes, planes,
                              (uint32_t)wpr);
   });
   BIC_HIP(hipGetLastError());
   return BIC_OK;
+}
+
+int bic_bitplanes_u8(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols,
+                     int nplanes, uint64_t* planes, size_t wpr) {
+  return bic_bitplanes_u8_range(ctx, gray, pitch, rows, cols, 0, nplanes, planes, wpr);
 }
 
 int bic_med_residual(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
@@ -440,12 +446,14 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
   return BIC_OK;
 }
 
-int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,
-                    uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
-                    uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg) {
+int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                          int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
+                          size_t slot_golomb, uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg,
+                          uint64_t* bits_eg) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if (nplanes < 1 || nplanes > 8 || pitch < cols || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
+  if (plane0 < 0 || nplanes < 1 || plane0 + nplanes > 8 || pitch < cols || !geom_ok(rows, cols, wpr))
+    return BIC_EINVAL;
   if (!out_golomb && !out_eg) return BIC_EINVAL;
   if (out_golomb && (!bits_golomb || slot_golomb == 0)) return BIC_EINVAL;
   if (out_eg && (!bits_eg || slot_eg == 0)) return BIC_EINVAL;
@@ -455,7 +463,7 @@ int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows
                     staged_pays(ctx, g) &&
                     bic::med_rows_supported(g, planes, nullptr) && bic::gray_rows_supported(g, gray, pitch, planes);
   if (!fuse) {  // the same result through the two separate calls
-    if ((rc = bic_bitplanes_u8(ctx, gray, pitch, rows, cols, nplanes, planes, wpr))) return rc;
+    if ((rc = bic_bitplanes_u8_range(ctx, gray, pitch, rows, cols, plane0, nplanes, planes, wpr))) return rc;
     return bic_encode_planes2(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
                               out_eg, slot_eg, bits_eg);
   }
@@ -471,7 +479,7 @@ int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows
   };
   stage(bic::kFusedPrep);
   timed(ctx, "bitplanes_count", [&] {
-    bic::launch_gray_rows(ctx->cur, gray, pitch, g, pr, planes, fs.sones, fs.krec, fs.kpos, fs.counter);
+    bic::launch_gray_rows(ctx->cur, gray, pitch, g, pr, plane0, planes, fs.sones, fs.krec, fs.kpos, fs.counter);
   });
   timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
   timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
@@ -479,6 +487,13 @@ int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows
   timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
   BIC_HIP(hipGetLastError());
   return BIC_OK;
+}
+
+int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,
+                    uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                    uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg) {
+  return bic_encode_gray_range(ctx, gray, pitch, rows, cols, 0, nplanes, planes, wpr, predict, out_golomb,
+                               slot_golomb, bits_golomb, out_eg, slot_eg, bits_eg);
 }
 
 int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,

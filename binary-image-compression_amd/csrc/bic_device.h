@@ -16,6 +16,12 @@ constexpr int kLdsWords = 1024;  // u32 staging words per wave in the emitter (3
 // wave / block primitives (wave64)
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// wave-uniform copies (SGPRs): the compiler cannot always prove a value uniform (e.g. the result of
+// a branchy index remap), and a uniform loop counter in VGPRs turns the loop into an exec-masked one
+__device__ __forceinline__ uint32_t uni_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
+  return ((uint64_t)uni_u32((uint32_t)(v >> 32)) << 32) | uni_u32((uint32_t)v);
+}
 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   const uint32_t lo = __shfl((unsigned)(v & 0xffffffffu), src);

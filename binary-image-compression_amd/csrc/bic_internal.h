@@ -44,7 +44,7 @@ ChunkScratch carve_chunk_scratch(void* base, const Geom& g);
 
 // Launchers (all asynchronous on `s`). flags[0] = overflow, flags[1] = domain error.
 void launch_bitplanes_u8(hipStream_t s, const uint8_t* gray, size_t pitch, uint32_t rows,
-                         uint32_t cols, int nplanes, uint64_t* planes, uint32_t wpr);
+                         uint32_t cols, int plane0, int nplanes, uint64_t* planes, uint32_t wpr);
 void launch_count(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
                   const ChunkScratch& cs, uint64_t* resid, uint64_t* weight_out);
 void launch_scan_rows(hipStream_t s, const Geom& g, const ChunkScratch& cs);
@@ -131,7 +131,7 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 // k statistics records per row (one per 64-word strip)
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes);
 uint32_t gray_strips(const Geom& g);
-void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
+void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero);
 
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,

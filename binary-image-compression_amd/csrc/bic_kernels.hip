@@ -37,7 +37,7 @@ __device__ __forceinline__ uint64_t transpose8x8(uint64_t x) {
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_bitplanes_u8(const uint8_t* __restrict__ gray, size_t pitch,
                                                          uint32_t rows, uint32_t cols, uint32_t used,
-                                                         int nplanes, uint64_t* __restrict__ planes,
+                                                         int plane0, int nplanes, uint64_t* __restrict__ planes,
                                                          uint32_t wpr) {
   const uint32_t groups = (used + 63) / 64;  // 64-word groups per row
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
@@ -72,23 +72,24 @@ __global__ __launch_bounds__(kBlock) void k_bitplanes_u8(const uint8_t* __restri
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
     if (b >= nplanes) break;
+    const int sb = 8 * (b + plane0);  // output plane b = bit plane0 + b of the gray value
     uint64_t v = 0;
 #pragma unroll
-    for (int g8 = 0; g8 < 8; ++g8) v |= ((T[g8] >> (8 * b)) & 0xffull) << (56 - 8 * g8);
+    for (int g8 = 0; g8 < 8; ++g8) v |= ((T[g8] >> sb) & 0xffull) << (56 - 8 * g8);
     dst[b * plane_words] = v;
   }
 }
 
 void launch_bitplanes_u8(hipStream_t s, const uint8_t* gray, size_t pitch, uint32_t rows,
-                         uint32_t cols, int nplanes, uint64_t* planes, uint32_t wpr) {
+                         uint32_t cols, int plane0, int nplanes, uint64_t* planes, uint32_t wpr) {
   const uint32_t used = (cols + 63) / 64;
   const uint64_t waves = (uint64_t)rows * ((used + 63) / 64);
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
   const bool vec = (pitch % 16 == 0) && (((uintptr_t)gray) % 16 == 0);
   if (vec)
-    k_bitplanes_u8<true><<<grid, kBlock, 0, s>>>(gray, pitch, rows, cols, used, nplanes, planes, wpr);
+    k_bitplanes_u8<true><<<grid, kBlock, 0, s>>>(gray, pitch, rows, cols, used, plane0, nplanes, planes, wpr);
   else
-    k_bitplanes_u8<false><<<grid, kBlock, 0, s>>>(gray, pitch, rows, cols, used, nplanes, planes, wpr);
+    k_bitplanes_u8<false><<<grid, kBlock, 0, s>>>(gray, pitch, rows, cols, used, plane0, nplanes, planes, wpr);
 }
 
 // ------------------------------------------------------------------------------------
@@ -344,7 +345,7 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
 
 template <bool PREDICT>
 __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
-                                                        uint32_t ns, uint64_t* __restrict__ planes,
+                                                        uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
                                                         uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
@@ -365,6 +366,13 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = in ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
     lb = (lane == 0 && s > 0) ? (uint32_t)src[-1] : 0u;
+    if (plane0) {  // planes plane0.. of the range: every pixel's bits shifted down (a wave-uniform branch)
+      const uint32_t m = 0x01010101u * (0xffu >> plane0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = make_uint4((v[q].x >> plane0) & m, (v[q].y >> plane0) & m,
+                                                    (v[q].z >> plane0) & m, (v[q].w >> plane0) & m);
+      lb >>= plane0;
+    }
   };
   uint64_t up[8];
 #pragma unroll
@@ -423,13 +431,13 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
          reinterpret_cast<uintptr_t>(gray) % 16 == 0 && reinterpret_cast<uintptr_t>(planes) % 8 == 0;
 }
 
-void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict,
+void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero) {
   const uint32_t ns = gray_strips(g);
   const uint64_t waves = (uint64_t)(g.rows + kGrayRows - 1) / kGrayRows * ns;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
-  if (predict) k_gray_strips<true><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos, zero);
-  else k_gray_strips<false><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, planes, sones, krec, kpos, zero);
+  if (predict) k_gray_strips<true><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero);
+  else k_gray_strips<false><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero);
 }
 
 void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,

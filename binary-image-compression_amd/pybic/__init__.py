@@ -27,6 +27,7 @@ EXPORTS = [
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_prof_only", "bic_enum_codelength", "bic_tile_lentab",
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
+    "bic_bitplanes_u8_range", "bic_encode_gray_range",
 ]
 
 
@@ -94,6 +95,8 @@ def load(path=LIB_PATH):
     sig("bic_match_encode", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_set_match_parts", i32, [vp, u32])
     sig("bic_encode_gray", i32, [vp, vp, sz, sz, sz, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
+    sig("bic_bitplanes_u8_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz])
+    sig("bic_encode_gray_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
     _lib = L
     return L
 
@@ -189,16 +192,21 @@ class Context:
         return out
 
     # -- ops --------------------------------------------------------------------------
-    def bitplanes_u8(self, gray, cols=None, nplanes=8, wpr=None, out=None):
-        """gray: uint8 device tensor [rows, pitch] -> int64 tensor [nplanes, rows, wpr]."""
+    def bitplanes_u8(self, gray, cols=None, nplanes=8, wpr=None, out=None, plane0=0):
+        """gray: uint8 device tensor [rows, pitch] -> int64 tensor [nplanes, rows, wpr] (planes
+        plane0 .. plane0 + nplanes - 1: bic_bitplanes_u8_range)."""
         rows, pitch = gray.shape
         cols = pitch if cols is None else cols
         wpr = wpr or (cols + 63) // 64
         if out is None:
             out = self.empty_i64(nplanes, rows, wpr)
         self._bind_stream()
-        self._chk(self.lib.bic_bitplanes_u8(self.h, _p(gray), pitch, rows, cols, nplanes, _p(out), wpr),
-                  "bic_bitplanes_u8")
+        if plane0:
+            self._chk(self.lib.bic_bitplanes_u8_range(self.h, _p(gray), pitch, rows, cols, plane0, nplanes, _p(out),
+                                                      wpr), "bic_bitplanes_u8_range")
+        else:
+            self._chk(self.lib.bic_bitplanes_u8(self.h, _p(gray), pitch, rows, cols, nplanes, _p(out), wpr),
+                      "bic_bitplanes_u8")
         return out
 
     def med_residual(self, planes, cols, predict=True, want_resid=True, want_weight=True):
@@ -251,9 +259,10 @@ class Context:
         return (og, bg) if golomb else None, (oe, be) if eg else None
 
     def encode_gray(self, gray, cols=None, nplanes=8, predict=True, planes=None, slots=(None, None),
-                    outs=(None, None), bits=(None, None), golomb=True, eg=True):
+                    outs=(None, None), bits=(None, None), golomb=True, eg=True, plane0=0):
         """gray uint8 [rows, pitch] -> (planes, (out_g, bits_g) or None, (out_e, bits_e) or None):
-        the bitplanes and both streams of every plane in one call (bic_encode_gray)."""
+        the bitplanes and both streams of every plane in one call (bic_encode_gray; planes plane0 ..
+        plane0 + nplanes - 1 with bic_encode_gray_range)."""
         rows, pitch = gray.shape
         cols = pitch if cols is None else cols
         wpr = (cols + 63) // 64
@@ -272,8 +281,13 @@ class Context:
             res.append((out, slot, b))
         (og, sg, bg), (oe, se, be) = res
         self._bind_stream()
-        self._chk(self.lib.bic_encode_gray(self.h, _p(gray), pitch, rows, cols, nplanes, _p(planes), wpr,
-                                           int(predict), _p(og), sg, _p(bg), _p(oe), se, _p(be)), "bic_encode_gray")
+        if plane0:
+            self._chk(self.lib.bic_encode_gray_range(self.h, _p(gray), pitch, rows, cols, plane0, nplanes, _p(planes),
+                                                     wpr, int(predict), _p(og), sg, _p(bg), _p(oe), se, _p(be)),
+                      "bic_encode_gray_range")
+        else:
+            self._chk(self.lib.bic_encode_gray(self.h, _p(gray), pitch, rows, cols, nplanes, _p(planes), wpr,
+                                               int(predict), _p(og), sg, _p(bg), _p(oe), se, _p(be)), "bic_encode_gray")
         return planes, ((og, bg) if golomb else None), ((oe, be) if eg else None)
 
     def set_encoder(self, name):

@@ -91,6 +91,11 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
  * pixel, LSB plane first; nplanes in 1..8 (bitplane_tool extracts #{bi : 2^bi < maxval}). */
 int bic_bitplanes_u8(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols,
                      int nplanes, uint64_t* planes, size_t wpr);
+/* The planes plane0 .. plane0 + nplanes - 1 (plane0 + nplanes <= 8) only: output plane b is bit
+ * plane0 + b of each pixel (bitplane_tool.cpp:24-30's plane index bi = plane0 + b). A rank of a
+ * plane-sharded encode extracts its own share of one image this way. */
+int bic_bitplanes_u8_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                           int nplanes, uint64_t* planes, size_t wpr);
 
 /* ---- a5/a6: med residual + weight (pred.cpp:3-15, binmat.cpp:57-67) -----------------------
  * resid (nullable): the med residual of each plane (R(0,0) = 0 and pad bits 0, which is what
@@ -123,6 +128,13 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
 int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,
                     uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
                     uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg);
+/* bic_encode_gray for the planes plane0 .. plane0 + nplanes - 1 of the image (plane0 + nplanes <= 8):
+ * `planes`, the slots and bit counts hold those planes in order (plane0 first). The streams are
+ * the ones bic_encode_gray produces for the same planes: each plane has its own coders. */
+int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                          int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
+                          size_t slot_golomb, uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg,
+                          uint64_t* bits_eg);
 /* A slot size (64-bit words) that every plane of this geometry fits for EG (exact) and for
  * Golomb on any input this build has seen (2*rows*(cols+1) bits + 64 words); a larger input
  * still reports BIC_ENOSPC rather than writing out of bounds. */

@@ -233,3 +233,33 @@ def test_encode_gray_matches_two_calls(ctx, oracle, staged):
     for k in range(8):
         assert stream_bytes(og[k], as_u64(bg)[k]) == stream_bytes(og2[k], as_u64(bg2)[k])
         assert stream_bytes(oe[k], as_u64(be)[k]) == stream_bytes(oe2[k], as_u64(be2)[k])
+
+
+@pytest.mark.parametrize("rows,cols,pitch,plane0,nplanes,kind", [
+    (40, 4096, 4096, 1, 7, "uniform"), (33, 16384, 16384, 5, 2, "smooth"), (20, 5000, 5120, 7, 1, "smooth"),
+    (9, 300, 300, 3, 4, "uniform"),  # the two-call path (bic_bitplanes_u8_range + bic_encode_planes2)
+])
+def test_encode_gray_range(ctx, oracle, staged, rows, cols, pitch, plane0, nplanes, kind):
+    """bic_encode_gray_range (a plane-sharded rank's share): planes plane0.. of the image and their
+    streams == the oracle's for bitplane_tool's planes plane0.. (the same planes as a full call)"""
+    img = np.zeros((rows, pitch), np.uint8)
+    img[:, :cols] = _gray(oracle, rows + plane0, rows, cols, kind)
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    planes, (og, bg), (oe, be) = ctx.encode_gray(g, cols=cols, nplanes=nplanes, plane0=plane0)
+    only = ctx.bitplanes_u8(g, cols=cols, nplanes=nplanes, plane0=plane0)
+    ctx.sync()
+    exp_planes = oracle.bitplanes(np.ascontiguousarray(img[:, :cols]), 8)[plane0:plane0 + nplanes]
+    assert np.array_equal(as_u64(planes), exp_planes)
+    assert np.array_equal(as_u64(only), exp_planes)
+    for k in range(nplanes):
+        for coder, out, bits in ((0, og, bg), (1, oe, be)):
+            eb, est, _ = oracle.encode_plane(exp_planes[k], cols, 1, coder)
+            nb = int(as_u64(bits)[k])
+            assert nb == eb, (k, coder)
+            assert stream_bytes(out[k], nb) == est.tobytes(), (k, coder)
+
+
+def test_encode_gray_range_rejects(ctx):
+    g = ctx.torch.zeros((4, 64), dtype=ctx.torch.uint8, device=ctx.dev)
+    with pytest.raises(pybic.BicError):
+        ctx.encode_gray(g, nplanes=4, plane0=5)
