@@ -238,8 +238,9 @@ class C3Planes(C3):
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
         n = max(1, self.nplanes)
-        self.out_g, self.out_e = ctx.empty_i64(n, self.slot_g), ctx.empty_i64(n, self.slot_e)
+        self.out_g, self.out_e = ctx.empty_i64(n * self.slot_g), ctx.empty_i64(n * self.slot_e)  # packed
         self.bits_g, self.bits_e = ctx.empty_i64(n), ctx.empty_i64(n)
+        self.off_g, self.off_e = ctx.empty_i64(n + 1), ctx.empty_i64(n + 1)
         self.gathered = (None, None)
         ctx.reserve(n, self.rows, self.cols)
         self.k = 0
@@ -252,17 +253,16 @@ class C3Planes(C3):
     def step(self):
         from pybic.parallel import gather_streams
         c = self.ctx
-        if self.nplanes:
-            c.encode_gray(self.gray[self.k & 1], nplanes=self.nplanes, plane0=self.lo, planes=self.planes,
-                          slots=(self.slot_g, self.slot_e), outs=(self.out_g, self.out_e),
-                          bits=(self.bits_g, self.bits_e))
+        if self.nplanes:  # both streams written packed (word-aligned, plane order): the gather sends them as is
+            c.encode_gray_packed(self.gray[self.k & 1], nplanes=self.nplanes, plane0=self.lo, planes=self.planes,
+                                 slots=(self.slot_g, self.slot_e), outs=(self.out_g, self.out_e),
+                                 bits=(self.bits_g, self.bits_e), offs=(self.off_g, self.off_e))
         got = []
-        for out, bits in ((self.out_g, self.bits_g), (self.out_e, self.bits_e)):
-            packed, off = c.pack_streams(out[:self.nplanes], bits[:self.nplanes])
+        for packed, off in ((self.out_g, self.off_g), (self.out_e, self.off_e)):
             if self.world > 1:
                 got.append(gather_streams(packed, off[-1:], self.world, self.rank))
             else:
-                got.append((packed, [0, int(off[-1].item())]))
+                got.append((packed, off))  # (no host sync in the step: the check reads the total)
         self.gathered = tuple(got)
         self.k += 1
 
@@ -301,6 +301,8 @@ class C3Planes(C3):
         ok = True
         for coder in (0, 1):
             words, offs = self.gathered[coder]
+            if self.world == 1:
+                offs = [0, int(self.pybic.as_u64(offs)[-1])]
             W = self.pybic.as_u64(words)
             for r in range(self.world):
                 a, b = r * 8 // self.world, (r + 1) * 8 // self.world
@@ -385,7 +387,7 @@ class C4(C3):
         self.out_g = ctx.empty_i64(self.nplanes, self.slot_g)
         self.bits_g = ctx.empty_i64(self.nplanes)
         self.bits_e = ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
-        self.packed = ctx.empty_i64(self.nplanes * self.slot_g)
+        self.packed = ctx.empty_i64(self.nplanes * self.slot_g)  # the streams, word-aligned back to back
         self.word_off = ctx.empty_i64(self.nplanes + 1)
         self.gathered = None
         ctx.reserve(self.nplanes, self.rows, self.cols)
@@ -397,8 +399,10 @@ class C4(C3):
     def step(self):
         from pybic.parallel import gather_streams
         c, p = self.ctx, self.pybic
-        c.encode_planes(self.planes, self.cols, True, p.CODER_GOLOMB, self.slot_g, self.out_g, self.bits_g)
-        self.packed, self.word_off = c.pack_streams(self.out_g, self.bits_g)
+        # packed output: the encoder writes each frame's stream at its packed word offset (no slots, no
+        # pack kernel), ready for the gather
+        c.encode_planes_packed(self.planes, self.cols, True, golomb=True, eg=False, slots=(self.slot_g, None),
+                               outs=(self.packed, None), bits=(self.bits_g, None), offs=(self.word_off, None))
         if self.world > 1:
             self.gathered = gather_streams(self.packed, self.word_off[-1:], self.world, self.rank)
         self.k += 1
@@ -410,10 +414,16 @@ class C4(C3):
                 "encode_rows_golomb": plane_b + g}
 
     def check(self, oracle):
-        P = self.pybic.as_u64(self.planes[0])
-        eb, est, _ = oracle.encode_plane(P, self.cols, 1, 0)
-        nb = int(self.pybic.as_u64(self.bits_g)[0])
-        return nb == eb and self.pybic.stream_bytes(self.out_g[0], nb) == est.tobytes()
+        """every frame of rank 0's share: its stream at its packed offset == the oracle's"""
+        P = self.pybic.as_u64(self.planes)
+        exp = oracle.encode_planes_par(P, self.cols, 1, coders=(0,))
+        B, O, D = (self.pybic.as_u64(x) for x in (self.bits_g, self.word_off, self.packed))
+        ok = True
+        for k in range(self.nplanes):
+            eb, est = exp[(k, 0)]
+            nw = (eb + 63) // 64
+            ok &= int(B[k]) == eb and int(O[k + 1] - O[k]) == nw and D[O[k]:O[k] + nw].tobytes() == est.tobytes()
+        return bool(ok)
 
 
 class C5(C3):

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <new>
 #include <string>
@@ -383,9 +384,25 @@ size_t bic_encode_slot_words(size_t rows, size_t cols, int coder) {
   return (size_t)((2 * base + 63) / 64 + 64);
 }
 
-int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
-                       size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
-                       uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg) {
+namespace {
+// Packed output where the encoder cannot write it in place (encoders other than the staged one, the
+// multi-pass path): encode into slots in a stream-ordered temporary, then bic_pack_streams' kernel.
+int pack_after(bic_ctx* ctx, int nplanes, uint64_t* out, size_t slot, uint64_t* bits, uint64_t* off,
+               const std::function<int(uint64_t*)>& encode) {
+  uint64_t* tmp = nullptr;
+  BIC_HIP(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)nplanes * slot * 8, ctx->cur));
+  const int rc = encode(tmp);
+  if (rc == BIC_OK) timed(ctx, "pack", [&] { bic::launch_pack(ctx->cur, tmp, nplanes, slot, bits, out, off); });
+  (void)hipFreeAsync(tmp, ctx->cur);
+  BIC_HIP(hipGetLastError());
+  return rc;
+}
+}  // namespace
+
+static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                              size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                              uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg, size_t slot_eg,
+                              uint64_t* bits_eg, uint64_t* off_eg) {
   int rc = bind(ctx);
   if (rc) return rc;
   if (nplanes < 1 || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
@@ -396,6 +413,8 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
   if (rows == 0) {
     if (out_golomb) BIC_HIP(hipMemsetAsync(bits_golomb, 0, sizeof(uint64_t) * nplanes, ctx->cur));
     if (out_eg) BIC_HIP(hipMemsetAsync(bits_eg, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+    if (off_golomb) BIC_HIP(hipMemsetAsync(off_golomb, 0, sizeof(uint64_t) * (nplanes + 1), ctx->cur));
+    if (off_eg) BIC_HIP(hipMemsetAsync(off_eg, 0, sizeof(uint64_t) * (nplanes + 1), ctx->cur));
     return BIC_OK;
   }
   const int pr = predict ? 1 : 0;
@@ -409,6 +428,21 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
                      : (ctx->single_kernel || !staged_pays(ctx, g) || !bic::med_rows_supported(g, planes, nullptr))
                          ? bic::kEncSingle
                                                                                             : bic::kEncStaged;
+    if ((off_golomb || off_eg) && mode != bic::kEncStaged) {  // packed output via slots + pack
+      if (off_golomb && (rc = pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, [&](uint64_t* t) {
+            return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, t, slot_golomb, bits_golomb,
+                                      nullptr, nullptr, 0, nullptr, nullptr);
+          })))
+        return rc;
+      if (off_eg)
+        return pack_after(ctx, nplanes, out_eg, slot_eg, bits_eg, off_eg, [&](uint64_t* t) {
+          return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, nullptr, 0, nullptr, nullptr, t,
+                                    slot_eg, bits_eg, nullptr);
+        });
+      return BIC_OK;
+    }
+    fs.off_g = off_golomb;
+    fs.off_e = off_eg;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -424,6 +458,19 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
     return BIC_OK;
   }
   // rows wider than 16384 columns: multi-pass chunk kernels (bic_kernels.hip)
+  if (off_golomb || off_eg) {  // packed output via slots + pack
+    if (off_golomb && (rc = pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, [&](uint64_t* t) {
+          return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, t, slot_golomb, bits_golomb, nullptr,
+                                    nullptr, 0, nullptr, nullptr);
+        })))
+      return rc;
+    if (off_eg)
+      return pack_after(ctx, nplanes, out_eg, slot_eg, bits_eg, off_eg, [&](uint64_t* t) {
+        return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, nullptr, 0, nullptr, nullptr, t,
+                                  slot_eg, bits_eg, nullptr);
+      });
+    return BIC_OK;
+  }
   if ((rc = ensure_scratch(ctx, bic::chunk_scratch_bytes(g)))) return rc;
   const bic::ChunkScratch cs = bic::carve_chunk_scratch(ctx->scratch, g);
   timed(ctx, "med_count", [&] { bic::launch_count(ctx->cur, g, planes, pr, cs, nullptr, nullptr); });
@@ -446,10 +493,26 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
   return BIC_OK;
 }
 
-int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
-                          int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
-                          size_t slot_golomb, uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg,
-                          uint64_t* bits_eg) {
+int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                       size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                       uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg) {
+  return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
+                            nullptr, out_eg, slot_eg, bits_eg, nullptr);
+}
+
+int bic_encode_planes_packed(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                             size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                             uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg, size_t slot_eg,
+                             uint64_t* bits_eg, uint64_t* off_eg) {
+  if ((out_golomb && !off_golomb) || (out_eg && !off_eg)) return BIC_EINVAL;
+  return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
+                            off_golomb, out_eg, slot_eg, bits_eg, off_eg);
+}
+
+static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                            int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
+                            size_t slot_golomb, uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg,
+                            size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg) {
   int rc = bind(ctx);
   if (rc) return rc;
   if (plane0 < 0 || nplanes < 1 || plane0 + nplanes > 8 || pitch < cols || !geom_ok(rows, cols, wpr))
@@ -464,14 +527,16 @@ int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_
                     bic::med_rows_supported(g, planes, nullptr) && bic::gray_rows_supported(g, gray, pitch, planes);
   if (!fuse) {  // the same result through the two separate calls
     if ((rc = bic_bitplanes_u8_range(ctx, gray, pitch, rows, cols, plane0, nplanes, planes, wpr))) return rc;
-    return bic_encode_planes2(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
-                              out_eg, slot_eg, bits_eg);
+    return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
+                              off_golomb, out_eg, slot_eg, bits_eg, off_eg);
   }
   const int pr = predict ? 1 : 0;
   if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
   bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
   fs.counted = true;
   fs.ns = bic::gray_strips(g);
+  fs.off_g = off_golomb;
+  fs.off_e = off_eg;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
@@ -487,6 +552,23 @@ int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_
   timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
   BIC_HIP(hipGetLastError());
   return BIC_OK;
+}
+
+int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                          int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
+                          size_t slot_golomb, uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg,
+                          uint64_t* bits_eg) {
+  return encode_gray_impl(ctx, gray, pitch, rows, cols, plane0, nplanes, planes, wpr, predict, out_golomb, slot_golomb,
+                          bits_golomb, nullptr, out_eg, slot_eg, bits_eg, nullptr);
+}
+
+int bic_encode_gray_packed(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                           int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
+                           size_t slot_golomb, uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg,
+                           size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg) {
+  if ((out_golomb && !off_golomb) || (out_eg && !off_eg)) return BIC_EINVAL;
+  return encode_gray_impl(ctx, gray, pitch, rows, cols, plane0, nplanes, planes, wpr, predict, out_golomb, slot_golomb,
+                          bits_golomb, off_golomb, out_eg, slot_eg, bits_eg, off_eg);
 }
 
 int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,

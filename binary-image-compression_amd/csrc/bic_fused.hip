@@ -506,6 +506,13 @@ struct FusedArgs {
   uint64_t slot_e;
   uint64_t* bits_e;
   uint32_t* flags;
+  // packed output (FusedScratch::off_g / off_e): per-plane totals of residual 1s (ONES scan), the
+  // planes' packed start words (k_plane_bases) and EG start bits; ebase null: slot mode
+  uint64_t* pones;
+  uint64_t* gbase;
+  uint64_t* ebase;
+  uint64_t* off_g;
+  uint64_t* off_e;
 #ifdef BIC_STAMPS
   int known;
   int dbg;  // diagnostic (BIC_EMIT_DBG): k_emit_known skips 1 = LDS-image Golomb rows, 2 = EG rows, 4 = k = 0 copies
@@ -1241,6 +1248,7 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       if (in && pre == 0 && v[i] > 0 && !walk) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)(base + r);
       pre += v[i];
     }
+    if (b == nb - 1 && threadIdx.x == 0) a.pones[plane] = btot + tot;  // the plane's residual 1s
   } else {
     const uint64_t cap = a.slot_g * 64;
 #pragma unroll
@@ -1389,7 +1397,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
       const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
       const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
       const uint64_t cap = a.slot_e * 64;
-      const uint64_t Ge = (uint64_t)plane * cap + Ge_rel;
+      const uint64_t Ge = (a.ebase ? a.ebase[plane] : (uint64_t)plane * cap) + Ge_rel;
       if (Ge_rel + Le <= cap) {
         if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
         if (lane == 0) {
@@ -1504,8 +1512,8 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
       const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1);
       const uint64_t cap = a.slot_e * 64;
       if (Ge_rel + Le <= cap)
-        write_row(eimg, Le, (uint64_t)plane * cap + Ge_rel, (int64_t)fcol + 1, a.out_e, a.efrag + 2 * id,
-                  threadIdx.x, blockDim.x);
+        write_row(eimg, Le, (a.ebase ? a.ebase[plane] : (uint64_t)plane * cap) + Ge_rel, (int64_t)fcol + 1, a.out_e,
+                  a.efrag + 2 * id, threadIdx.x, blockDim.x);
     }
     if (gmix) {
       const uint32_t arow = row * (g.cols + 1);
@@ -1534,6 +1542,48 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
     }
     __syncthreads();  // the images and sh are reused by the next row
   }
+}
+
+// Packed output: the planes' start words in each coder's buffer (streams word-aligned, plane order:
+// bic_pack_streams' layout) from the Golomb totals (LEN scan) and the EG lengths (rows (cols + 1), + 1
+// when the plane holds a residual 1: eg.cpp's first-run bit), each capped at the slot size so that an
+// overflowing plane (BIC_ENOSPC) cannot push a later one past the buffer. One workgroup.
+__global__ __launch_bounds__(1024) void k_plane_bases(FusedArgs a) {
+  __shared__ uint64_t tmp[17];
+  const Geom& g = a.g;
+  uint64_t cg = 0, ce = 0;  // running bases (words)
+  for (uint32_t q0 = 0; q0 < g.nplanes; q0 += 1024) {
+    const uint32_t q = q0 + threadIdx.x;
+    const bool in = q < g.nplanes;
+    uint64_t gw = 0, ew = 0;
+    if (in && a.off_g) gw = min((a.bits_g[q] + 63) / 64, a.slot_g);
+    if (in && a.off_e) ew = min(((uint64_t)g.rows * (g.cols + 1) + (a.pones[q] ? 1 : 0) + 63) / 64, a.slot_e);
+    uint64_t tg, te;
+    const uint64_t pg = block_excl_scan<uint64_t>(gw, tmp, tg) + cg;
+    const uint64_t pe = block_excl_scan<uint64_t>(ew, tmp, te) + ce;
+    if (in && a.off_g) {
+      a.off_g[q] = pg;
+      a.gbase[q] = pg;
+    }
+    if (in && a.off_e) {
+      a.off_e[q] = pe;
+      a.ebase[q] = pe * 64;
+    }
+    cg += tg;
+    ce += te;
+  }
+  if (threadIdx.x == 0) {
+    if (a.off_g) a.off_g[g.nplanes] = cg;
+    if (a.off_e) a.off_e[g.nplanes] = ce;
+  }
+}
+
+// Packed Golomb output: every row's offset moves from its plane's slot to the plane's packed start.
+__global__ __launch_bounds__(256) void k_shift_gboff(FusedArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (uint64_t)a.g.rows * a.g.nplanes) return;
+  const uint32_t plane = (uint32_t)(id / a.g.rows);
+  a.gboff[id] = a.gboff[id] - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64;
 }
 
 // Combine the fragments of the words rows share: the row holding a shared word's first bit
@@ -1570,7 +1620,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024;
+  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024 + (size_t)g.nplanes * 8 * 3 + 64;
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -1596,6 +1646,13 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
   fs.row_o = fs.sones + n * kMaxStrips;
   fs.walk_ids = fs.row_o + n;
   fs.rest_ids = fs.walk_ids + n;
+  {
+    uintptr_t e = reinterpret_cast<uintptr_t>(fs.rest_ids + n);
+    e = (e + 7) & ~(uintptr_t)7;
+    fs.pones = reinterpret_cast<uint64_t*>(e);
+    fs.gbase = fs.pones + g.nplanes;
+    fs.ebase = fs.gbase + g.nplanes;
+  }
   fs.ns = 1;
   fs.counted = false;
   fs.slow_n = fs.counter + 1;  // zeroed with the counter
@@ -1624,6 +1681,11 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   FusedArgs a{g, planes, lut, fs.counter, fs.ones_rec, fs.bits_rec, fs.gboff, fs.glen, fs.gfrag, fs.gslow,
               fs.eboff, fs.elen, fs.efrag, fs.row_o, fs.sones, fs.krec, fs.kpos, fs.counted ? fs.ns : 1u, fs.walk_ids, fs.rest_ids, fs.slow_n, fs.slow_ids, out_g, slot_g, bits_g, out_e, slot_e,
               bits_e, flags};
+  a.pones = fs.pones;
+  a.gbase = fs.gbase;
+  a.off_g = out_g ? fs.off_g : nullptr;
+  a.off_e = out_e ? fs.off_e : nullptr;
+  a.ebase = a.off_e ? fs.ebase : nullptr;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
   a.dbg = getenv("BIC_EMIT_DBG") ? atoi(getenv("BIC_EMIT_DBG")) : 0;
@@ -1656,6 +1718,10 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
         if (predict) k_row_walk<true><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
         else k_row_walk<false><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
         k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);
+      }
+      if (a.off_g || a.off_e) {  // packed output: the planes' start words, then the rows' Golomb offsets
+        k_plane_bases<<<1, 1024, 0, s>>>(a);
+        if (a.off_g) k_shift_gboff<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
       }
       return;
     }

@@ -106,6 +106,12 @@ struct FusedScratch {
   bool counted;      // the count pass already ran (bic_encode_gray's fused bitplane kernel)
   uint32_t* slow_n;
   uint64_t* slow_ids;
+  // packed output (staged encoder): when off_g / off_e are set, each coder's streams are written
+  // word-aligned back to back from word 0 of its buffer (what bic_pack_streams makes of slots) and
+  // off_*[0..nplanes] receive the word offsets; pones / gbase / ebase: per-plane scratch
+  uint64_t* off_g = nullptr;
+  uint64_t* off_e = nullptr;
+  uint64_t *pones, *gbase, *ebase;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);

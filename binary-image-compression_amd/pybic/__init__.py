@@ -27,7 +27,7 @@ EXPORTS = [
     "bic_pack_streams", "bic_prof_enable", "bic_prof_collect", "bic_prof_only", "bic_enum_codelength", "bic_tile_lentab",
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
-    "bic_bitplanes_u8_range", "bic_encode_gray_range",
+    "bic_bitplanes_u8_range", "bic_encode_gray_range", "bic_encode_planes_packed", "bic_encode_gray_packed",
 ]
 
 
@@ -97,6 +97,8 @@ def load(path=LIB_PATH):
     sig("bic_encode_gray", i32, [vp, vp, sz, sz, sz, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
     sig("bic_bitplanes_u8_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz])
     sig("bic_encode_gray_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
+    sig("bic_encode_planes_packed", i32, [vp, vp, i32, sz, sz, sz, i32, vp, sz, vp, vp, vp, sz, vp, vp])
+    sig("bic_encode_gray_packed", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, vp, sz, vp, vp])
     _lib = L
     return L
 
@@ -289,6 +291,47 @@ class Context:
             self._chk(self.lib.bic_encode_gray(self.h, _p(gray), pitch, rows, cols, nplanes, _p(planes), wpr,
                                                int(predict), _p(og), sg, _p(bg), _p(oe), se, _p(be)), "bic_encode_gray")
         return planes, ((og, bg) if golomb else None), ((oe, be) if eg else None)
+
+    def encode_planes_packed(self, planes, cols, predict=True, golomb=True, eg=False, slots=(None, None),
+                             outs=(None, None), bits=(None, None), offs=(None, None)):
+        """-> ((out_g, bits_g, off_g) or None, (out_e, bits_e, off_e) or None): each coder's streams
+        packed word-aligned in plane order, off = start words + total (bic_encode_planes_packed)."""
+        planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
+        n, rows, wpr = planes.shape
+        res = self._packed_bufs(n, rows, cols, golomb, eg, slots, outs, bits, offs)
+        (og, sg, bg, fg), (oe, se, be, fe) = res
+        self._bind_stream()
+        self._chk(self.lib.bic_encode_planes_packed(self.h, _p(planes), n, rows, cols, wpr, int(predict), _p(og), sg,
+                                                    _p(bg), _p(fg), _p(oe), se, _p(be), _p(fe)),
+                  "bic_encode_planes_packed")
+        return ((og, bg, fg) if golomb else None), ((oe, be, fe) if eg else None)
+
+    def encode_gray_packed(self, gray, cols=None, nplanes=8, plane0=0, predict=True, planes=None, golomb=True,
+                           eg=True, slots=(None, None), outs=(None, None), bits=(None, None), offs=(None, None)):
+        """bic_encode_gray_packed -> (planes, (out_g, bits_g, off_g) or None, (out_e, bits_e, off_e) or None)"""
+        rows, pitch = gray.shape
+        cols = pitch if cols is None else cols
+        if planes is None:
+            planes = self.empty_i64(nplanes, rows, (cols + 63) // 64)
+        wpr = planes.shape[-1]
+        (og, sg, bg, fg), (oe, se, be, fe) = self._packed_bufs(nplanes, rows, cols, golomb, eg, slots, outs, bits, offs)
+        self._bind_stream()
+        self._chk(self.lib.bic_encode_gray_packed(self.h, _p(gray), pitch, rows, cols, plane0, nplanes, _p(planes), wpr,
+                                                  int(predict), _p(og), sg, _p(bg), _p(fg), _p(oe), se, _p(be),
+                                                  _p(fe)), "bic_encode_gray_packed")
+        return planes, ((og, bg, fg) if golomb else None), ((oe, be, fe) if eg else None)
+
+    def _packed_bufs(self, n, rows, cols, golomb, eg, slots, outs, bits, offs):
+        res = []
+        for i, (on, coder) in enumerate(((golomb, CODER_GOLOMB), (eg, CODER_EG))):
+            if not on:
+                res.append((None, 0, None, None))
+                continue
+            slot = slots[i] or self.slot_words(rows, cols, coder)
+            res.append((self.empty_i64(n * slot) if outs[i] is None else outs[i], slot,
+                        self.empty_i64(n) if bits[i] is None else bits[i],
+                        self.empty_i64(n + 1) if offs[i] is None else offs[i]))
+        return res
 
     def set_encoder(self, name):
         """row encoder for rows <= 16384 columns: "auto" (default: staged from 32768 rows on, the

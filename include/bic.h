@@ -135,6 +135,20 @@ int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_
                           int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
                           size_t slot_golomb, uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg,
                           uint64_t* bits_eg);
+/* Packed output (what bic_pack_streams makes of the slots, without the copy): each coder's streams
+ * are written word-aligned back to back from word 0 of out_golomb / out_eg (capacity nplanes *
+ * slot words each, as for the slots), and off_golomb / off_eg (device, nplanes + 1 u64) receive
+ * every plane's start word and the total. The multi-GPU gather sends these buffers as they are.
+ * The staged encoder writes the packed positions directly; the other encoders go through slots
+ * in a temporary and the pack kernel. off_* must be given for every coder that is written. */
+int bic_encode_planes_packed(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
+                             size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
+                             uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg, size_t slot_eg,
+                             uint64_t* bits_eg, uint64_t* off_eg);
+int bic_encode_gray_packed(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
+                           int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
+                           size_t slot_golomb, uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg,
+                           size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg);
 /* A slot size (64-bit words) that every plane of this geometry fits for EG (exact) and for
  * Golomb on any input this build has seen (2*rows*(cols+1) bits + 64 words); a larger input
  * still reports BIC_ENOSPC rather than writing out of bounds. */

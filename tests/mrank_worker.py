@@ -2,10 +2,10 @@
 one GPU of the box, talk over gloo (host tensors; RCCL needs one GPU per rank), and run the real
 sharded chains through libbic.so -- the same code bench.py runs at N GPUs over RCCL:
 
-  frames  C4: frames split over the ranks -> med + Golomb (bic_encode_planes) -> bic_pack_streams
-          -> gather_streams to rank 0
-  planes  C3: the 8 planes of one gray image split over the ranks -> bic_encode_gray_range (Golomb
-          and EG) -> bic_pack_streams -> gather_streams
+  frames  C4: frames split over the ranks -> med + Golomb, written packed by the encoder
+          (bic_encode_planes_packed; odd ranks: slots + bic_pack_streams) -> gather_streams to rank 0
+  planes  C3: the 8 planes of one gray image split over the ranks -> bic_encode_gray_packed (planes
+          plane0.., Golomb and EG written packed) -> gather_streams
   tiles   C5: bands of tile rows -> bic_patch_encode per band -> one adaptive Golomb coder over the
           whole tile sequence continued across ranks (sharded_golomb + bic_golomb_encode_samples)
 
@@ -62,8 +62,11 @@ def frames(ctx, oracle, world, rank):
     F, rows, cols = 6, 130, 640
     P = np.stack([oracle.gen_plane(0x5EED0000 + k, (0.5, 0.2, 0.05)[k % 3], rows, cols) for k in range(F)])
     lo, hi = share(F, world, rank)
-    out, bits = ctx.encode_planes(ctx.to_dev(P[lo:hi]), cols, True, CODER_GOLOMB)
-    packed, off = ctx.pack_streams(out, bits)
+    if rank % 2:  # slots + bic_pack_streams on odd ranks, the encoder's packed output on even ones
+        out, bits = ctx.encode_planes(ctx.to_dev(P[lo:hi]), cols, True, CODER_GOLOMB)
+        packed, off = ctx.pack_streams(out, bits)
+    else:
+        (packed, bits, off), _ = ctx.encode_planes_packed(ctx.to_dev(P[lo:hi]), cols, True, golomb=True, eg=False)
     allbits = gather_bits(bits, F, world, rank)
     words, offs = gather_streams(packed, off[-1:], world, rank)
     if rank:
@@ -87,10 +90,9 @@ def planes(ctx, oracle, world, rank):
     img = gray_image(oracle, rows, cols)
     g = torch.from_numpy(img).to(ctx.dev)
     lo, hi = share(8, world, rank)
-    _, (og, bg), (oe, be) = ctx.encode_gray(g, nplanes=hi - lo, plane0=lo)
+    _, (og, bg, fg), (oe, be, fe) = ctx.encode_gray_packed(g, nplanes=hi - lo, plane0=lo)
     res = {}
-    for coder, out, bits in ((0, og, bg), (1, oe, be)):
-        packed, off = ctx.pack_streams(out, bits)
+    for coder, packed, bits, off in ((0, og, bg, fg), (1, oe, be, fe)):
         allbits = gather_bits(bits, 8, world, rank)
         words, offs = gather_streams(packed, off[-1:], world, rank)
         res[coder] = (allbits, words, offs)

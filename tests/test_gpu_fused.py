@@ -263,3 +263,47 @@ def test_encode_gray_range_rejects(ctx):
     g = ctx.torch.zeros((4, 64), dtype=ctx.torch.uint8, device=ctx.dev)
     with pytest.raises(pybic.BicError):
         ctx.encode_gray(g, nplanes=4, plane0=5)
+
+
+def _packed_expect(oracle, P, cols, pred, coder):
+    """the packed buffer bic_pack_streams makes of the oracle's streams, and the word offsets"""
+    words, offs = [], [0]
+    for k in range(P.shape[0]):
+        eb, est, _ = oracle.encode_plane(P[k], cols, pred, coder)
+        words.append(est.tobytes())
+        offs.append(offs[-1] + (eb + 63) // 64)
+    return b"".join(words), offs
+
+
+@pytest.mark.parametrize("encoder_name", ["staged", "single-kernel", "two-pass", "multipass"])
+@pytest.mark.parametrize("n,rows,cols,p", [(5, 40, 1000, 0.3), (3, 17, 16384, 0.5), (4, 9, 130, 0.02)])
+def test_encode_planes_packed(ctx, oracle, encoder_name, n, rows, cols, p):
+    """bic_encode_planes_packed == each plane's oracle stream, word-aligned back to back"""
+    P = np.stack([oracle.gen_plane(0x5EED + 31 * k + rows, (p, 0.5, 0.05)[k % 3], rows, cols) for k in range(n)])
+    ctx.set_encoder(encoder_name)
+    try:
+        for pred in (1, 0):
+            (og, bg, fg), (oe, be, fe) = ctx.encode_planes_packed(ctx.to_dev(P), cols, pred, golomb=True, eg=True)
+            ctx.sync()
+            for coder, out, off in ((0, og, fg), (1, oe, fe)):
+                exp, eoff = _packed_expect(oracle, P, cols, pred, coder)
+                O = as_u64(off)
+                assert list(O) == eoff, (pred, coder)
+                assert as_u64(out)[:eoff[-1]].tobytes() == exp, (pred, coder)
+    finally:
+        ctx.set_encoder("auto")
+
+
+@pytest.mark.parametrize("plane0,nplanes", [(0, 8), (2, 3)])
+def test_encode_gray_packed(ctx, oracle, staged, plane0, nplanes):
+    rows, cols = 45, 4096
+    img = _gray(oracle, 11 + plane0, rows, cols, "smooth")
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    planes, (og, bg, fg), (oe, be, fe) = ctx.encode_gray_packed(g, nplanes=nplanes, plane0=plane0)
+    ctx.sync()
+    P = oracle.bitplanes(img, 8)[plane0:plane0 + nplanes]
+    assert np.array_equal(as_u64(planes), P)
+    for coder, out, off in ((0, og, fg), (1, oe, fe)):
+        exp, eoff = _packed_expect(oracle, P, cols, 1, coder)
+        assert list(as_u64(off)) == eoff
+        assert as_u64(out)[:eoff[-1]].tobytes() == exp
