@@ -163,6 +163,7 @@ const char* bic_strerror(int code) {
     case BIC_EDEVICE: return "HIP runtime error";
     case BIC_ENOSPC: return "output slot too small";
     case BIC_ENODEV: return "no gfx950 device";
+    case BIC_EDATA: return "malformed stream";
     default: return "unknown error";
   }
 }
@@ -253,6 +254,7 @@ int bic_sync(bic_ctx* ctx) {
   if (f[0] || f[1] || f[2] || f[3]) BIC_HIP(hipMemset(ctx->flags, 0, sizeof(f)));
   if (f[2]) return BIC_EDEVICE;  // a look-back record never arrived (should not happen)
   if (f[3]) return BIC_EDEVICE;  // the row encoder's length pass disagreed with its emission (a bug)
+  if (f[1] & 2u) return BIC_EDATA;  // a decoder met a malformed stream
   if (f[1]) return BIC_EINVAL;
   if (f[0]) return BIC_ENOSPC;
   return BIC_OK;
@@ -402,7 +404,7 @@ int pack_after(bic_ctx* ctx, int nplanes, uint64_t* out, size_t slot, uint64_t* 
 static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
                               size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
                               uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg, size_t slot_eg,
-                              uint64_t* bits_eg, uint64_t* off_eg) {
+                              uint64_t* bits_eg, uint64_t* off_eg, uint64_t* row_index = nullptr) {
   int rc = bind(ctx);
   if (rc) return rc;
   if (nplanes < 1 || !geom_ok(rows, cols, wpr)) return BIC_EINVAL;
@@ -428,6 +430,12 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
                      : (ctx->single_kernel || !staged_pays(ctx, g) || !bic::med_rows_supported(g, planes, nullptr))
                          ? bic::kEncSingle
                                                                                             : bic::kEncStaged;
+    if (row_index && (mode != bic::kEncStaged || !out_golomb)) {  // the index from the staged prefix kernels
+      if ((rc = encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb,
+                                   bits_golomb, off_golomb, out_eg, slot_eg, bits_eg, off_eg)))
+        return rc;
+      return bic_row_index(ctx, planes, nplanes, rows, cols, wpr, predict, row_index);
+    }
     if ((off_golomb || off_eg) && mode != bic::kEncStaged) {  // packed output via slots + pack
       if (off_golomb && (rc = pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, [&](uint64_t* t) {
             return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, t, slot_golomb, bits_golomb,
@@ -443,6 +451,7 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     }
     fs.off_g = off_golomb;
     fs.off_e = off_eg;
+    fs.index = row_index;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -458,6 +467,7 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     return BIC_OK;
   }
   // rows wider than 16384 columns: multi-pass chunk kernels (bic_kernels.hip)
+  if (row_index) return BIC_EINVAL;  // (the decoders take rows of up to 16384 columns)
   if (off_golomb || off_eg) {  // packed output via slots + pack
     if (off_golomb && (rc = pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, [&](uint64_t* t) {
           return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, t, slot_golomb, bits_golomb, nullptr,
@@ -503,16 +513,16 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
 int bic_encode_planes_packed(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
                              size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
                              uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg, size_t slot_eg,
-                             uint64_t* bits_eg, uint64_t* off_eg) {
+                             uint64_t* bits_eg, uint64_t* off_eg, uint64_t* row_index) {
   if ((out_golomb && !off_golomb) || (out_eg && !off_eg)) return BIC_EINVAL;
   return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
-                            off_golomb, out_eg, slot_eg, bits_eg, off_eg);
+                            off_golomb, out_eg, slot_eg, bits_eg, off_eg, row_index);
 }
 
 static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
                             int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
                             size_t slot_golomb, uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg,
-                            size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg) {
+                            size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg, uint64_t* row_index = nullptr) {
   int rc = bind(ctx);
   if (rc) return rc;
   if (plane0 < 0 || nplanes < 1 || plane0 + nplanes > 8 || pitch < cols || !geom_ok(rows, cols, wpr))
@@ -528,7 +538,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   if (!fuse) {  // the same result through the two separate calls
     if ((rc = bic_bitplanes_u8_range(ctx, gray, pitch, rows, cols, plane0, nplanes, planes, wpr))) return rc;
     return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
-                              off_golomb, out_eg, slot_eg, bits_eg, off_eg);
+                              off_golomb, out_eg, slot_eg, bits_eg, off_eg, row_index);
   }
   const int pr = predict ? 1 : 0;
   if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
@@ -537,6 +547,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   fs.ns = bic::gray_strips(g);
   fs.off_g = off_golomb;
   fs.off_e = off_eg;
+  fs.index = out_golomb ? row_index : nullptr;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
@@ -551,6 +562,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
         [&] { stage(bic::kFusedRows); });
   timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
   BIC_HIP(hipGetLastError());
+  if (row_index && !out_golomb) return bic_row_index(ctx, planes, nplanes, rows, cols, wpr, predict, row_index);
   return BIC_OK;
 }
 
@@ -565,10 +577,66 @@ int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_
 int bic_encode_gray_packed(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
                            int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
                            size_t slot_golomb, uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg,
-                           size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg) {
+                           size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg, uint64_t* row_index) {
   if ((out_golomb && !off_golomb) || (out_eg && !off_eg)) return BIC_EINVAL;
   return encode_gray_impl(ctx, gray, pitch, rows, cols, plane0, nplanes, planes, wpr, predict, out_golomb, slot_golomb,
-                          bits_golomb, off_golomb, out_eg, slot_eg, bits_eg, off_eg);
+                          bits_golomb, off_golomb, out_eg, slot_eg, bits_eg, off_eg, row_index);
+}
+
+int bic_row_index(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
+                  int predict, uint64_t* index) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (nplanes < 1 || !geom_ok(rows, cols, wpr) || (rows && (!planes || !index))) return BIC_EINVAL;
+  if (rows == 0) return BIC_OK;
+  const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
+  if (!bic::fused_supported(g)) return BIC_EINVAL;
+  if (!bic::med_rows_supported(g, planes, nullptr)) {
+    // the count kernel reads 16-byte pairs of words: an even-pitched, aligned copy of the planes
+    const size_t wpr2 = (wpr + 1) & ~(size_t)1;
+    uint64_t* tmp = nullptr;
+    BIC_HIP(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)nplanes * rows * wpr2 * 8, ctx->cur));
+    rc = BIC_OK;
+    if (hipMemcpy2DAsync(tmp, wpr2 * 8, planes, wpr * 8, wpr * 8, (size_t)nplanes * rows, hipMemcpyDeviceToDevice,
+                         ctx->cur) != hipSuccess)
+      rc = BIC_EDEVICE;
+    if (rc == BIC_OK) rc = bic_row_index(ctx, tmp, nplanes, rows, cols, wpr2, predict, index);
+    (void)hipFreeAsync(tmp, ctx->cur);
+    return rc;
+  }
+  if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
+  bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
+  fs.index = index;
+  const size_t slot = bic_encode_slot_words(rows, cols, BIC_CODER_GOLOMB);
+  // the staged encoder's prefix kernels alone (counts, scans, the walk of mixed-k rows, the
+  // length scan): they touch no output words, only the scratch, the per-plane totals (gbase) and
+  // the index; `index` stands in for the Golomb output, which they never write
+  timed(ctx, "row_index", [&] {
+    bic::launch_fused(ctx->cur, g, planes, ctx->lut, predict ? 1 : 0, fs, index, slot, fs.gbase, nullptr, 0, nullptr,
+                      ctx->flags, bic::kEncStaged, bic::kFusedPrefix);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_decode_planes(bic_ctx* ctx, int coder, const uint64_t* streams, size_t slot_words, const uint64_t* word_off,
+                      const uint64_t* plane_bits, const uint64_t* index, int nplanes, size_t rows, size_t cols,
+                      size_t wpr, int predict, const uint8_t* p00, uint64_t* planes) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (coder != BIC_CODER_GOLOMB && coder != BIC_CODER_EG) return BIC_EINVAL;
+  if (nplanes < 1 || !geom_ok(rows, cols, wpr) || !bic::decode_supported((uint32_t)cols)) return BIC_EINVAL;
+  if (rows == 0) return BIC_OK;
+  if (!streams || !plane_bits || !planes || (slot_words == 0 && !word_off)) return BIC_EINVAL;
+  if (coder == BIC_CODER_GOLOMB && !index) return BIC_EINVAL;
+  if ((rc = ensure_scratch(ctx, bic::decode_scratch_bytes((uint32_t)rows, (uint32_t)wpr, (uint32_t)nplanes)))) return rc;
+  timed(ctx, "decode", [&] {
+    bic::launch_decode(ctx->cur, coder == BIC_CODER_GOLOMB ? 0 : 1, streams, slot_words, word_off, plane_bits, index,
+                       p00, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, (uint32_t)nplanes, predict ? 1 : 0, planes,
+                       ctx->scratch, ctx->flags);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
 }
 
 int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,

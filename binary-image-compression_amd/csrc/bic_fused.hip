@@ -513,6 +513,7 @@ struct FusedArgs {
   uint64_t* ebase;
   uint64_t* off_g;
   uint64_t* off_e;
+  uint64_t* index;  // FusedScratch::index
 #ifdef BIC_STAMPS
   int known;
   int dbg;  // diagnostic (BIC_EMIT_DBG): k_emit_known skips 1 = LDS-image Golomb rows, 2 = EG rows, 4 = k = 0 copies
@@ -1578,6 +1579,16 @@ __global__ __launch_bounds__(1024) void k_plane_bases(FusedArgs a) {
   }
 }
 
+// The decoders' row index (bic_row_index): [2 id] = the row's Golomb bit offset in its plane's stream
+// (before the packed-output shift), [2 id + 1] = the plane's residual 1s before the row.
+__global__ __launch_bounds__(256) void k_row_index(FusedArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (uint64_t)a.g.rows * a.g.nplanes) return;
+  const uint32_t plane = (uint32_t)(id / a.g.rows);
+  a.index[2 * id] = a.gboff[id] - (uint64_t)plane * a.slot_g * 64;
+  a.index[2 * id + 1] = a.row_o[id];
+}
+
 // Packed Golomb output: every row's offset moves from its plane's slot to the plane's packed start.
 __global__ __launch_bounds__(256) void k_shift_gboff(FusedArgs a) {
   const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1686,6 +1697,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   a.off_g = out_g ? fs.off_g : nullptr;
   a.off_e = out_e ? fs.off_e : nullptr;
   a.ebase = a.off_e ? fs.ebase : nullptr;
+  a.index = out_g ? fs.index : nullptr;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
   a.dbg = getenv("BIC_EMIT_DBG") ? atoi(getenv("BIC_EMIT_DBG")) : 0;
@@ -1718,6 +1730,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
         if (predict) k_row_walk<true><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
         else k_row_walk<false><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
         k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);
+        if (a.index) k_row_index<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
       }
       if (a.off_g || a.off_e) {  // packed output: the planes' start words, then the rows' Golomb offsets
         k_plane_bases<<<1, 1024, 0, s>>>(a);

@@ -51,6 +51,13 @@ void launch_scan_rows(hipStream_t s, const Geom& g, const ChunkScratch& cs);
 // bic_med_residual for rows of <= 256 words: RPW rows per wave, 16-byte loads; part = one u32 per
 // wave (scratch, ceil(rows/8) per plane)
 bool med_rows_supported(const Geom& g, const void* planes, const void* resid);
+// f1 decoders (bic_decode.hip)
+bool decode_supported(uint32_t cols);
+size_t decode_scratch_bytes(uint32_t rows, uint32_t wpr, uint32_t nplanes);
+void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t slot, const uint64_t* word_off,
+                   const uint64_t* plane_bits, const uint64_t* index, const uint8_t* p00, uint32_t rows,
+                   uint32_t cols, uint32_t wpr, uint32_t nplanes, int predict, uint64_t* out, void* scratch,
+                   uint32_t* flags);
 void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,
                      uint32_t* part, uint64_t* weight_out);
 void launch_golomb_bits(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
@@ -112,6 +119,9 @@ struct FusedScratch {
   uint64_t* off_g = nullptr;
   uint64_t* off_e = nullptr;
   uint64_t *pones, *gbase, *ebase;
+  // row index for the decoders (bic_row_index): per row, the bit offset of its first Golomb
+  // codeword in its plane's stream and the residual 1s of the plane before it; null: not written
+  uint64_t* index = nullptr;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);

@@ -15,7 +15,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("BIC_LIB_PATH") or os.path.join(PKG, "lib", "libbic.so")
 
-BIC_OK, BIC_EINVAL, BIC_ENOMEM, BIC_EDEVICE, BIC_ENOSPC, BIC_ENODEV = range(6)
+BIC_OK, BIC_EINVAL, BIC_ENOMEM, BIC_EDEVICE, BIC_ENOSPC, BIC_ENODEV, BIC_EDATA = range(7)
 CODER_GOLOMB, CODER_EG = 0, 1
 
 # every symbol include/bic.h declares (tests check the library exports all of them)
@@ -28,6 +28,7 @@ EXPORTS = [
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
     "bic_bitplanes_u8_range", "bic_encode_gray_range", "bic_encode_planes_packed", "bic_encode_gray_packed",
+    "bic_row_index", "bic_decode_planes",
 ]
 
 
@@ -97,8 +98,10 @@ def load(path=LIB_PATH):
     sig("bic_encode_gray", i32, [vp, vp, sz, sz, sz, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
     sig("bic_bitplanes_u8_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz])
     sig("bic_encode_gray_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
-    sig("bic_encode_planes_packed", i32, [vp, vp, i32, sz, sz, sz, i32, vp, sz, vp, vp, vp, sz, vp, vp])
-    sig("bic_encode_gray_packed", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, vp, sz, vp, vp])
+    sig("bic_encode_planes_packed", i32, [vp, vp, i32, sz, sz, sz, i32, vp, sz, vp, vp, vp, sz, vp, vp, vp])
+    sig("bic_encode_gray_packed", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, vp, sz, vp, vp, vp])
+    sig("bic_row_index", i32, [vp, vp, i32, sz, sz, sz, i32, vp])
+    sig("bic_decode_planes", i32, [vp, i32, vp, sz, vp, vp, vp, i32, sz, sz, sz, i32, vp, vp])
     _lib = L
     return L
 
@@ -293,7 +296,7 @@ class Context:
         return planes, ((og, bg) if golomb else None), ((oe, be) if eg else None)
 
     def encode_planes_packed(self, planes, cols, predict=True, golomb=True, eg=False, slots=(None, None),
-                             outs=(None, None), bits=(None, None), offs=(None, None)):
+                             outs=(None, None), bits=(None, None), offs=(None, None), row_index=None):
         """-> ((out_g, bits_g, off_g) or None, (out_e, bits_e, off_e) or None): each coder's streams
         packed word-aligned in plane order, off = start words + total (bic_encode_planes_packed)."""
         planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
@@ -302,12 +305,13 @@ class Context:
         (og, sg, bg, fg), (oe, se, be, fe) = res
         self._bind_stream()
         self._chk(self.lib.bic_encode_planes_packed(self.h, _p(planes), n, rows, cols, wpr, int(predict), _p(og), sg,
-                                                    _p(bg), _p(fg), _p(oe), se, _p(be), _p(fe)),
+                                                    _p(bg), _p(fg), _p(oe), se, _p(be), _p(fe), _p(row_index)),
                   "bic_encode_planes_packed")
         return ((og, bg, fg) if golomb else None), ((oe, be, fe) if eg else None)
 
     def encode_gray_packed(self, gray, cols=None, nplanes=8, plane0=0, predict=True, planes=None, golomb=True,
-                           eg=True, slots=(None, None), outs=(None, None), bits=(None, None), offs=(None, None)):
+                           eg=True, slots=(None, None), outs=(None, None), bits=(None, None), offs=(None, None),
+                           row_index=None):
         """bic_encode_gray_packed -> (planes, (out_g, bits_g, off_g) or None, (out_e, bits_e, off_e) or None)"""
         rows, pitch = gray.shape
         cols = pitch if cols is None else cols
@@ -318,8 +322,30 @@ class Context:
         self._bind_stream()
         self._chk(self.lib.bic_encode_gray_packed(self.h, _p(gray), pitch, rows, cols, plane0, nplanes, _p(planes), wpr,
                                                   int(predict), _p(og), sg, _p(bg), _p(fg), _p(oe), se, _p(be),
-                                                  _p(fe)), "bic_encode_gray_packed")
+                                                  _p(fe), _p(row_index)), "bic_encode_gray_packed")
         return planes, ((og, bg, fg) if golomb else None), ((oe, be, fe) if eg else None)
+
+    def row_index(self, planes, cols, predict=True, out=None):
+        """bic_row_index: int64 [nplanes * rows * 2] (per row: Golomb bit offset, residual 1s before)"""
+        planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
+        n, rows, wpr = planes.shape
+        out = self.empty_i64(n * rows * 2) if out is None else out
+        self._bind_stream()
+        self._chk(self.lib.bic_row_index(self.h, _p(planes), n, rows, cols, wpr, int(predict), _p(out)), "bic_row_index")
+        return out
+
+    def decode_planes(self, coder, streams, plane_bits, nplanes, rows, cols, predict=True, word_off=None,
+                      row_index=None, p00=None, out=None, wpr=None):
+        """bic_decode_planes: streams int64 [nplanes, slot] (slots) or [words] with word_off (packed)
+        -> planes int64 [nplanes, rows, wpr]. p00: uint8 device tensor [nplanes] or None."""
+        wpr = wpr or (cols + 63) // 64
+        out = self.empty_i64(nplanes, rows, wpr) if out is None else out
+        slot = streams.shape[-1] if (word_off is None and streams.dim() == 2) else 0
+        self._bind_stream()
+        self._chk(self.lib.bic_decode_planes(self.h, coder, _p(streams), slot, _p(word_off), _p(plane_bits),
+                                             _p(row_index), nplanes, rows, cols, wpr, int(predict), _p(p00), _p(out)),
+                  "bic_decode_planes")
+        return out
 
     def _packed_bufs(self, n, rows, cols, golomb, eg, slots, outs, bits, offs):
         res = []

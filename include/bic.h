@@ -37,6 +37,7 @@ extern "C" {
 #define BIC_EDEVICE 3  /* HIP runtime error */
 #define BIC_ENOSPC 4   /* an output slot was too small (reported by bic_sync) */
 #define BIC_ENODEV 5   /* no usable gfx950 device */
+#define BIC_EDATA 6    /* a decoder met a malformed stream (reported by bic_sync) */
 
 #define BIC_CODER_GOLOMB 0 /* GolombCoder::codeSample over the run samples (GolombCoder.cpp:29-34) */
 #define BIC_CODER_EG 1     /* EGCoder::codeRun as written: incBlockSize disabled (eg.cpp:20-37) */
@@ -144,11 +145,30 @@ int bic_encode_gray_range(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_
 int bic_encode_planes_packed(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols,
                              size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
                              uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg, size_t slot_eg,
-                             uint64_t* bits_eg, uint64_t* off_eg);
+                             uint64_t* bits_eg, uint64_t* off_eg, uint64_t* row_index);
 int bic_encode_gray_packed(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int plane0,
                            int nplanes, uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb,
                            size_t slot_golomb, uint64_t* bits_golomb, uint64_t* off_golomb, uint64_t* out_eg,
-                           size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg);
+                           size_t slot_eg, uint64_t* bits_eg, uint64_t* off_eg, uint64_t* row_index);
+
+/* ---- f1: decoders on the device (GolombDecoder.cpp:15-23 read order, eg.cpp:20-37 as written) --
+ * row_index (device, nplanes * rows * 2 u64; nullable in the encoders above): per row of each plane,
+ * [2 (p rows + r)] = the bit offset of the row's first Golomb codeword in plane p's stream and
+ * [2 (p rows + r) + 1] = the residual 1s of plane p before row r (the coder state at the row start:
+ * N = ones + r, A = r cols - ones, Golomb.h:21-24). The staged encoder writes it from its scans;
+ * bic_row_index computes it from planes (the encoder's prefix kernels alone; cols <= 16384, planes
+ * 16-byte aligned). */
+int bic_row_index(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
+                  int predict, uint64_t* index);
+/* streams -> planes (device): slot_words > 0: plane p's stream at streams + p * slot_words;
+ * slot_words == 0: packed, at streams + word_off[p]. plane_bits: each stream's length. Golomb needs
+ * row_index (rows decode independently); EG finds the row of the plane's first 1 itself. predict:
+ * the streams code the med residual; P(0, 0), which med discards, comes from p00 (device, one byte
+ * per plane; nullable: 0). cols <= 16384. A malformed stream (bad codeword, wrong length, missing
+ * end-of-row bit) is reported by bic_sync as BIC_EDATA; the planes are then undefined. */
+int bic_decode_planes(bic_ctx* ctx, int coder, const uint64_t* streams, size_t slot_words, const uint64_t* word_off,
+                      const uint64_t* plane_bits, const uint64_t* row_index, int nplanes, size_t rows, size_t cols,
+                      size_t wpr, int predict, const uint8_t* p00, uint64_t* planes);
 /* A slot size (64-bit words) that every plane of this geometry fits for EG (exact) and for
  * Golomb on any input this build has seen (2*rows*(cols+1) bits + 64 words); a larger input
  * still reports BIC_ENOSPC rather than writing out of bounds. */

@@ -275,6 +275,33 @@ int64_t bo_encode_plane(const uint64_t* plane, size_t rows, size_t cols, size_t 
     return (int64_t)bw.pos;
 }
 
+/* bo_scan_runs with the coder state recorded at every row start (GolombCoder.cpp:29-34 lengths) */
+void bo_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, int predict, uint64_t* index) {
+    const uint64_t* src = plane;
+    uint64_t* R = NULL;
+    if (predict) {
+        R = (uint64_t*)malloc(sizeof(uint64_t) * rows * wpr + 8);
+        bo_med(plane, R, rows, cols, wpr);
+        src = R;
+    }
+    bo_golomb g;
+    bo_golomb_init(&g);
+    uint64_t ones = 0;
+    for (size_t i = 0; i < rows; ++i) {
+        index[2 * i] = (uint64_t)g.bitcount;
+        index[2 * i + 1] = ones;
+        long last = -1;
+        for (size_t j = 0; j < cols; ++j)
+            if (bo_get(src, wpr, i, j)) {
+                bo_golomb_code(&g, (uint32_t)((long)j - last - 1), NULL);
+                last = (long)j;
+                ++ones;
+            }
+        bo_golomb_code(&g, (uint32_t)((long)cols - 1 - last), NULL);
+    }
+    free(R);
+}
+
 size_t bo_plane_runs(const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
                      uint32_t* runs, uint8_t* eols, size_t cap) {
     size_t n = 0;

@@ -122,6 +122,9 @@ int64_t bo_golomb_samples(const uint32_t* s, size_t n, uint8_t* out, size_t cap_
  * from `corner` (the one bit med discards). Returns 0 on success. */
 int bo_decode_plane_golomb(const uint8_t* stream, uint64_t nbits, size_t rows, size_t cols,
                            size_t wpr, int predict, int corner, uint64_t* plane);
+/* The decoders' row index (bic.h bic_row_index): per row, the Golomb stream's bit offset of
+ * the row's first codeword and the residual 1s of the plane before the row. */
+void bo_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, int predict, uint64_t* index);
 /* inverse med with P(0,0) = corner */
 void bo_unmed(const uint64_t* R, uint64_t* P, size_t rows, size_t cols, size_t wpr, int corner);
 

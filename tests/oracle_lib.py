@@ -43,6 +43,7 @@ class Oracle:
         _sig(L, "bo_golomb_samples", C.c_int64, [u32p, sz, u8p, sz, u32p, u32p])
         _sig(L, "bo_decode_plane_golomb", C.c_int, [u8p, C.c_uint64, sz, sz, sz, C.c_int, C.c_int, u64p])
         _sig(L, "bo_unmed", None, [u64p, u64p, sz, sz, sz, C.c_int])
+        _sig(L, "bo_row_index", None, [u64p, sz, sz, sz, C.c_int, u64p])
         _sig(L, "bo_get_submatrix", None, [u64p, sz, sz, sz, sz, sz, sz, sz, u64p, sz])
         _sig(L, "bo_set_submatrix", None, [u64p, sz, sz, sz, sz, sz, u64p, sz, sz, sz])
         _sig(L, "bo_enumL", C.c_double, [C.c_uint, C.c_uint])
@@ -133,6 +134,14 @@ class Oracle:
         stream = np.ascontiguousarray(stream, np.uint8)
         rc = self.lib.bo_decode_plane_golomb(ptr(stream, u8p), nbits, rows, cols, wpr, predict, corner, ptr(P, u64p))
         return rc, P
+
+    def row_index(self, P, cols, predict):
+        """per row: (Golomb bit offset of its first codeword, residual 1s before it), flat u64"""
+        P = np.ascontiguousarray(P)
+        rows, wpr = P.shape
+        out = np.zeros(2 * rows, np.uint64)
+        self.lib.bo_row_index(ptr(P, u64p), rows, cols, wpr, predict, ptr(out, u64p))
+        return out
 
     def get_submatrix(self, I, cols, i0, i1, j0, j1):
         I = np.ascontiguousarray(I)
@@ -284,6 +293,14 @@ class Ref:
         bits = np.zeros(len(lens), np.uint32)
         b = self.lib.ref_eg(ptr(lens, i32p), ptr(eols, u8p), len(lens), ptr(bits, u32p))
         return int(b), bits
+
+    def row_index(self, P, cols, predict):
+        """per row: (Golomb bit offset of its first codeword, residual 1s before it), flat u64"""
+        P = np.ascontiguousarray(P)
+        rows, wpr = P.shape
+        out = np.zeros(2 * rows, np.uint64)
+        self.lib.bo_row_index(ptr(P, u64p), rows, cols, wpr, predict, ptr(out, u64p))
+        return out
 
     def get_submatrix(self, I, cols, i0, i1, j0, j1):
         I = np.ascontiguousarray(I)

@@ -143,3 +143,22 @@ def test_c1_match_loop_full(ctx, oracle):
     assert bytes(res["modes"].cpu().numpy()).decode() == exp["modes"]
     assert stream_bytes(res["stream_match"], exp["bits_match"]) == exp["stream_match"].tobytes()
     assert stream_bytes(res["stream_nomatch"], exp["bits_nomatch"]) == exp["stream_nomatch"].tobytes()
+
+
+def test_c3_full_round_trip(ctx, oracle):
+    """§8 f1 at configs[2]'s size: the 8 planes of a 16384^2 gray image -> Golomb and EG streams
+    (packed, with the row index) -> decoded on the device (med inverted there) == the planes"""
+    rows = cols = 16384
+    img = _gray(oracle, 0x5EED0002, rows, cols, "smooth")
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    idx = ctx.empty_i64(8 * rows * 2)
+    planes, (og, bg, fg), (oe, be, fe) = ctx.encode_gray_packed(g, nplanes=8, row_index=idx)
+    p00 = ctx.torch.from_numpy(((img[0, 0] >> np.arange(8)) & 1).astype(np.uint8)).to(ctx.dev)
+    back = ctx.decode_planes(0, og, bg, 8, rows, cols, True, word_off=fg, row_index=idx, p00=p00)
+    ctx.sync()
+    assert ctx.torch.equal(back, planes)
+    back = ctx.decode_planes(1, oe, be, 8, rows, cols, True, word_off=fe, p00=p00, out=back)
+    ctx.sync()
+    assert ctx.torch.equal(back, planes)
+    exp_planes = oracle.bitplanes_par(img, 8)
+    assert np.array_equal(as_u64(planes), exp_planes)
