@@ -183,19 +183,26 @@ class C3:
         """The predictor + run-length pass on its own (BASELINE.json north star: >= 50 % of the HBM
         roofline for 16384x16384x8): med residual of every plane, per-row 1-counts (the run
         counts) and plane weights -- bic_med_residual without storing the residual. Reads the
-        planes once; not part of `value`."""
+        planes once; not part of `value`. Two plane buffers (the planes of the two gray images)
+        alternate, so the 256 MB Infinity Cache cannot hold the input of the next launch
+        (SURVEY.md §8 d)."""
+        alt = self.ctx.bitplanes_u8(self.gray[self.k & 1], nplanes=8)  # the other image's planes
+        bufs = [self.planes, alt]
+        self.ctx.sync()
         self.ctx.prof_enable(True)
-        for _ in range(reps):
-            self.ctx.med_residual(self.planes, self.cols, True, want_resid=False)
+        for i in range(reps):
+            self.ctx.med_residual(bufs[i & 1], self.cols, True, want_resid=False)
         self.ctx.sync()
         prof = self.ctx.prof_collect()
         self.ctx.prof_enable(False)
+        del alt, bufs
         n, ms = prof["med_count"]
         avg_s = ms / 1e3 / n
         byts = self.nplanes * self.rows * self.wpr * 8
         return {"kernel": "med_count (k_med_rows + k_plane_weight)", "algorithmic_bytes_per_launch": byts,
                 "achieved": round(byts / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(byts / avg_s / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 2)}
+                "frac": round(byts / avg_s / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 2),
+                "input": "two plane buffers (2 x 256 MiB) alternated"}
 
     def check(self, oracle):
         """every plane of the last step: the planes == the oracle's bitplanes of the gray image,
@@ -649,10 +656,28 @@ def cpu_baseline(wl, args):
         dt += t
         reps += 1
     px = reps * nplanes * rows * wl.cols
-    return {"value": px / dt / 1e6, "unit": "MPix/s", "cores": int(min(used, nplanes)), "kind": kind,
-            "sample": f"{nplanes} planes x {rows} rows x {wl.cols} cols (first {rows} rows of the bench input), "
-                      f"{'med+Golomb+EG' if do_eg else ('med+Golomb' if predict else 'Golomb')}, "
-                      f"OpenMP over planes, {reps} repetitions, {dt:.2f} s"}
+    what = 'med+Golomb+EG' if do_eg else ('med+Golomb' if predict else 'Golomb')
+    host = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    out = {"value": px / dt / 1e6, "unit": "MPix/s", "cores": int(min(used, nplanes)), "kind": kind,
+           "sample": f"{nplanes} planes x {rows} rows x {wl.cols} cols (first {rows} rows of the bench input), "
+                     f"{what}, bit counts as the reference's coders keep them (their writers are commented out), "
+                     f"OpenMP over planes (one coder per plane: at most {nplanes} threads), {reps} repetitions, "
+                     f"{dt:.2f} s",
+           "host": host}
+    # the strong CPU line (BASELINE.md plan): a word-parallel restatement (oracle/cpu_fast.c) writing the
+    # same streams as the GPU, OpenMP over planes, on the same sample
+    o = Oracle()
+    reps2, dt2, used2 = 0, 0.0, 0
+    while reps2 == 0 or (dt2 < args.cpu_seconds / 2 and reps2 < 64):
+        t0 = time.perf_counter()
+        *_, used2 = o.fast_encode(planes, wl.cols, predict, do_eg=do_eg)
+        dt2 += time.perf_counter() - t0
+        reps2 += 1
+    out["strong"] = {"value": reps2 * nplanes * rows * wl.cols / dt2 / 1e6, "unit": "MPix/s", "cores": used2,
+                     "kind": "port", "sample": f"the same sample, {what} streams written (word-parallel med, clz runs, "
+                                               f"64-bit bit writer), {reps2} repetitions, {dt2:.2f} s"}
+    return out
 
 
 def main():
@@ -723,6 +748,14 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc(args.workload, dom), "kernel": dom,
                 "algorithmic_bytes_per_launch": kb[dom], "avg_launch_us": round(avg_s * 1e6, 2)}
     pred_pass = wl.predictor_pass(max(args.steps, 5)) if hasattr(wl, "predictor_pass") and type(wl) is C3 else None
+    if pred_pass is not None and "bitplanes_count" in per_kernel:
+        # the pass that runs inside the step: bic_encode_gray's count pass (k_gray_strips: gray -> planes,
+        # med residual, per-strip run statistics), gray read + planes written, alternating images
+        us = per_kernel["bitplanes_count"]["avg_us"]
+        b = kb["bitplanes_count"]
+        pred_pass["in_step"] = {"kernel": "bitplanes_count (k_gray_strips)", "algorithmic_bytes_per_launch": b,
+                                "achieved": round(b / us / 1e3, 1), "frac": round(b / us / 1e3 / HBM_PEAK_GBS, 4),
+                                "avg_launch_us": round(us, 2)}
     if hasattr(wl, "collect"):
         wl.collect()
     ok = None

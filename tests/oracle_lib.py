@@ -44,6 +44,8 @@ class Oracle:
         _sig(L, "bo_decode_plane_golomb", C.c_int, [u8p, C.c_uint64, sz, sz, sz, C.c_int, C.c_int, u64p])
         _sig(L, "bo_unmed", None, [u64p, u64p, sz, sz, sz, C.c_int])
         _sig(L, "bo_row_index", None, [u64p, sz, sz, sz, C.c_int, u64p])
+        _sig(L, "cf_encode_planes", C.c_uint64, [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, u64p, C.c_uint64, u64p,
+                                                  C.c_uint64, u64p, u64p, C.POINTER(C.c_int)])
         _sig(L, "bo_get_submatrix", None, [u64p, sz, sz, sz, sz, sz, sz, sz, u64p, sz])
         _sig(L, "bo_set_submatrix", None, [u64p, sz, sz, sz, sz, sz, u64p, sz, sz, sz])
         _sig(L, "bo_enumL", C.c_double, [C.c_uint, C.c_uint])
@@ -134,6 +136,20 @@ class Oracle:
         stream = np.ascontiguousarray(stream, np.uint8)
         rc = self.lib.bo_decode_plane_golomb(ptr(stream, u8p), nbits, rows, cols, wpr, predict, corner, ptr(P, u64p))
         return rc, P
+
+    def fast_encode(self, planes, cols, predict, do_eg=1, want_streams=True):
+        """the word-parallel strong-CPU encoder (oracle/cpu_fast.c): (gbits, ebits, G slots, E slots, threads)"""
+        planes = np.ascontiguousarray(planes)
+        n, rows, wpr = planes.shape
+        gslot = 2 * rows * (cols + 1) // 64 + 64
+        eslot = (rows * (cols + 1) + 1 + 63) // 64 + 1
+        G = np.zeros((n, gslot), np.uint64) if want_streams else None
+        E = np.zeros((n, eslot), np.uint64) if want_streams and do_eg else None
+        gb, eb = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+        used = C.c_int(0)
+        self.lib.cf_encode_planes(ptr(planes, u64p), n, rows, cols, wpr, predict, do_eg, ptr(G, u64p), gslot,
+                                  ptr(E, u64p), eslot, ptr(gb, u64p), ptr(eb, u64p), C.byref(used))
+        return gb, eb, G, E, used.value
 
     def row_index(self, P, cols, predict):
         """per row: (Golomb bit offset of its first codeword, residual 1s before it), flat u64"""
@@ -293,6 +309,20 @@ class Ref:
         bits = np.zeros(len(lens), np.uint32)
         b = self.lib.ref_eg(ptr(lens, i32p), ptr(eols, u8p), len(lens), ptr(bits, u32p))
         return int(b), bits
+
+    def fast_encode(self, planes, cols, predict, do_eg=1, want_streams=True):
+        """the word-parallel strong-CPU encoder (oracle/cpu_fast.c): (gbits, ebits, G slots, E slots, threads)"""
+        planes = np.ascontiguousarray(planes)
+        n, rows, wpr = planes.shape
+        gslot = 2 * rows * (cols + 1) // 64 + 64
+        eslot = (rows * (cols + 1) + 1 + 63) // 64 + 1
+        G = np.zeros((n, gslot), np.uint64) if want_streams else None
+        E = np.zeros((n, eslot), np.uint64) if want_streams and do_eg else None
+        gb, eb = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+        used = C.c_int(0)
+        self.lib.cf_encode_planes(ptr(planes, u64p), n, rows, cols, wpr, predict, do_eg, ptr(G, u64p), gslot,
+                                  ptr(E, u64p), eslot, ptr(gb, u64p), ptr(eb, u64p), C.byref(used))
+        return gb, eb, G, E, used.value
 
     def row_index(self, P, cols, predict):
         """per row: (Golomb bit offset of its first codeword, residual 1s before it), flat u64"""

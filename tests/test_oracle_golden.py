@@ -121,3 +121,16 @@ def test_decode_roundtrip(oracle):
             corner = int(P[0, 0] >> np.uint64(63))
             rc, Q = oracle.decode_plane_golomb(st, b, rows, cols, pred, corner)
             assert rc == 0 and np.array_equal(P, Q)
+
+
+@pytest.mark.parametrize("rows,cols,p,pred", [(40, 1000, 0.5, 1), (17, 16384, 0.05, 1), (9, 65, 0.9, 0),
+                                              (3, 64, 0.0, 1), (25, 300, 0.3, 0)])
+def test_cpu_fast_matches_oracle(oracle, rows, cols, p, pred):
+    """bench.py's strong-CPU line (oracle/cpu_fast.c, word-parallel) writes the oracle's streams"""
+    P = np.stack([oracle.gen_plane(0x5EED + k, p if k else 0.5, rows, cols) for k in range(3)])
+    gb, eb, G, E, _ = oracle.fast_encode(P, cols, pred)
+    for k in range(3):
+        for coder, bits, S in ((0, gb, G), (1, eb, E)):
+            b, st, _ = oracle.encode_plane(P[k], cols, pred, coder)
+            assert int(bits[k]) == b, (k, coder)
+            assert S[k, :len(st) // 8].tobytes() == st.tobytes(), (k, coder)
