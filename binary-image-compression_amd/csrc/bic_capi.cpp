@@ -655,6 +655,23 @@ int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t 
   if (coder == BIC_CODER_EG)
     return bic_encode_planes2(ctx, planes, nplanes, rows, cols, wpr, predict, nullptr, 0, nullptr, out,
                               slot_words, plane_bits);
+  if (coder == BIC_CODER_EG_ADAPTIVE) {  // bic_egad.hip
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (nplanes < 1 || !geom_ok(rows, cols, wpr) || (rows && (!planes || !out || !plane_bits)) || slot_words == 0)
+      return BIC_EINVAL;
+    if (rows == 0) {
+      BIC_HIP(hipMemsetAsync(plane_bits, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+      return BIC_OK;
+    }
+    if ((rc = ensure_scratch(ctx, bic::egad_scratch_bytes((uint64_t)rows * nplanes)))) return rc;
+    timed(ctx, "encode_eg_adaptive", [&] {
+      bic::launch_egad(ctx->cur, planes, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, (uint32_t)nplanes,
+                       predict ? 1 : 0, out, slot_words, plane_bits, ctx->scratch, ctx->flags);
+    });
+    BIC_HIP(hipGetLastError());
+    return BIC_OK;
+  }
   return BIC_EINVAL;
 }
 

@@ -1628,6 +1628,13 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
   out[wt] = bswap64(v);
 }
 
+// the fixup of any row encoder that leaves its shared words as fragments (bic_egad.hip)
+void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len, const uint64_t* frag, uint64_t* out,
+                       uint32_t rows, uint64_t nrows) {
+  const uint32_t grid = (uint32_t)((nrows + 255) / 256);
+  k_fixup<<<grid, 256, 0, s>>>(boff, len, frag, out, boff, len, frag, out, rows, nrows, 0xffffffffu);
+}
+
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;

@@ -51,6 +51,10 @@ void launch_scan_rows(hipStream_t s, const Geom& g, const ChunkScratch& cs);
 // bic_med_residual for rows of <= 256 words: RPW rows per wave, 16-byte loads; part = one u32 per
 // wave (scratch, ceil(rows/8) per plane)
 bool med_rows_supported(const Geom& g, const void* planes, const void* resid);
+// a9 adaptive EG (bic_egad.hip)
+size_t egad_scratch_bytes(uint64_t nrows);
+void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t nplanes,
+                 int predict, uint64_t* out, uint64_t slot, uint64_t* bits, void* scratch, uint32_t* flags);
 // f1 decoders (bic_decode.hip)
 bool decode_supported(uint32_t cols);
 size_t decode_scratch_bytes(uint32_t rows, uint32_t wpr, uint32_t nplanes);

@@ -16,7 +16,7 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("BIC_LIB_PATH") or os.path.join(PKG, "lib", "libbic.so")
 
 BIC_OK, BIC_EINVAL, BIC_ENOMEM, BIC_EDEVICE, BIC_ENOSPC, BIC_ENODEV, BIC_EDATA = range(7)
-CODER_GOLOMB, CODER_EG = 0, 1
+CODER_GOLOMB, CODER_EG, CODER_EG_ADAPTIVE = 0, 1, 2
 
 # every symbol include/bic.h declares (tests check the library exports all of them)
 EXPORTS = [

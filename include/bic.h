@@ -41,6 +41,10 @@ extern "C" {
 
 #define BIC_CODER_GOLOMB 0 /* GolombCoder::codeSample over the run samples (GolombCoder.cpp:29-34) */
 #define BIC_CODER_EG 1     /* EGCoder::codeRun as written: incBlockSize disabled (eg.cpp:20-37) */
+/* EGCoder::codeRun as intended: incBlockSize() per full block (eg.cpp:25 uncommented) -- the JPEG-LS
+ * run mode the #if 0 decoder (eg.cpp:41-55) reads; EGLUT's index saturates at 31. bic_encode_planes
+ * only (slots as for Golomb: bic_encode_slot_words). */
+#define BIC_CODER_EG_ADAPTIVE 2
 
 typedef struct bic_ctx bic_ctx;
 

@@ -275,6 +275,20 @@ int64_t bo_encode_plane(const uint64_t* plane, size_t rows, size_t cols, size_t 
     return (int64_t)bw.pos;
 }
 
+int64_t bo_eg_runs(const int32_t* len, const uint8_t* eol, size_t n, int adaptive, uint8_t* out,
+                   size_t cap_bytes, uint32_t* bits_out) {
+    bo_bw bw;
+    bo_bw_init(&bw, out, cap_bytes);
+    bo_eg e;
+    bo_eg_init(&e, adaptive);
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t b = bo_eg_code(&e, len[i], eol[i], out ? &bw : NULL);
+        if (bits_out) bits_out[i] = b;
+    }
+    if (out && bw.overflow) return -1;
+    return (int64_t)e.bitcount;
+}
+
 /* bo_scan_runs with the coder state recorded at every row start (GolombCoder.cpp:29-34 lengths) */
 void bo_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, int predict, uint64_t* index) {
     const uint64_t* src = plane;

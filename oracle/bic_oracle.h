@@ -122,6 +122,10 @@ int64_t bo_golomb_samples(const uint32_t* s, size_t n, uint8_t* out, size_t cap_
  * from `corner` (the one bit med discards). Returns 0 on success. */
 int bo_decode_plane_golomb(const uint8_t* stream, uint64_t nbits, size_t rows, size_t cols,
                            size_t wpr, int predict, int corner, uint64_t* plane);
+/* EG over a run list (coder: 1 as written, 2 adaptive), MSB-first bits into out (nullable);
+ * per-run bits into bits_out (nullable). Returns the total bits, -1 on overflow. */
+int64_t bo_eg_runs(const int32_t* len, const uint8_t* eol, size_t n, int adaptive, uint8_t* out,
+                   size_t cap_bytes, uint32_t* bits_out);
 /* The decoders' row index (bic.h bic_row_index): per row, the Golomb stream's bit offset of
  * the row's first codeword and the residual 1s of the plane before the row. */
 void bo_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, int predict, uint64_t* index);

@@ -93,6 +93,40 @@ uint64_t ref_eg(const int32_t* len, const uint8_t* eol, size_t n, uint32_t* bits
   return e.bitcount;
 }
 
+// eg.cpp:20-37 with line 25's incBlockSize() enabled (what the #if 0 decoder, eg.cpp:41-55, reads),
+// stepped by the reference's own EG state machine (EG::incBlockSize / decBlockSize over EGLUT,
+// eg.cpp:2-18); the writes of lines 24, 29, 32-33 as an MSB-first bit string. The index is not
+// stepped past 31: there the reference's incBlockSize would read EGLUT[32], past the table.
+uint64_t ref_eg_adaptive(const int32_t* len, const uint8_t* eol, size_t n, uint32_t* bits_out, uint8_t* out,
+                         size_t cap_bytes) {
+  EGCoder e;
+  uint64_t pos = 0;
+  auto put = [&](uint32_t v, unsigned nb) {
+    for (unsigned b = nb; b-- > 0;) {
+      if (out && (pos >> 3) < cap_bytes && ((v >> b) & 1u)) out[pos >> 3] |= (uint8_t)(0x80u >> (pos & 7));
+      ++pos;
+    }
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t before = pos;
+    int l = len[i];
+    while (l >= (int)e.blockSize) {
+      l -= (int)e.blockSize;
+      put(1, 1);
+      if (e.lutIndex < 31) e.incBlockSize();
+    }
+    if (eol[i]) {
+      put(1, 1);
+    } else {
+      put(0, 1);
+      put((uint32_t)l, e.g);
+      e.decBlockSize();
+    }
+    if (bits_out) bits_out[i] = (uint32_t)(pos - before);
+  }
+  return pos;
+}
+
 int ref_get_submatrix(const uint64_t* I, size_t rows, size_t cols, size_t wpr, size_t i0,
                       size_t i1, size_t j0, size_t j1, uint64_t* B, size_t bwpr) {
   binary_matrix A = from_words(I, rows, cols, wpr);

@@ -64,6 +64,27 @@ def main():
         arrays[f"eg_{name}_bits"] = per
         meta["eg"][name] = bits
 
+    # ---- adaptive EG KATs (eg.cpp:20-37 with line 25's incBlockSize enabled) --------------
+    # from the reference's own EG state machine (incBlockSize / decBlockSize / EGLUT), the writes
+    # of eg.cpp:24/29/32-33 as an MSB-first bit string (oracle/ref_capi.cpp ref_eg_adaptive)
+    rng_ad = np.random.default_rng(777)
+    Pad = o.gen_plane(0x5EED00AD, 0.1, 64, 1000)
+    run_l, run_e = o.plane_runs(o.med(Pad, 1000), 1000)
+    egad_cases = {
+        "survey": (np.array([3, 0, 7, 2], np.int32), np.array([0, 0, 1, 1], np.uint8)),
+        "short": ((rng_ad.geometric(0.5, 3000) - 1).astype(np.int32), (rng_ad.random(3000) < 0.02).astype(np.uint8)),
+        "long": (rng_ad.integers(0, 20000, 500).astype(np.int32), (rng_ad.random(500) < 0.3).astype(np.uint8)),
+        "plane_64x1000": (run_l.astype(np.int32), run_e.astype(np.uint8)),
+    }
+    meta["eg_adaptive"] = {}
+    for name, (lens, eols) in egad_cases.items():
+        bits, per, stream = r.eg_adaptive(lens, eols)
+        arrays[f"egad_{name}_len"] = lens
+        arrays[f"egad_{name}_eol"] = eols
+        arrays[f"egad_{name}_bits"] = per
+        arrays[f"egad_{name}_stream"] = stream
+        meta["eg_adaptive"][name] = bits
+
     # ---- planes: med residual, weights, Golomb/EG bitcounts of the run samples -----------
     plane_cases = [
         (1, 1, 0.5, 1), (1, 64, 0.5, 2), (1, 65, 0.3, 3), (2, 1, 0.5, 4), (3, 1, 1.0, 5),

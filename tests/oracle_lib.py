@@ -44,6 +44,7 @@ class Oracle:
         _sig(L, "bo_decode_plane_golomb", C.c_int, [u8p, C.c_uint64, sz, sz, sz, C.c_int, C.c_int, u64p])
         _sig(L, "bo_unmed", None, [u64p, u64p, sz, sz, sz, C.c_int])
         _sig(L, "bo_row_index", None, [u64p, sz, sz, sz, C.c_int, u64p])
+        _sig(L, "bo_eg_runs", C.c_int64, [i32p, u8p, sz, C.c_int, u8p, sz, u32p])
         _sig(L, "cf_encode_planes", C.c_uint64, [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, u64p, C.c_uint64, u64p,
                                                   C.c_uint64, u64p, u64p, C.POINTER(C.c_int)])
         _sig(L, "bo_get_submatrix", None, [u64p, sz, sz, sz, sz, sz, sz, sz, u64p, sz])
@@ -150,6 +151,17 @@ class Oracle:
         self.lib.cf_encode_planes(ptr(planes, u64p), n, rows, cols, wpr, predict, do_eg, ptr(G, u64p), gslot,
                                   ptr(E, u64p), eslot, ptr(gb, u64p), ptr(eb, u64p), C.byref(used))
         return gb, eb, G, E, used.value
+
+    def eg_runs(self, lens, eols, adaptive):
+        """EG over a run list: (total bits, per-run bits, MSB-first stream bytes padded to 64 bits)"""
+        lens = np.ascontiguousarray(lens, np.int32)
+        eols = np.ascontiguousarray(eols, np.uint8)
+        n = len(lens)
+        per = np.zeros(n, np.uint32)
+        cap = int(np.sum(lens.astype(np.int64))) // 2 + 32 * n + 64
+        buf = np.zeros(cap, np.uint8)
+        b = self.lib.bo_eg_runs(ptr(lens, i32p), ptr(eols, u8p), n, adaptive, ptr(buf, u8p), cap, ptr(per, u32p))
+        return int(b), per, buf[: ((b + 63) // 64) * 8].copy()
 
     def row_index(self, P, cols, predict):
         """per row: (Golomb bit offset of its first codeword, residual 1s before it), flat u64"""
@@ -310,27 +322,19 @@ class Ref:
         b = self.lib.ref_eg(ptr(lens, i32p), ptr(eols, u8p), len(lens), ptr(bits, u32p))
         return int(b), bits
 
-    def fast_encode(self, planes, cols, predict, do_eg=1, want_streams=True):
-        """the word-parallel strong-CPU encoder (oracle/cpu_fast.c): (gbits, ebits, G slots, E slots, threads)"""
-        planes = np.ascontiguousarray(planes)
-        n, rows, wpr = planes.shape
-        gslot = 2 * rows * (cols + 1) // 64 + 64
-        eslot = (rows * (cols + 1) + 1 + 63) // 64 + 1
-        G = np.zeros((n, gslot), np.uint64) if want_streams else None
-        E = np.zeros((n, eslot), np.uint64) if want_streams and do_eg else None
-        gb, eb = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
-        used = C.c_int(0)
-        self.lib.cf_encode_planes(ptr(planes, u64p), n, rows, cols, wpr, predict, do_eg, ptr(G, u64p), gslot,
-                                  ptr(E, u64p), eslot, ptr(gb, u64p), ptr(eb, u64p), C.byref(used))
-        return gb, eb, G, E, used.value
-
-    def row_index(self, P, cols, predict):
-        """per row: (Golomb bit offset of its first codeword, residual 1s before it), flat u64"""
-        P = np.ascontiguousarray(P)
-        rows, wpr = P.shape
-        out = np.zeros(2 * rows, np.uint64)
-        self.lib.bo_row_index(ptr(P, u64p), rows, cols, wpr, predict, ptr(out, u64p))
-        return out
+    def eg_adaptive(self, lens, eols):
+        """the reference's EG state machine with incBlockSize enabled: (bits, per-run bits, stream bytes)"""
+        lens = np.ascontiguousarray(lens, np.int32)
+        eols = np.ascontiguousarray(eols, np.uint8)
+        n = len(lens)
+        per = np.zeros(n, np.uint32)
+        cap = int(np.sum(lens.astype(np.int64))) // 2 + 32 * n + 64
+        buf = np.zeros(cap, np.uint8)
+        f = self.lib.ref_eg_adaptive
+        f.restype = C.c_uint64
+        f.argtypes = [i32p, u8p, sz, u32p, u8p, sz]
+        b = f(ptr(lens, i32p), ptr(eols, u8p), n, ptr(per, u32p), ptr(buf, u8p), cap)
+        return int(b), per, buf[: ((b + 63) // 64) * 8].copy()
 
     def get_submatrix(self, I, cols, i0, i1, j0, j1):
         I = np.ascontiguousarray(I)

@@ -162,3 +162,15 @@ def test_c3_full_round_trip(ctx, oracle):
     assert ctx.torch.equal(back, planes)
     exp_planes = oracle.bitplanes_par(img, 8)
     assert np.array_equal(as_u64(planes), exp_planes)
+
+
+@pytest.mark.parametrize("p", [0.5, 0.05])
+def test_c2_full_eg_adaptive(ctx, oracle, p):
+    """configs[1]'s 4096^2 plane through the adaptive EG coder (BIC_CODER_EG_ADAPTIVE), med on"""
+    rows = cols = 4096
+    P = oracle.gen_plane(0x5EED00E0 + int(p * 100), p, rows, cols)
+    out, bits = ctx.encode_planes(ctx.to_dev(P[None]), cols, True, 2)
+    ctx.sync()
+    eb, est, _ = oracle.encode_plane(P, cols, 1, 2)
+    assert int(as_u64(bits)[0]) == eb
+    assert stream_bytes(out[0], eb) == est.tobytes()

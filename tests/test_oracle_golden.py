@@ -134,3 +134,15 @@ def test_cpu_fast_matches_oracle(oracle, rows, cols, p, pred):
             b, st, _ = oracle.encode_plane(P[k], cols, pred, coder)
             assert int(bits[k]) == b, (k, coder)
             assert S[k, :len(st) // 8].tobytes() == st.tobytes(), (k, coder)
+
+
+@pytest.mark.parametrize("name", ["survey", "short", "long", "plane_64x1000"])
+def test_eg_adaptive_kat(oracle, golden, name):
+    """the oracle's adaptive EG (coder 2) == the reference's EG state machine with incBlockSize
+    enabled (golden vectors from oracle/ref_capi.cpp ref_eg_adaptive): per-run bits and the stream"""
+    meta, arr = golden
+    lens, eols = arr[f"egad_{name}_len"], arr[f"egad_{name}_eol"]
+    bits, per, stream = oracle.eg_runs(lens, eols, 1)
+    assert bits == meta["eg_adaptive"][name]
+    assert np.array_equal(per, arr[f"egad_{name}_bits"])
+    assert stream.tobytes() == arr[f"egad_{name}_stream"].tobytes()
