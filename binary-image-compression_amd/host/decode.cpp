@@ -50,6 +50,41 @@ int decode_plane(const uint8_t* stream, uint64_t bits, int coder, binary_matrix&
       }
       if (!in.bit()) return -1;  // end of row
     }
+  } else if (coder == BIC_CODER_EG_ADAPTIVE) {
+    // eg.cpp:41-55 (the #if 0 decoder): '1' = a full block (len += blockSize, incBlockSize), until
+    // a '0' and the g-bit remainder (then decBlockSize) -- or until the blocks pass the columns left,
+    // which is the end-of-row '1'. The index saturates at 31 as in the encoder (bic.h).
+    static const unsigned J[32] = {0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3,
+                                   4, 4, 5, 5, 6, 6, 7, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+    int idx = 0;
+    unsigned g = 1, bs = 1;  // eg.h:9
+    for (idx_t i = 0; i < rows; ++i) {
+      idx_t j = 0;
+      for (;;) {
+        const uint64_t maxlen = (uint64_t)(cols - j);
+        uint64_t len = 0;
+        bool eol = false;
+        while (in.bit()) {
+          if (in.overrun()) return -1;
+          len += bs;
+          if (len > maxlen) {
+            eol = true;
+            break;
+          }
+          if (idx < 31) ++idx;
+          g = J[idx];
+          bs = 1u << g;
+        }
+        if (eol) break;
+        len += in.bits(g);
+        if (idx > 0) --idx;
+        g = J[idx];
+        bs = 1u << g;
+        if (in.overrun() || len >= maxlen) return -1;
+        R.set(i, j + (idx_t)len);
+        j += (idx_t)len + 1;
+      }
+    }
   } else {
     return -1;
   }

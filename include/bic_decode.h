@@ -58,8 +58,8 @@ class GolombStreamDecoder : public Golomb {
   BitReader* r_;
 };
 
-// Residual plane of a stream into R (allocated rows x cols): coder = BIC_CODER_GOLOMB or
-// BIC_CODER_EG. Returns 0, or -1 if the stream is malformed or its length is not `bits`.
+// Residual plane of a stream into R (allocated rows x cols): coder = BIC_CODER_GOLOMB,
+// BIC_CODER_EG or BIC_CODER_EG_ADAPTIVE. Returns 0, or -1 if the stream is malformed or its length is not `bits`.
 int decode_plane(const uint8_t* stream, uint64_t bits, int coder, binary_matrix& R);
 
 // P from its med residual R (pred.h) and P(0,0); P allocated like R.

@@ -41,10 +41,10 @@ def test_coder_known_answers(exe):
                                          (64, 1024, 0.5), (9, 130, 0.0), (7, 65, 1.0)])
 @pytest.mark.parametrize("predict", [0, 1])
 def test_decoders_read_oracle_streams(exe, oracle, tmp_path, rows, cols, p, predict):
-    """oracle stream -> C++ decoder -> the residual the oracle coded (both coders)"""
+    """oracle stream -> C++ decoder -> the residual the oracle coded (Golomb, EG as written, EG adaptive)"""
     P = oracle.gen_plane(7 * rows + cols, p, rows, cols)
     R = oracle.med(P, cols) if predict else P
-    for coder in (0, 1):
+    for coder in (0, 1, 2):
         bits, stream, _ = oracle.encode_plane(P, cols, predict, coder)
         sp = tmp_path / f"s{coder}.bin"
         sp.write_bytes(stream.tobytes())
