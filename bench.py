@@ -32,7 +32,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c1", "c1m", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c1m", "c2", "c3", "c3f", "c4", "c5"])
     ap.add_argument("--rows", type=int, default=0, help="override image rows (c3/c2/c5)")
     ap.add_argument("--cols", type=int, default=0, help="override image cols")
     ap.add_argument("--cpu-rows", type=int, default=16384, help="rows per plane in the CPU baseline sample")
@@ -328,6 +328,60 @@ class C3Planes(C3):
         g = int(self.pybic.as_u64(self.bits_g[:self.nplanes]).astype(np.int64).sum()) // 8
         e = int(self.pybic.as_u64(self.bits_e[:self.nplanes]).astype(np.int64).sum()) // 8
         return {"bitplanes_count": self.rows * self.cols + plane_b, "encode_rows_golomb_eg": plane_b + g + e}
+
+
+class C3File(C3):
+    """C3 from a P5 file's bytes: the whole file -- header + 16384^2 raster -- is
+    resident in HBM as read; a step parses the header on the host (bic_pnm_parse_header, from the
+    file's first bytes), extracts the planes from the raster where it lies (19 bytes into the file:
+    bic_pgm_bitplanes, unaligned loads) and encodes them (bic_encode_planes2, Golomb + EG)."""
+
+    def __init__(self, ctx, args, rank):
+        import pybic
+        t = ctx.torch
+        self.ctx, self.pybic = ctx, pybic
+        self.rows = args.rows or 16384
+        self.cols = args.cols or 16384
+        self.nplanes = 8
+        g = t.Generator(device=ctx.dev)
+        g.manual_seed(0x5EED0000 + rank)
+        hdr = f"P5\n{self.cols} {self.rows}\n255\n".encode()
+        self.head = hdr + b"\0" * 45  # the host's copy of the file's first bytes
+        self.files = []
+        for _ in range(2):  # two files alternated (the Infinity Cache cannot serve a re-run)
+            f = t.empty(len(hdr) + self.rows * self.cols, dtype=t.uint8, device=ctx.dev)
+            f[:len(hdr)] = t.tensor(list(hdr), dtype=t.uint8)
+            f[len(hdr):] = t.randint(0, 256, (self.rows * self.cols,), dtype=t.uint8, device=ctx.dev, generator=g)
+            self.files.append(f)
+        self.gray = [f[len(hdr):].view(self.rows, self.cols) for f in self.files]
+        self.wpr = (self.cols + 63) // 64
+        self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr)
+        self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
+        self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
+        self.out_g = ctx.empty_i64(self.nplanes, self.slot_g)
+        self.out_e = ctx.empty_i64(self.nplanes, self.slot_e)
+        self.bits_g = ctx.empty_i64(self.nplanes)
+        self.bits_e = ctx.empty_i64(self.nplanes)
+        ctx.reserve(self.nplanes, self.rows, self.cols)
+        self.k = 0
+        self.separate = True
+        self.pixels = self.rows * self.cols * self.nplanes
+        self.workload = (f"c3f: a {self.rows}x{self.cols} P5 file's bytes in HBM -> header (host) -> 8 bitplanes "
+                         f"from the raster in place -> med -> Golomb + EG streams per plane")
+
+    def step(self):
+        c = self.ctx
+        h = self.pybic.pnm_header(self.head)
+        f = self.files[self.k & 1]
+        c.pgm_bitplanes(f[h.data_offset:], h.rows, h.cols, h.maxval, self.nplanes, out=self.planes)
+        c.encode_planes2(self.planes, self.cols, True, slots=(self.slot_g, self.slot_e), outs=(self.out_g, self.out_e),
+                         bits=(self.bits_g, self.bits_e))
+        self.k += 1
+
+    def kernel_bytes(self):
+        kb = super().kernel_bytes()
+        kb["pgm_bitplanes"] = kb["bitplanes_u8"]
+        return kb
 
 
 class C2(C3):
@@ -638,7 +692,7 @@ def cpu_baseline(wl, args):
         return None
     nplanes = planes.shape[0]
     threads = max(1, min(nplanes, int(os.environ.get("OMP_NUM_THREADS", "8") or 8)))
-    do_eg = 1 if type(wl) in (C3, C3Planes) else 0
+    do_eg = 1 if type(wl) in (C3, C3Planes, C3File) else 0
     predict = 0 if isinstance(wl, C2) else 1
     reps, dt, used = 0, 0.0, 0
     while reps == 0 or (dt < args.cpu_seconds and reps < 32):
@@ -691,6 +745,8 @@ def main():
         wl = C3Planes(ctx, args, rank, world)
     elif args.workload == "c3":
         wl = C3(ctx, args, rank)
+    elif args.workload == "c3f":
+        wl = C3File(ctx, args, rank)
     elif args.workload == "c2":
         wl = C2(ctx, args, rank)
     elif args.workload == "c4":

@@ -5,6 +5,7 @@
 #include "bic.h"
 #include "bic_internal.h"
 
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -850,6 +851,83 @@ int bic_pbm_unpack(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols
     bic::launch_pbm(ctx->cur, false, raster, nullptr, nullptr, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr);
   });
   BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_pgm_bitplanes(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, int maxval, int plane0,
+                      int nplanes, uint64_t* planes, size_t wpr) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (maxval < 1 || maxval > 65535 || plane0 < 0 || nplanes < 1 || plane0 + nplanes > (maxval < 256 ? 8 : 16))
+    return BIC_EINVAL;
+  if (!geom_ok(rows, cols, wpr) || (rows && (!raster || !planes))) return BIC_EINVAL;
+  if (rows == 0) return BIC_OK;
+  timed(ctx, "pgm_bitplanes", [&] {
+    bic::launch_raster_planes(ctx->cur, raster, maxval < 256 ? 1 : 2, (uint32_t)rows, (uint32_t)cols, plane0, nplanes,
+                              planes, (uint32_t)wpr);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+namespace {
+// pnm.cpp:5-18 skip_comments on a byte buffer: whitespace, then a '#' line (fgets into a 100-byte
+// buffer: at most 99 bytes, through the newline) and again
+void pnm_skip_comments(const uint8_t* b, size_t n, size_t& i) {
+  for (;;) {
+    while (i < n && std::isspace(b[i])) ++i;
+    if (i >= n || b[i] != '#') return;
+    ++i;  // the '#' (fgetc), then fgets' at most 99 bytes
+    size_t k = 0;
+    while (i < n && k < 99) {
+      const uint8_t c = b[i++];
+      ++k;
+      if (c == '\n') break;
+    }
+  }
+}
+// fscanf("%d"): leading whitespace, an optional sign, digits
+bool pnm_int(const uint8_t* b, size_t n, size_t& i, long long& v) {
+  while (i < n && std::isspace(b[i])) ++i;
+  bool neg = false;
+  if (i < n && (b[i] == '+' || b[i] == '-')) neg = b[i++] == '-';
+  if (i >= n || !std::isdigit(b[i])) return false;
+  v = 0;
+  while (i < n && std::isdigit(b[i])) {
+    v = v * 10 + (b[i++] - '0');
+    if (v > 0x7fffffffLL) return false;
+  }
+  if (neg) v = -v;
+  return true;
+}
+}  // namespace
+
+int bic_pnm_parse_header(const uint8_t* bytes, size_t n, bic_pnm_info* info) {
+  if (!bytes || !info || n < 2 || bytes[0] != 'P') return BIC_EINVAL;
+  size_t i = 2;
+  long long w = 0, h = 0, mv = 1;
+  const int type = bytes[1] - '0';
+  if (type == 4) {  // pbm.cpp:4-27: " %d" then " %d " (which also eats whitespace-valued raster bytes)
+    if (!pnm_int(bytes, n, i, w) || !pnm_int(bytes, n, i, h) || w <= 0 || h <= 0) return BIC_EINVAL;
+    while (i < n && std::isspace(bytes[i])) ++i;
+  } else if (type == 2 || type == 5 || type == 6) {  // pnm.cpp:20-42
+    pnm_skip_comments(bytes, n, i);
+    if (!pnm_int(bytes, n, i, w)) return BIC_EINVAL;
+    pnm_skip_comments(bytes, n, i);
+    if (!pnm_int(bytes, n, i, h)) return BIC_EINVAL;
+    pnm_skip_comments(bytes, n, i);
+    if (!pnm_int(bytes, n, i, mv)) return BIC_EINVAL;
+    if (w <= 0 || h <= 0 || mv <= 0 || mv > 65535) return BIC_EINVAL;
+    ++i;  // the fgetc after maxval
+  } else {
+    return BIC_EINVAL;
+  }
+  if (i > n) return BIC_EINVAL;
+  info->type = type;
+  info->cols = (size_t)w;
+  info->rows = (size_t)h;
+  info->maxval = (int)mv;
+  info->data_offset = i;
   return BIC_OK;
 }
 

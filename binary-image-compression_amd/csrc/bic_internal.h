@@ -188,6 +188,9 @@ void launch_match_code(hipStream_t s, const MatchArgs& a, unsigned long long* ou
                        size_t cap_words, uint64_t* stats);
 void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* raster_out, const uint64_t* plane_in,
                 uint64_t* plane_out, uint32_t rows, uint32_t cols, uint32_t wpr);
+// P5 samples (1 or 2 bytes, any alignment) -> planes plane0.. (bic_raster.hip)
+void launch_raster_planes(hipStream_t s, const uint8_t* raster, int bpp, uint32_t rows, uint32_t cols, int plane0,
+                          int nplanes, uint64_t* planes, uint32_t wpr);
 
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);

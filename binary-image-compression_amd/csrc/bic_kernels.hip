@@ -1316,50 +1316,6 @@ void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, ui
 }
 
 // ------------------------------------------------------------------------------------
-// PBM rasters (pbm.cpp:29-77): a plane word is a big-endian load of 8 raster bytes. One thread
-// per plane word; raster rows are only byte-aligned, so bytes move one at a time (coalesced
-// across the wave).
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_pbm_unpack(const uint8_t* __restrict__ raster, uint32_t rows,
-                                                       uint32_t cols, uint32_t wpr, uint64_t* __restrict__ plane) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t used = (cols + 63) / 64, nb = (cols + 7) / 8;
-  if (i >= (uint64_t)rows * wpr) return;
-  const uint32_t row = (uint32_t)(i / wpr), w = (uint32_t)(i % wpr);
-  uint64_t v = 0;
-  if (w < used) {
-    const uint8_t* src = raster + (uint64_t)row * nb + 8ull * w;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) v = (v << 8) | (8 * w + b < nb ? src[b] : 0u);
-    if (w == used - 1 && (cols & 63)) v &= ~(~0ull >> (cols & 63));
-  }
-  plane[i] = v;
-}
-
-__global__ __launch_bounds__(kBlock) void k_pbm_pack(const uint64_t* __restrict__ plane, uint32_t rows,
-                                                     uint32_t cols, uint32_t wpr, uint8_t* __restrict__ raster) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t used = (cols + 63) / 64, nb = (cols + 7) / 8;
-  if (i >= (uint64_t)rows * used) return;
-  const uint32_t row = (uint32_t)(i / used), w = (uint32_t)(i % used);
-  uint64_t v = plane[(uint64_t)row * wpr + w];
-  if (w == used - 1 && (cols & 63)) v &= ~(~0ull >> (cols & 63));
-  uint8_t* dst = raster + (uint64_t)row * nb + 8ull * w;
-#pragma unroll
-  for (int b = 0; b < 8; ++b)
-    if (8 * w + b < nb) dst[b] = (uint8_t)(v >> (56 - 8 * b));
-}
-
-void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* raster_out, const uint64_t* plane_in,
-                uint64_t* plane_out, uint32_t rows, uint32_t cols, uint32_t wpr) {
-  const uint64_t n = pack ? (uint64_t)rows * ((cols + 63) / 64) : (uint64_t)rows * wpr;
-  const uint32_t grid = (uint32_t)((n + kBlock - 1) / kBlock);
-  if (grid == 0) return;
-  if (pack) k_pbm_pack<<<grid, kBlock, 0, s>>>(plane_in, rows, cols, wpr, raster_out);
-  else k_pbm_unpack<<<grid, kBlock, 0, s>>>(raster_in, rows, cols, wpr, plane_out);
-}
-
-// ------------------------------------------------------------------------------------
 // Host: the fused encoder's byte table (bic_fused.hip encode_word). For k in 1..3 and byte v
 // (MSB = first pixel), the codewords of the runs that start AND end inside v -- between its
 // first and last 1 -- as one MSB-first pattern, with the byte's leading and trailing zeros.

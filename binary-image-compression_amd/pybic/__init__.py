@@ -28,8 +28,14 @@ EXPORTS = [
     "bic_malloc", "bic_free", "bic_memcpy_h2d", "bic_memcpy_d2h", "bic_memset", "bic_pbm_unpack", "bic_pbm_pack",
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
     "bic_bitplanes_u8_range", "bic_encode_gray_range", "bic_encode_planes_packed", "bic_encode_gray_packed",
-    "bic_row_index", "bic_decode_planes",
+    "bic_row_index", "bic_decode_planes", "bic_pgm_bitplanes", "bic_pnm_parse_header",
 ]
+
+
+class PnmInfo(C.Structure):
+    """include/bic.h bic_pnm_info"""
+    _fields_ = [("type", C.c_int), ("rows", C.c_size_t), ("cols", C.c_size_t), ("maxval", C.c_int),
+                ("data_offset", C.c_size_t)]
 
 
 class BicError(RuntimeError):
@@ -102,6 +108,8 @@ def load(path=LIB_PATH):
     sig("bic_encode_gray_packed", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, vp, sz, vp, vp, vp])
     sig("bic_row_index", i32, [vp, vp, i32, sz, sz, sz, i32, vp])
     sig("bic_decode_planes", i32, [vp, i32, vp, sz, vp, vp, vp, i32, sz, sz, sz, i32, vp, vp])
+    sig("bic_pgm_bitplanes", i32, [vp, vp, sz, sz, i32, i32, i32, vp, sz])
+    sig("bic_pnm_parse_header", i32, [C.c_char_p, sz, C.POINTER(PnmInfo)])
     _lib = L
     return L
 
@@ -453,6 +461,15 @@ class Context:
     def set_match_parts(self, parts):
         self._chk(self.lib.bic_set_match_parts(self.h, parts), "bic_set_match_parts")
 
+    def pgm_bitplanes(self, raster, rows, cols, maxval, nplanes, plane0=0, wpr=None, out=None):
+        """P5 samples (uint8 device tensor view starting at the first sample, any alignment) -> planes"""
+        wpr = wpr or (cols + 63) // 64
+        out = self.empty_i64(nplanes, rows, wpr) if out is None else out
+        self._bind_stream()
+        self._chk(self.lib.bic_pgm_bitplanes(self.h, _p(raster), rows, cols, maxval, plane0, nplanes, _p(out), wpr),
+                  "bic_pgm_bitplanes")
+        return out
+
     def pbm_unpack(self, raster, rows, cols, wpr=None):
         """P4 raster bytes (uint8 device tensor, rows x ceil(cols/8)) -> int64 plane [rows, wpr]."""
         wpr = wpr or (cols + 63) // 64
@@ -461,10 +478,10 @@ class Context:
         self._chk(self.lib.bic_pbm_unpack(self.h, _p(raster), rows, cols, _p(plane), wpr), "bic_pbm_unpack")
         return plane
 
-    def pbm_pack(self, plane, cols):
-        """int64 plane [rows, wpr] -> P4 raster bytes (uint8 device tensor)."""
+    def pbm_pack(self, plane, cols, out=None):
+        """int64 plane [rows, wpr] -> P4 raster bytes (uint8 device tensor; `out`: any alignment)."""
         rows, wpr = plane.shape
-        raster = self.torch.empty(rows * ((cols + 7) // 8), dtype=self.torch.uint8, device=self.dev)
+        raster = self.torch.empty(rows * ((cols + 7) // 8), dtype=self.torch.uint8, device=self.dev) if out is None else out
         self._bind_stream()
         self._chk(self.lib.bic_pbm_pack(self.h, _p(plane), rows, cols, wpr, _p(raster)), "bic_pbm_pack")
         return raster
@@ -477,6 +494,15 @@ class Context:
         self._chk(self.lib.bic_pack_streams(self.h, _p(slots), n, slot_words, _p(plane_bits), _p(dst), _p(off)),
                   "bic_pack_streams")
         return dst, off
+
+
+def pnm_header(data):
+    """bic_pnm_parse_header on host bytes -> PnmInfo (raises BicError on a malformed header)"""
+    info = PnmInfo()
+    rc = load().bic_pnm_parse_header(bytes(data), len(data), C.byref(info))
+    if rc != BIC_OK:
+        raise BicError(rc, "bic_pnm_parse_header")
+    return info
 
 
 def enum_codelength(n, r):

@@ -253,10 +253,29 @@ int bic_pack_streams(bic_ctx* ctx, const uint64_t* slots, int nplanes, size_t sl
 
 /* ---- PBM (P4) rasters on the device (pbm.cpp:29-77) ------------------------------------------
  * A P4 raster is rows x ceil(cols/8) bytes, MSB = leftmost pixel, rows byte-aligned (device
- * memory, no header). unpack: raster -> planes (rows x wpr words; pad bits 0); pack: planes ->
- * raster (pad bits of the last byte of a row 0), as read_pbm_data / write_pbm do bit by bit. */
+ * memory, no header, any alignment: e.g. a file's bytes + data_offset). unpack: raster -> planes
+ * (rows x wpr words; pad bits 0); pack: planes -> raster (pad bits of the last byte of a row 0), as
+ * read_pbm_data / write_pbm do bit by bit. */
 int bic_pbm_unpack(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, uint64_t* plane, size_t wpr);
 int bic_pbm_pack(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, uint8_t* raster);
+
+/* ---- a1 / f3: PNM headers on the host, PGM samples on the device (pnm.cpp:5-89) -------------
+ * bic_pnm_parse_header: the header of a P4 (pbm.cpp:4-27, " %d " swallowing whitespace after the
+ * height, raster bytes included) or P2 / P5 / P6 file (pnm.cpp:20-42: '#' comment lines between
+ * fields, one byte after maxval) from its first n bytes (host memory); data_offset = where the
+ * raster starts. P4: maxval = 1. */
+typedef struct {
+  int type;            /* 4 = P4 (PBM); 2, 5 = PGM; 6 = PPM */
+  size_t rows, cols;
+  int maxval;
+  size_t data_offset;
+} bic_pnm_info;
+int bic_pnm_parse_header(const uint8_t* bytes, size_t n, bic_pnm_info* info);
+/* P5 samples on the device -> planes plane0 .. plane0 + nplanes - 1 (bitplane_tool.cpp:24-30):
+ * raster = the first sample (device, any alignment, e.g. a file's bytes + data_offset), 1 byte per
+ * sample when maxval < 256 else 2 bytes big-endian (pnm.cpp:71-74), rows of cols samples. */
+int bic_pgm_bitplanes(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, int maxval, int plane0,
+                      int nplanes, uint64_t* planes, size_t wpr);
 
 /* ---- kernel timing ------------------------------------------------------------------------
  * When enabled, every kernel launch of this ctx is bracketed by HIP events on the launch stream.

@@ -127,6 +127,35 @@ uint64_t ref_eg_adaptive(const int32_t* len, const uint8_t* eol, size_t n, uint3
   return pos;
 }
 
+// The reference's header readers on a file (pnm.cpp:20-42 read_pnm_header, pbm.cpp:4-27
+// read_pbm_header) and where they leave the file position: the raster offset.
+int ref_pnm_header(const char* path, int* type, long* rows, long* cols, int* maxval, long* offset) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return -2;
+  int c0 = fgetc(f), c1 = fgetc(f);
+  rewind(f);
+  int rc;
+  if (c0 == 'P' && c1 == '4') {
+    idx_t r = 0, c = 0;
+    rc = read_pbm_header(f, r, c) == PBM_OK ? 0 : -1;
+    *type = 4;
+    *rows = (long)r;
+    *cols = (long)c;
+    *maxval = 1;
+  } else {
+    int t = 0, w = 0, h = 0, mv = 0;
+    rc = read_pnm_header(f, t, w, h, mv);  // closes f on a bad magic
+    if (rc) return rc;
+    *type = t;
+    *rows = h;
+    *cols = w;
+    *maxval = mv;
+  }
+  *offset = ftell(f);
+  fclose(f);
+  return rc;
+}
+
 int ref_get_submatrix(const uint64_t* I, size_t rows, size_t cols, size_t wpr, size_t i0,
                       size_t i1, size_t j0, size_t j1, uint64_t* B, size_t bwpr) {
   binary_matrix A = from_words(I, rows, cols, wpr);

@@ -174,3 +174,21 @@ def test_c2_full_eg_adaptive(ctx, oracle, p):
     eb, est, _ = oracle.encode_plane(P, cols, 1, 2)
     assert int(as_u64(bits)[0]) == eb
     assert stream_bytes(out[0], eb) == est.tobytes()
+
+
+def test_c3_p5_file_full(ctx, oracle):
+    """configs[2] from a P5 file's bytes on the device: header parsed on the host, the planes of the
+    raster in place (it starts 19 bytes into the file), both streams of every plane"""
+    import pybic
+    rows = cols = 16384
+    img = _gray(oracle, 0x5EED0004, rows, cols, "uniform")
+    hdr = f"P5\n{cols} {rows}\n255\n".encode()
+    data = np.frombuffer(hdr + img.tobytes(), np.uint8)
+    h = pybic.pnm_header(data[:64].tobytes())
+    dev = ctx.torch.from_numpy(data.copy()).to(ctx.dev)
+    planes = ctx.pgm_bitplanes(dev[h.data_offset:], h.rows, h.cols, h.maxval, 8)
+    (og, bg), (oe, be) = ctx.encode_planes2(planes, cols, True)
+    ctx.sync()
+    exp_planes = oracle.bitplanes_par(img, 8)
+    assert np.array_equal(as_u64(planes), exp_planes)
+    _check_streams(ctx, oracle.encode_planes_par(exp_planes, cols, 1), 8, ((og, bg), (oe, be)))

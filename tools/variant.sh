@@ -9,5 +9,5 @@ mkdir -p build/var lib
 /opt/rocm/bin/hipcc $FL -c -o build/var/${N}_fused.o $F &
 /opt/rocm/bin/hipcc $FL -c -o build/var/${N}_kern.o $K &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/var_$N.so build/var/${N}_fused.o build/var/${N}_kern.o build/bic_match.o build/bic_decode.o build/bic_capi.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/var_$N.so build/var/${N}_fused.o build/var/${N}_kern.o build/bic_match.o build/bic_decode.o build/bic_egad.o build/bic_raster.o build/bic_capi.o
 echo lib/var_$N.so
