@@ -14,6 +14,7 @@
 #include "GolombCoder.h"
 #include "eg.h"
 
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <vector>
@@ -61,6 +62,28 @@ int ref_med(const uint64_t* P, uint64_t* R, size_t rows, size_t cols, size_t wpr
   A.destroy();
   B.destroy();
   return 0;
+}
+
+// The same call pattern on the reference's own med (pred.cpp:3-15): n calls on separate W x W
+// tiles, as compress7_test.cpp:205-206 makes them. Returns seconds per call.
+double ref_med_calls(int n, int W) {
+  binary_matrix P(W, W), R(W, W);
+  P.clear();
+  R.clear();
+  uint64_t s = 0x5EED;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int t = 0; t < n; ++t) {
+    for (int i = 0; i < W; ++i)
+      for (int j = 0; j < W; ++j) {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        P.set(i, j, (s >> 62) & 1);
+      }
+    med(P, R);
+  }
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  P.destroy();
+  R.destroy();
+  return dt / n;
 }
 
 uint64_t ref_weight(const uint64_t* P, size_t rows, size_t cols, size_t wpr) {

@@ -8,6 +8,7 @@
 //   gpu <in.pgm> <outdir>                GPU path: bitplanes, med, encode, tiles; self-checks
 //                                        against the reference coders and the decoders, writes
 //                                        planes and streams for the oracle comparison
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -404,6 +405,46 @@ int gpu(int argc, char** argv) {
   return failures ? 1 : 0;
 }
 
+// The compress7_test.cpp:205-206 call pattern: med() on n separate W x W tiles, each call a full
+// round trip to the device (copy in, kernel, copy out). Prints the time per call; checks the tiles
+// against the word-form med restated here (the host never computes med for the product).
+int medcalls(int argc, char** argv) {
+  const int n = argc > 2 ? std::atoi(argv[2]) : 65536, W = argc > 3 ? std::atoi(argv[3]) : 32;
+  binary_matrix P(W, W), R(W, W);
+  uint64_t s = 0x5EED;
+  auto rnd = [&]() {
+    s += 0x9E3779B97F4A7C15ull;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  long bad = 0;
+  med(P, R);  // the first call pays the context creation
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int t = 0; t < n; ++t) {
+    block_t* p = P.raw_blocks();
+    for (idx_t i = 0; i < (idx_t)W; ++i) p[i * P.get_blocks_per_row()] = rnd() & (W == 64 ? ~0ull : ~(~0ull >> W));
+    med(P, R);
+    if (t % 4096 == 0) {  // spot check: R(i,j) = P(i-1,j-1)^P(i,j-1)^P(i-1,j)^P(i,j), R(0,0) kept
+      for (idx_t i = 0; i < (idx_t)W; ++i)
+        for (idx_t j = 0; j < (idx_t)W; ++j) {
+          if (i == 0 && j == 0) continue;
+          int e = P.get(i, j);
+          if (j) e ^= P.get(i, j - 1);
+          if (i) e ^= P.get(i - 1, j);
+          if (i && j) e ^= P.get(i - 1, j - 1);
+          bad += e != R.get(i, j);
+        }
+    }
+  }
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::printf("medcalls n=%d W=%d us_per_call=%.2f total_s=%.3f bad=%ld\n", n, W, dt / n * 1e6, dt, bad);
+  P.destroy();
+  R.destroy();
+  return bad ? 1 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -413,5 +454,6 @@ int main(int argc, char** argv) {
   if (mode == "decode") return decode(argc, argv);
   if (mode == "unmed") return unmed_cmd(argc, argv);
   if (mode == "gpu") return gpu(argc, argv);
+  if (mode == "medcalls") return medcalls(argc, argv);
   return 2;
 }

@@ -135,3 +135,19 @@ def test_library_exports_reference_api():
     defined = {line.split(" ", 2)[2] for line in syms.splitlines() if line.count(" ") >= 2}
     missing = [s for s in REFERENCE_API if s not in defined]
     assert not missing, missing
+
+
+@pytest.mark.gpu
+def test_med_call_pattern(exe):
+    """compress7_test.cpp:205-206's pattern through the drop-in med(): 65,536 separate 32x32 calls (one
+    8192^2 plane's tiles), each a device round trip; the time per call goes to INTEGRATION.md"""
+    rc, out = run(exe, "medcalls", 65536, 32, timeout=600)
+    assert rc == 0, out
+    print(out.strip())
+    from oracle_lib import REF_SO, have_ref
+    if have_ref():  # the reference's own med, same pattern, on this host (tile fill included)
+        import ctypes as C
+        f = C.CDLL(REF_SO).ref_med_calls
+        f.restype = C.c_double
+        f.argtypes = [C.c_int, C.c_int]
+        print(f"reference med (oracle/_ref) us_per_call={f(65536, 32) * 1e6:.2f}")
