@@ -327,6 +327,124 @@ __device__ __forceinline__ LaneEnc encode_word_k1(uint64_t x, uint32_t w, int jp
   return e;
 }
 
+// encode_word_k1 without branches: every byte runs the same instructions (its codeword from the k = 1
+// table whether or not it holds a 1, selected in or out), so a wave never executes divergent paths.
+// Inside a word a run's zeros are < 64 + 7, so a byte's pattern (bin, q zeros, '1', R) is < 64 bits;
+// out-of-range shift amounts of unselected bytes are clamped.
+__device__ __forceinline__ LaneEnc encode_word_k1b(uint64_t x, uint32_t w, int jp, bool eol, uint32_t cols,
+                                                   const uint32_t* T1) {
+  LaneEnc e{};
+  e.k0 = 1;
+  uint32_t c = w * 64 - (uint32_t)(jp + 1);  // zeros of the open run
+  if (!x) {
+    if (eol) {
+      const uint32_t s = cols - 1 - (uint32_t)jp;
+      e.head = s & 1u;
+      e.z = s >> 1;
+      e.t0 = BIC_MSB;
+      e.tlen = 1;
+      e.len = 2 + e.z;
+    }
+    return e;
+  }
+  const uint32_t bf = (uint32_t)__builtin_clzll(x), fb = bf >> 3;
+  const uint32_t s1 = c + bf;
+  e.head = s1 & 1u;
+  e.z = s1 >> 1;
+  uint64_t hi = 0, lo = 0;
+  uint32_t p = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t v = (uint32_t)(x >> (56 - 8 * i)) & 0xffu;
+    const uint32_t en = T1[v];
+    const uint32_t R = en & 0x1fffffu, lr = (en >> 21) & 31u, t = (en >> 26) & 7u, tz = en >> 29;
+    const uint32_t sr = c + t;
+    const uint32_t q1 = min((sr >> 1) + 1u, 62u - lr);  // the '1' after q zeros, then R
+    const uint64_t tail = (1ull << lr) | R;
+    const bool first = i == fb;
+    const uint64_t pat = first ? tail : ((uint64_t)(sr & 1u) << (q1 + lr)) | tail;
+    const uint32_t nb = first ? lr + 1 : q1 + 1 + lr;  // 1..63
+    const bool act = v != 0;
+    const uint64_t nhi = (hi << nb) | (lo >> (64 - nb));
+    const uint64_t nlo = (lo << nb) | pat;
+    hi = act ? nhi : hi;
+    lo = act ? nlo : lo;
+    p += act ? nb : 0u;
+    c = act ? tz : c + 8;
+  }
+  if (eol) {  // the row's trailing zeros (pad columns excluded): bin, q zeros, '1' (< 64 bits)
+    const uint32_t sr = c - (w * 64 + 64 - cols), q1 = (sr >> 1) + 1;
+    const uint32_t nb = q1 + 1;
+    const uint64_t pat = ((uint64_t)(sr & 1u) << q1) | 1ull;
+    hi = (hi << nb) | (lo >> (64 - nb));
+    lo = (lo << nb) | pat;
+    p += nb;
+  }
+  e.tlen = p;
+  e.len = 1 + e.z + p;
+  e.lng = p > 128;
+  if (!e.lng) {  // left-align the p-bit string
+    const uint32_t sh = 128 - p;
+    if (sh >= 64) {
+      e.t0 = lo << (sh - 64);
+      e.t1 = 0;
+    } else if (sh) {
+      e.t0 = (hi << sh) | (lo >> (64 - sh));
+      e.t1 = lo << sh;
+    } else {
+      e.t0 = hi;
+      e.t1 = lo;
+    }
+  }
+  return e;
+}
+
+// A row image of 64-bit LDS words (bit 64 i + b at significance 63 - b of word i), OR'd with
+// ds_or_b64: a lane's string (<= 128 bits at any offset) lands in at most three words.
+__device__ __forceinline__ void lds_or64(uint64_t* img, uint32_t i, uint64_t v) {
+  if (v) atomicOr(reinterpret_cast<unsigned long long*>(img + i), (unsigned long long)v);
+}
+__device__ __forceinline__ void place128_64(uint64_t* img, uint32_t off, uint64_t A, uint64_t B, uint32_t tlen) {
+  if (!tlen) return;
+  const uint32_t i = off >> 6, sh = off & 63;
+  uint64_t D0 = A, D1 = B, D2 = 0;
+  if (sh) {
+    D0 = A >> sh;
+    D1 = (A << (64 - sh)) | (B >> sh);
+    D2 = B << (64 - sh);
+  }
+  const uint32_t nw = (sh + tlen + 63) >> 6;
+  lds_or64(img, i, D0);
+  if (nw > 1) lds_or64(img, i + 1, D1);
+  if (nw > 2) lds_or64(img, i + 2, D2);
+}
+struct LdsSink64 {
+  uint64_t* buf;
+  uint32_t idx;
+  uint64_t cur;
+  __device__ __forceinline__ void flush() {
+    if (cur) atomicOr(reinterpret_cast<unsigned long long*>(buf + idx), (unsigned long long)cur);
+    cur = 0;
+  }
+  __device__ __forceinline__ void orw(uint32_t i, uint64_t v) {
+    if (i != idx) {
+      flush();
+      idx = i;
+    }
+    cur |= v;
+  }
+  __device__ __forceinline__ void put(uint32_t off, uint32_t v, uint32_t nb) {  // nb <= 32
+    const uint32_t i = off >> 6, sh = off & 63;
+    if (sh + nb <= 64) {
+      orw(i, (uint64_t)v << (64 - sh - nb));
+    } else {
+      orw(i, (uint64_t)v >> (sh + nb - 64));
+      orw(i + 1, (uint64_t)v << (128 - sh - nb));
+    }
+  }
+  __device__ __forceinline__ void bit(uint32_t off) { orw(off >> 6, BIC_MSB >> (off & 63)); }
+};
+
 // emit_word for k = 1 rows (the lng fallback of encode_word_k1).
 template <typename Sink, typename Off>
 __device__ __forceinline__ void emit_word_k1(Sink& sk, Off off, uint64_t x, uint32_t w, int jp, bool eol, uint32_t cols) {
@@ -471,6 +589,22 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
     if (a < 0) v >>= -a;
     if (t != 0 && t != (uint32_t)nw - 1) out[w0 + t] = bswap64(v);
     else if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
+    else frag[t == 0 ? 0 : 1] = v;
+  }
+}
+
+// write_row for a 64-bit LDS image (place128_64): output word t of the row holds image bits
+// [64 t - G % 64, 64 t - G % 64 + 64): two LDS words and a funnel shift.
+__device__ __forceinline__ void write_row64(const uint64_t* img, uint64_t L, uint64_t G, uint64_t* out,
+                                            uint64_t* frag) {
+  const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6;
+  const uint32_t nw = (uint32_t)(w1 - w0 + 1), g = (uint32_t)(G & 63);
+  const bool head_whole = g == 0, tail_whole = ((G + L) & 63) == 0;
+  for (uint32_t t = lane_id(); t < nw; t += 64) {
+    const uint64_t cur = img[t], prev = t ? img[t - 1] : 0ull;
+    const uint64_t v = g ? (prev << (64 - g)) | (cur >> g) : cur;
+    const bool whole = (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
+    if (whole) out[w0 + t] = bswap64(v);
     else frag[t == 0 ? 0 : 1] = v;
   }
 }
@@ -1368,6 +1502,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
   for (uint64_t id = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave; id < nrows; id += stride) {
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+    STAMP(0);
     uint64_t cp_[WPL], cu_[WPL];
     row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
     const uint32_t O = a.row_o[id];
@@ -1412,13 +1547,19 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
       }
       if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
     }
+    STAMP(1);
+#ifdef BIC_STAMPS
+    if (lane == 0) g_stamps[id * 8 + 3] = (k0 ? 1u : 0u) | (gk1 ? 2u : 0u) | ((uint64_t)blockIdx.x << 8) |
+                                          ((uint64_t)(threadIdx.x >> 6) << 40);
+#endif
     if constexpr (DO_G) {
       if (k0 && L) {
 #ifdef BIC_STAMPS
         if (!(a.dbg & 4))
 #endif
         eg_row_regs<WPL, false>(rr, g, a.gboff[id], L, a.out_g, a.gfrag + 2 * id);
-      } else if (gk1) {  // every codeword k = 1: branch-free byte-table words
+      } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
+        uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
         int jpc = -1;
         uint32_t loc = 0;
 #pragma unroll
@@ -1428,15 +1569,15 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
           const uint64_t x = rr[t];
           const int jp = step_jp(x, w, jpc);
           const bool eol = w == g.used - 1;
-          const LaneEnc e = encode_word_k1(x, w, jp, eol, g.cols, s_lut);
+          const LaneEnc e = encode_word_k1b(x, w, jp, eol, g.cols, s_lut);
           const uint32_t inc = wave_incl_sum_u32(e.len);
           const uint32_t off = loc + inc - e.len;
           loc += lane63_u32(inc);
           if (!e.lng) {
-            place_small(gimg, off, e.head, 1);
-            place128(gimg, off + 1 + e.z, e.t0, e.t1, e.tlen);
+            if (e.head) lds_or64(img, off >> 6, BIC_MSB >> (off & 63));
+            place128_64(img, off + 1 + e.z, e.t0, e.t1, e.tlen);
           } else {
-            LdsSink ls{gimg, 0, 0};
+            LdsSink64 ls{img, 0, 0};
             emit_word_k1(ls, off, x, w, jp, eol, g.cols);
             ls.flush();
           }
@@ -1444,7 +1585,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
         if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id);
+        write_row64(img, L, a.gboff[id], a.out_g, a.gfrag + 2 * id);
       }
       if (lane == 0) {
         // glen keeps its flags: k_emit_rest (on the other stream) reads them too
@@ -1453,6 +1594,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
         if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
       }
     }
+    STAMP(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
     __builtin_amdgcn_wave_barrier();
   }
