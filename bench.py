@@ -101,18 +101,26 @@ def sum_over_ranks(x, world, dev):
 
 
 def load_pmc(workload, kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    """HBM bytes per launch from the newest round's committed rocprofv3 PMC summary
+    (profiles/rNN/pmc_<workload>.json), or None."""
+    pdir = os.path.join(ROOT, "profiles")
     try:
-        with open(path) as f:
-            d = json.load(f)
+        rounds = sorted((d for d in os.listdir(pdir) if d.startswith("r") and d[1:].isdigit()), reverse=True)
+    except OSError:
+        return None
+    for r in rounds:
+        path = os.path.join(pdir, r, f"pmc_{workload}.json")
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
         for sec in ("timers", "kernels"):
             v = d.get(sec, {}).get(kernel, {}).get("hbm_bytes_per_launch")
             if v is not None:
                 return v
         return None
-    except (OSError, ValueError):
-        return None
+    return None
 
 
 def rand_words(t, shape, dev, g):
