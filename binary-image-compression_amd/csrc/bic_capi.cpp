@@ -121,8 +121,10 @@ void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
     hipStream_t st = nullptr;
     hipEvent_t a = nullptr, b = nullptr;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
-    if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+    // device-scope events: the fork / join only order two streams of this device (a system-scope
+    // release would write back L2 at every fork)
+    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+    if (hipEventCreateWithFlags(&a, fl) != hipSuccess || hipEventCreateWithFlags(&b, fl) != hipSuccess) {
       if (a) (void)hipEventDestroy(a);
       (void)hipStreamDestroy(st);
       return;

@@ -1436,8 +1436,8 @@ __device__ __forceinline__ WideRow wide_prefix(uint64_t x, uint32_t w, uint32_t 
 
 // The listed rows' Golomb lengths (codeword walk, word_len), one workgroup per row and one word
 // per lane, so a row's serial codeword chain is one word long; a fixed grid strides over the
-// list, whose length k_scan_rows left in counter[2]. Rows with mixed k, and the row holding the
-// plane's first 1, are listed for k_emit_rest.
+// list, whose length k_scan_rows left in counter[2]. k_emit_rest takes the rows with mixed k, and
+// the row holding the plane's first 1, from this same list.
 constexpr uint32_t kWalkWaves = 8192;  // the walk grid in waves (32 per CU), whatever the row width
 template <bool PREDICT>
 __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
@@ -1468,8 +1468,10 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
         L += sl[u];
         kk |= sk[u];
       }
+      // (mixed-k rows and the plane's first-1 row are k_emit_rest's: it finds them in this list by
+      // glen's flags and row_o, so no row is appended here -- thousands of same-address atomics
+      // would serialise this kernel)
       a.glen[id] = L | (!(kk & 1u) ? kK0Row : (!(kk & 2u) ? kK1Row : 0));
-      if (kk == 3u || (O == 0 && p.ones > 0)) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)id;
     }
     __syncthreads();
   }
@@ -1600,9 +1602,10 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   }
 }
 
-// The rows the prefix kernels listed (counter[3]): Golomb rows with mixed k (per-codeword k,
-// encode_word) and the EG row holding the plane's first 1 (with its inserted '0'). One workgroup
-// per row, one word per lane (wide_prefix), one LDS image per workgroup.
+// The rows the prefix kernels leave to this launch: Golomb rows with mixed k (per-codeword k,
+// encode_word; among the walked rows, counter[2]) and the EG row holding the plane's first 1 (with
+// its inserted '0'; walked, or listed by k_scan_rows in counter[3]). One workgroup per row, one word
+// per lane (wide_prefix), one LDS image per workgroup.
 template <bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t gimg[kGImg];
@@ -1617,14 +1620,21 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
   __syncthreads();
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
-  const uint32_t nlist = __hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
-    const uint64_t id = a.rest_ids[i];
+  // the scan's list (first-1 rows it did not walk), then the walked rows that are mixed-k or hold
+  // their plane's first 1
+  const uint32_t nrest = __hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nwalk = DO_G ? __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  for (uint32_t i = blockIdx.x; i < nrest + nwalk; i += gridDim.x) {
+    const uint64_t id = i < nrest ? a.rest_ids[i] : a.walk_ids[i - nrest];
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     const uint32_t O = a.row_o[id];
     const uint64_t Lf = DO_G ? a.glen[id] : 0;
     const uint64_t L = Lf & kLenMask;
     const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0;
+    if (i >= nrest) {  // a walked row: skip it unless mixed or the first-1 row (uniform over the workgroup)
+      const uint64_t onext = row + 1 < g.rows ? a.row_o[id + 1] : a.pones[plane];
+      if (!(L && !k0 && !k1) && !(O == 0 && onext > 0)) continue;
+    }
     const bool gmix = DO_G && L && !k0 && !k1 && L <= kCapBits;
     uint64_t rr[1];
     resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
@@ -1895,8 +1905,16 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (cus <= 0) cus = 256;
     }
-    // one resident wave set: 4 workgroups per CU (the main launch holds <= 128 VGPRs: 4 waves per SIMD)
-    const uint32_t egrid2 = (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * 4);
+    // one resident wave set: as many workgroups per CU as the instance's registers and LDS allow
+    // (WPL = 4: <= 128 VGPRs, 4; WPL = 1: 7), queried once per instance
+    auto occ_of = [](const void* fn) {
+      int occ = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64 * kEmitWaves, 0) != hipSuccess || occ < 1) occ = 4;
+      return std::min(occ, 8);
+    };
+    auto egrid_of = [&](int occ) {
+      return (uint32_t)std::min<uint64_t>((nrows + kEmitWaves - 1) / kEmitWaves, (uint64_t)cus * (uint32_t)occ);
+    };
     // k_emit_rest (listed rows, latency bound: few workgroups) first, on the aux stream when there
     // is one, so that it can overlap the main launch, which skips the listed rows' parts
     const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
@@ -1908,7 +1926,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
 #define BIC_EMIT1(W, P, DG, DE)                                                                        \
   {                                                                                                  \
     k_emit_rest<P, DG, DE><<<rgrid, 64 * nwv, 0, rs>>>(a);                                           \
-    k_emit_known<W, P, DG, DE><<<egrid2, 64 * kEmitWaves, 0, s>>>(a);                                \
+    static const int occ_ = occ_of(reinterpret_cast<const void*>(&k_emit_known<W, P, DG, DE>));   \
+    k_emit_known<W, P, DG, DE><<<egrid_of(occ_), 64 * kEmitWaves, 0, s>>>(a);                        \
   }
 #define BIC_EMIT(W, P)                                                                                \
   if (dg && de) BIC_EMIT1(W, P, true, true) else if (dg) BIC_EMIT1(W, P, true, false) else BIC_EMIT1(W, P, false, true)
