@@ -40,6 +40,8 @@ def parse():
                     help="repeat the CPU baseline sample until this much CPU time has been measured")
     ap.add_argument("--encoder", default="auto", choices=["auto", "staged", "single-kernel", "two-pass", "multipass"],
                     help="row encoder for rows <= 16384 columns (bic_ctx_set_option)")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="diagnostic: the staged encoder's two emission launches one after the other on one stream")
     ap.add_argument("--shard", default="images", choices=["images", "planes"],
                     help="c3 at N GPUs: one image per GPU (weak scaling, no exchange) or the 8 planes of ONE "
                          "image split over the GPUs, every rank's packed streams gathered to rank 0 over RCCL "
@@ -749,6 +751,8 @@ def main():
     import pybic
     ctx = pybic.Context(local)
     ctx.set_encoder(args.encoder)
+    if args.one_stream:
+        ctx.set_one_stream(True)
     if args.workload == "c3" and args.shard == "planes":
         wl = C3Planes(ctx, args, rank, world)
     elif args.workload == "c3":

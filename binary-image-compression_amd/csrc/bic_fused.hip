@@ -1509,6 +1509,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
     row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
     const uint32_t O = a.row_o[id];
     const uint64_t Lf = DO_G ? a.glen[id] : 0;
+    const uint64_t Gb = DO_G ? a.gboff[id] : 0;  // loaded with the row, not after the branch that uses it
     const uint64_t L = Lf & kLenMask;
     const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
     bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
@@ -1559,7 +1560,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
 #ifdef BIC_STAMPS
         if (!(a.dbg & 4))
 #endif
-        eg_row_regs<WPL, false>(rr, g, a.gboff[id], L, a.out_g, a.gfrag + 2 * id);
+        eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.gfrag + 2 * id);
       } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
         uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
         int jpc = -1;
@@ -1587,7 +1588,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
         if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        write_row64(img, L, a.gboff[id], a.out_g, a.gfrag + 2 * id);
+        write_row64(img, L, Gb, a.out_g, a.gfrag + 2 * id);
       }
       if (lane == 0) {
         // glen keeps its flags: k_emit_rest (on the other stream) reads them too
