@@ -11,9 +11,8 @@
 //    samples), so rows are decoded independently from a row index -- per row the bit offset of
 //    its first codeword and the plane's residual 1s before it, which give the coder state at the
 //    row start (N = ones + row, A = row * cols - ones: Golomb.h:21-24). The staged encoder writes
-//    the index for free (bic_encode_*_packed), bic_row_index computes it from planes. One wave per
-//    row: the row's stream bits are staged in LDS with coalesced loads, one lane walks the
-//    codewords (the chain is serial), the wave writes the row.
+//    the index for free (bic_encode_*_packed), bic_row_index computes it from planes. One lane per
+//    row walks its codewords (the chain is serial; a wave runs 64 rows' chains side by side).
 //  * EG: every row is cols + 1 bits at an offset known in closed form once the row holding the
 //    plane's first residual 1 is known (the first row that is not all '1's): word-parallel.
 //  * unmed (pred.cpp:3-15 inverted): with D(i, j) = P(i, j) ^ P(i - 1, j), med is R(i, j) =
@@ -24,9 +23,7 @@
 
 namespace bic {
 
-constexpr int kDecWaves = 4;
-constexpr uint32_t kDecWin = 1024;  // u64 stream words staged per wave (65,536 bits)
-constexpr uint32_t kDecRowWords = 256;  // cols <= 16384
+constexpr uint32_t kDecRowWords = 256;  // cols <= 16384 (the EG row kernel's four words per lane)
 
 struct DecArgs {
   uint32_t rows, cols, wpr, used, nplanes;
@@ -77,99 +74,136 @@ __device__ __forceinline__ void store_row(const DecArgs& a, uint32_t plane, uint
   for (uint32_t w = a.used + lane; w < a.wpr; w += 64) dst[w] = 0;  // pad words
 }
 
-__global__ __launch_bounds__(64 * kDecWaves) void k_dec_golomb_rows(DecArgs a) {
-  __shared__ uint64_t win[kDecWaves][kDecWin + 2];
-  __shared__ uint64_t rowbuf[kDecWaves][kDecRowWords];
-  const int lane = lane_id();
-  const uint32_t wave = uni_u32(threadIdx.x >> 6);
-  const uint64_t id = (uint64_t)blockIdx.x * kDecWaves + wave;
-  if (id >= (uint64_t)a.rows * a.nplanes) return;  // whole wave
+// Golomb: one LANE per row, so a wave decodes 64 rows side by side (each lane's codeword chain is
+// serial, and 64 chains in lockstep keep the SIMD issuing). The lanes' stream words come through a
+// per-lane ring in LDS, refilled on a uniform cadence: every kDecRefill codewords each lane issues
+// the loads of its next kDecBatch words into registers and writes the batch loaded one cadence
+// earlier into its ring. (Loading each word when a lane crosses into it would make the wave wait
+// for the latest load into the same registers -- issued one codeword earlier by some other lane --
+// at nearly every codeword: vmcnt is per wave and in order.) A lane that runs ahead of its ring
+// (long codewords) reads the words it lacks directly. Each 1 of the residual row goes into an
+// output word in a register; a word is stored when the next 1 lies beyond it -- as D (the row's
+// prefix XOR, unmed's row part) when predicting, R otherwise.
+constexpr uint32_t kDecRing = 32, kDecBatch = 8, kDecRefill = 16;
+__global__ __launch_bounds__(256) void k_dec_golomb_lanes(DecArgs a) {
+  __shared__ uint64_t ring[kDecRing * 256];  // [slot][thread]
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const uint64_t* st = plane_stream(a, plane);
   const uint64_t G = a.index[2 * id], O = a.index[2 * id + 1];
   const uint64_t E = row + 1 < a.rows ? a.index[2 * id + 2] : a.plane_bits[plane];
-  uint64_t* W = win[wave];
-  uint64_t* rb = rowbuf[wave];
-  for (uint32_t w = lane; w < kDecRowWords; w += 64) rb[w] = 0;
+  const uint64_t maxw = (a.plane_bits[plane] + 63) >> 6;  // words of this plane's stream
+  uint64_t* dst = a.out + ((uint64_t)plane * a.rows + row) * a.wpr;
   bool bad = E < G + 1;  // every row has at least its end-of-row codeword
-  const uint64_t w0 = G >> 6, nw = bad ? 0 : ((E + 63) >> 6) - w0;
-  const bool global = nw > kDecWin;  // (not reached for cols <= 16384 streams this build writes)
-  if (!global) {
-    for (uint64_t t = lane; t < nw; t += 64) W[t] = bswap64(st[w0 + t]);
-    if (lane < 2) W[nw + lane] = 0;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (lane == 0 && !bad) {
-    auto word = [&](uint64_t i) -> uint64_t {
-      if (!global) return W[i];
-      return i < nw ? bswap64(st[w0 + i]) : 0ull;
-    };
-    auto get64 = [&](uint64_t p) -> uint64_t {
-      const uint64_t i = p >> 6;
-      const uint32_t sh = (uint32_t)(p & 63);
-      const uint64_t hi = word(i);
-      return sh ? (hi << sh) | (word(i + 1) >> (64 - sh)) : hi;
-    };
-    uint64_t pos = G & 63;
-    const uint64_t end = pos + (E - G);
-    uint32_t n = (uint32_t)(O + row), A = (uint32_t)((uint64_t)row * a.cols - O);
-    uint32_t j = 0;
-    for (;;) {
-      const uint32_t k = golomb_k_state(n, A);
-      const uint64_t x = get64(pos);
-      const uint32_t low = k ? (uint32_t)(x >> (64 - k)) : 0u;
-      const uint64_t y = k ? x << k : x;
-      uint64_t z;
-      if (y) {
-        z = (uint64_t)__builtin_clzll(y);
-      } else {  // a unary run past this window
-        z = 64 - k;
-        uint64_t p2 = pos + 64;
-        for (;;) {
-          if (p2 >= end) {
-            bad = true;
-            break;
-          }
-          const uint64_t x2 = get64(p2);
-          if (x2) {
-            z += (uint64_t)__builtin_clzll(x2);
-            break;
-          }
-          z += 64;
-          p2 += 64;
-        }
-        if (bad) break;
-      }
-      if (z > a.cols) {
-        bad = true;
-        break;
-      }
-      const uint32_t s = ((uint32_t)z << k) | low;
-      pos += k + z + 1;
-      if (pos > end || (uint64_t)j + s > a.cols) {
-        bad = true;
-        break;
-      }
-      ++n;
-      A += s;
-      if (j + s == a.cols) break;  // the end-of-row codeword
-      rb[(j + s) >> 6] |= BIC_MSB >> ((j + s) & 63);
-      j += s + 1;
-    }
-    if (pos != end) bad = true;
-  }
-  if (__ballot(bad)) {
-    if (lane == 0) atomicOr(&a.flags[1], 2u);  // malformed stream (bic_sync: BIC_EDATA)
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  uint64_t r[4];
+  const uint64_t len = bad ? 0 : E - G;
+  auto ld = [&](uint64_t i) -> uint64_t { return i < maxw ? bswap64(st[i]) : 0ull; };
+  uint64_t* my = ring + threadIdx.x;
+  auto slot = [&](uint64_t i) -> uint64_t& { return my[(uint32_t)(i % kDecRing) * 256]; };
+  // ring: words [wl - kDecRing, wr) readable from LDS; [wr, wl) in flight in pend[]
+  uint64_t pend[kDecBatch];
+  uint64_t wl = (G >> 6) & ~(uint64_t)(kDecBatch - 1), wr = wl;
+  auto issue = [&]() {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) r[t] = rb[t * 64 + lane];
-  store_row(a, plane, row, r);
+    for (uint32_t q = 0; q < kDecBatch; ++q) pend[q] = wl + q < maxw ? st[wl + q] : 0ull;
+    wl += kDecBatch;
+  };
+  auto commit = [&]() {  // the batch in pend[] -> its ring slots
+#pragma unroll
+    for (uint32_t q = 0; q < kDecBatch; ++q) slot(wr + q) = bswap64(pend[q]);
+    wr += kDecBatch;
+  };
+  issue();
+  commit();
+  issue();
+  uint64_t wi = G >> 6;
+  auto get = [&](uint64_t i) -> uint64_t { return i < wr ? slot(i) : ld(i); };
+  uint64_t w0 = get(wi), w1 = get(wi + 1);
+  uint32_t b = (uint32_t)(G & 63);  // bit position in w0
+  uint64_t used_bits = 0;           // stream bits consumed by the row so far
+  auto peek = [&]() -> uint64_t { return b ? (w0 << b) | (w1 >> (64 - b)) : w0; };
+  auto advance = [&](uint32_t nb) {  // nb <= 64
+    used_bits += nb;
+    b += nb;
+    if (b >= 64) {
+      b -= 64;
+      w0 = w1;
+      ++wi;
+      w1 = get(wi + 1);
+    }
+  };
+  auto refill = [&]() {  // every lane still decoding, at the same codeword count
+    if (wl > wr) commit();
+    if (wl + kDecBatch - wi <= kDecRing) issue();  // (the slots it will fill hold words < wi)
+  };
+  uint32_t it = 0;
+  const bool pred = a.predict != 0;
+  const uint64_t p00 = (pred && row == 0 && a.p00 && a.p00[plane]) ? BIC_MSB : 0ull;
+  uint32_t ow = 0, carry = 0;  // output word being filled, the prefix-XOR carry into it
+  uint64_t acc = 0;
+  auto flush = [&]() {  // store word ow (then ow + 1 is the open one)
+    uint64_t x = acc;
+    if (pred) {
+      if (row == 0 && ow == 0) x = (x & ~BIC_MSB) | p00;  // R(0, 0) -> P(0, 0)
+      x ^= x >> 1;
+      x ^= x >> 2;
+      x ^= x >> 4;
+      x ^= x >> 8;
+      x ^= x >> 16;
+      x ^= x >> 32;  // bit j (MSB-first) = XOR of the word's bits 0..j
+      const uint32_t par = (uint32_t)(x & 1ull);
+      if (carry) x = ~x;
+      carry ^= par;
+    }
+    if (ow == a.used - 1) x &= a.trail;
+    dst[ow] = x;
+    ++ow;
+    acc = 0;
+  };
+  uint32_t n = (uint32_t)(O + row), A = (uint32_t)((uint64_t)row * a.cols - O);
+  uint32_t j = 0;  // the row's next column
+  while (!bad) {
+    if ((++it & (kDecRefill - 1)) == 0) refill();
+    const uint32_t k = golomb_k_state(n, A);
+    uint32_t low = 0;
+    if (k) {
+      low = (uint32_t)(peek() >> (64 - k));
+      advance(k);
+    }
+    uint64_t z = 0;  // unary zeros up to the '1'
+    for (;;) {
+      const uint64_t y = peek();
+      if (y) {
+        const uint32_t c = (uint32_t)__builtin_clzll(y);
+        z += c;
+        advance(c + 1);
+        break;
+      }
+      z += 64;
+      advance(64);
+      if (used_bits > len || z > a.cols) break;
+    }
+    if (used_bits > len || z > a.cols) {
+      bad = true;
+      break;
+    }
+    const uint32_t s = ((uint32_t)z << k) | low;
+    if ((uint64_t)j + s > a.cols) {
+      bad = true;
+      break;
+    }
+    ++n;
+    A += s;
+    if (j + s == a.cols) break;  // the end-of-row codeword
+    const uint32_t c = j + s;    // the 1 of this codeword's sample
+    while ((c >> 6) > ow) flush();
+    acc |= BIC_MSB >> (c & 63);
+    j = c + 1;
+  }
+  if (used_bits != len) bad = true;
+  while (ow < a.used) flush();
+  for (uint32_t w = a.used; w < a.wpr; ++w) dst[w] = 0;  // pad words
+  if (bad) atomicOr(&a.flags[1], 2u);                     // malformed stream (bic_sync: BIC_EDATA)
 }
 
 // EG: the row holding each plane's first residual 1 = the first row whose cols + 1 bits at the
@@ -194,7 +228,11 @@ __global__ __launch_bounds__(256) void k_dec_eg_first(DecArgs a) {
     const uint64_t m = nb == 64 ? ~0ull : ~(~0ull >> nb);
     if ((v & m) != m) ones = false;
   }
-  if (__ballot(!ones) && lane_id() == 0) atomicMin(&a.first_row[plane], row);
+  // (an atomic only below the current minimum: every row of a dense plane qualifies, and as many
+  // same-address atomics would serialise the launch)
+  if (__ballot(!ones) && lane_id() == 0 &&
+      row < __hip_atomic_load(&a.first_row[plane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMin(&a.first_row[plane], row);
 }
 
 __global__ __launch_bounds__(256) void k_dec_eg_rows(DecArgs a) {
@@ -335,7 +373,7 @@ void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t s
   const uint64_t nrows = (uint64_t)rows * nplanes;
   const uint32_t grid = (uint32_t)((nrows + 3) / 4);
   if (coder == 0) {
-    k_dec_golomb_rows<<<grid, 64 * kDecWaves, 0, s>>>(a);
+    k_dec_golomb_lanes<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
   } else {
     (void)hipMemsetAsync(a.first_row, 0xff, (size_t)nplanes * 4, s);
     k_dec_eg_first<<<grid, 256, 0, s>>>(a);

@@ -21,8 +21,9 @@
 
 namespace bic {
 
-__constant__ uint8_t kEgJ[32] = {0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3,
-                                 4, 4, 5, 5, 6, 6, 7, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+// EGLUT = J[] (eg.cpp:2-10: 0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,5,5,6,6,7,7,8,9,...,15) in closed
+// form: a table indexed by a per-lane state would be a dependent memory load per block step
+__device__ __forceinline__ uint32_t eg_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
 constexpr uint32_t kFresh = 32;  // eg.h:9: index 0, block size 1, g = 1
 
 struct EgadArgs {
@@ -48,13 +49,13 @@ __device__ __forceinline__ uint32_t eg_run(uint32_t i, uint32_t len, bool eol, u
                                            uint32_t& g, uint32_t& rem) {
   m = 0;
   for (;;) {
-    const uint32_t B = i == kFresh ? 1u : 1u << kEgJ[i];
+    const uint32_t B = i == kFresh ? 1u : 1u << eg_j(i);
     if (len < B) break;
     len -= B;
     ++m;
     i = i == kFresh ? 1u : (i < 31 ? i + 1 : 31u);
   }
-  g = i == kFresh ? 1u : kEgJ[i];
+  g = i == kFresh ? 1u : eg_j(i);
   rem = len;
   nbits = m + 1 + (eol ? 0u : g);
   if (!eol) i = (i == kFresh || i == 0) ? 0u : i - 1;
@@ -62,21 +63,27 @@ __device__ __forceinline__ uint32_t eg_run(uint32_t i, uint32_t len, bool eol, u
 }
 
 // The runs of one row: f(len, eol) per run, from the residual computed word by
-// word (med of the row and the row above, pred.cpp:3-15), four words loaded ahead.
+// word (med of the row and the row above, pred.cpp:3-15); the next four words' loads are in flight
+// while four are used (uniform across the wave: every lane's row has the same words).
 template <typename F>
 __device__ __forceinline__ void row_runs(const EgadArgs& a, uint32_t plane, uint32_t row, F&& f) {
   const uint64_t* cur = a.planes + (uint64_t)plane * a.plane_words + (uint64_t)row * a.wpr;
   const uint64_t* up = row ? cur - a.wpr : nullptr;
   uint64_t dcarry = 0;
   int64_t last = -1;
-  for (uint32_t w0 = 0; w0 < a.used; w0 += 4) {
-    uint64_t p[4], u[4];
+  uint64_t p[4], u[4];  // this group's words; the next group's loads are in flight while it is used
+  auto load = [&](uint32_t w0, uint64_t (&pp)[4], uint64_t (&uu)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t w = min(w0 + q, a.used - 1);
-      p[q] = cur[w];
-      u[q] = (a.predict && up) ? up[w] : 0;
+      pp[q] = cur[w];
+      uu[q] = (a.predict && up) ? up[w] : 0;
     }
+  };
+  load(0, p, u);
+  for (uint32_t w0 = 0; w0 < a.used; w0 += 4) {
+    uint64_t np[4], nu[4];
+    if (w0 + 4 < a.used) load(w0 + 4, np, nu);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t w = w0 + q;
@@ -96,6 +103,11 @@ __device__ __forceinline__ void row_runs(const EgadArgs& a, uint32_t plane, uint
         f((uint32_t)(j - last - 1), false);
         last = j;
       }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      p[q] = np[q];
+      u[q] = nu[q];
     }
   }
   f((uint32_t)((int64_t)a.cols - 1 - last), true);
