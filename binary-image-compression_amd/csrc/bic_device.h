@@ -547,6 +547,27 @@ struct LdsSink {
   __device__ __forceinline__ void bit(uint32_t off) { orw(off >> 5, 0x80000000u >> (off & 31)); }
 };
 
+// A row image of 64-bit LDS words (bit 64 i + b at significance 63 - b of word i), OR'd with
+// ds_or_b64: a lane's string (<= 128 bits at any offset) lands in at most three words.
+__device__ __forceinline__ void lds_or64(uint64_t* img, uint32_t i, uint64_t v) {
+  if (v) atomicOr(reinterpret_cast<unsigned long long*>(img + i), (unsigned long long)v);
+}
+// write_row for a 64-bit LDS image (bic_fused.hip place128_64, bic_egad.hip): output word t of the row holds image bits
+// [64 t - G % 64, 64 t - G % 64 + 64): two LDS words and a funnel shift.
+__device__ __forceinline__ void write_row64(const uint64_t* img, uint64_t L, uint64_t G, uint64_t* out,
+                                            uint64_t* frag) {
+  const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6;
+  const uint32_t nw = (uint32_t)(w1 - w0 + 1), g = (uint32_t)(G & 63);
+  const bool head_whole = g == 0, tail_whole = ((G + L) & 63) == 0;
+  for (uint32_t t = lane_id(); t < nw; t += 64) {
+    const uint64_t cur = img[t], prev = t ? img[t - 1] : 0ull;
+    const uint64_t v = g ? (prev << (64 - g)) | (cur >> g) : cur;
+    const bool whole = (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
+    if (whole) out[w0 + t] = bswap64(v);
+    else frag[t == 0 ? 0 : 1] = v;
+  }
+}
+
 struct GlobalSink {
   unsigned long long* buf;  // big-endian 64-bit words
   uint64_t idx, cur;

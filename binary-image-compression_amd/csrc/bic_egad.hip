@@ -25,6 +25,8 @@ namespace bic {
 // form: a table indexed by a per-lane state would be a dependent memory load per block step
 __device__ __forceinline__ uint32_t eg_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
 constexpr uint32_t kFresh = 32;  // eg.h:9: index 0, block size 1, g = 1
+constexpr uint32_t kIdent = 0xFF;  // a lane without runs: its map is the identity
+constexpr uint32_t kUnk = 0xFE;    // a start state not known yet
 
 struct EgadArgs {
   uint32_t rows, cols, wpr, used, nplanes;
@@ -42,6 +44,15 @@ struct EgadArgs {
   uint64_t slot;     // words per plane
   uint64_t* bits;    // per plane
   uint32_t* flags;
+  // wave-per-row form (rows of <= 256 words): per (row, lane) the lane's state map at 0 and 31
+  // (kIdent: the lane holds no run), its start state and its bits; the rows whose codewords do not
+  // fit the LDS image are listed for the thread-per-row emission
+  uint8_t* lane_lo;
+  uint8_t* lane_hi;
+  uint8_t* lane_st;
+  uint32_t* lane_bits;
+  uint32_t* slow_n;
+  uint32_t* slow_ids;
 };
 
 // One run from state i: bits of its codeword, the new state. (eg.cpp:20-37 with incBlockSize.)
@@ -120,40 +131,53 @@ __global__ __launch_bounds__(256) void k_egad_map(EgadArgs a) {
   uint32_t lo = 0, hi = 31;
   row_runs(a, plane, row, [&](uint32_t len, bool eol) {
     uint32_t nb, m, g, rem;
+    const bool same = hi == lo;  // met: one trajectory from here on
     lo = eg_run(lo, len, eol, nb, m, g, rem);
-    if (hi != lo) hi = eg_run(hi, len, eol, nb, m, g, rem);
+    hi = same ? lo : eg_run(hi, len, eol, nb, m, g, rem);
   });
   a.lo_end[id] = (uint8_t)lo;
   a.hi_end[id] = (uint8_t)hi;
 }
 
-// One wave per plane: the row start states in order, 64 rows' end points loaded at a time.
+// One wave per plane: the row start states in order, 64 rows per step. Row q of a step starts at
+// F_{q-1}'s constant end when that map is constant (every lane at once); the others, in order, from
+// the row before's start (0 or 31: its map's ends; else a walk of that row, all lanes the same walk).
+__device__ __forceinline__ uint32_t egad_apply(const EgadArgs& a, uint32_t plane, uint32_t row, uint32_t s, uint32_t lo,
+                                               uint32_t hi) {
+  if (lo == hi || s == 0 || s == kFresh) return lo;
+  if (s == 31) return hi;
+  uint32_t t = s;
+  row_runs(a, plane, row, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    t = eg_run(t, len, eol, nb, m, g, rem);
+  });
+  return t;
+}
 __global__ __launch_bounds__(64) void k_egad_resolve(EgadArgs a) {
   const uint32_t plane = blockIdx.x;
   const int lane = lane_id();
   const uint64_t base = (uint64_t)plane * a.rows;
-  uint32_t s = 0;  // the map state of the row start (a fresh coder steps like index 0)
+  uint32_t s = kFresh;  // the start of the step's first row
   for (uint32_t r0 = 0; r0 < a.rows; r0 += 64) {
     const uint32_t r = r0 + lane;
-    const uint32_t lo = r < a.rows ? a.lo_end[base + r] : 0, hi = r < a.rows ? a.hi_end[base + r] : 0;
-    const uint32_t n = min(64u, a.rows - r0);
-    for (uint32_t q = 0; q < n; ++q) {
-      const uint32_t row = r0 + q;
-      if (lane == 0) a.start[base + row] = row == 0 ? (uint8_t)kFresh : (uint8_t)s;
-      const uint32_t l = (uint32_t)__shfl((int)lo, (int)q), h = (uint32_t)__shfl((int)hi, (int)q);
-      if (l == h || s == 0) {
-        s = l;
-      } else if (s == 31) {
-        s = h;
-      } else {  // F_r is not constant here: walk the row from s (all lanes, the same walk)
-        uint32_t t = s;
-        row_runs(a, plane, row, [&](uint32_t len, bool eol) {
-          uint32_t nb, m, g, rem;
-          t = eg_run(t, len, eol, nb, m, g, rem);
-        });
-        s = t;
-      }
+    const bool in = r < a.rows;
+    const uint32_t lo = in ? a.lo_end[base + r] : 0, hi = in ? a.hi_end[base + r] : 0;
+    const uint32_t plo = (uint32_t)dpp_or<0x138>((int)kUnk, (int)(lo == hi ? lo : kUnk));  // row r - 1's constant end
+    uint32_t st = lane == 0 ? s : plo;
+    for (uint64_t unk = __ballot(in && st == kUnk); unk; unk = __ballot(in && st == kUnk)) {
+      const int q = __builtin_ctzll(unk);  // rows before it are known
+      const uint32_t ps = (uint32_t)__builtin_amdgcn_readlane((int)st, q - 1);
+      const uint32_t pl = (uint32_t)__builtin_amdgcn_readlane((int)lo, q - 1);
+      const uint32_t ph = (uint32_t)__builtin_amdgcn_readlane((int)hi, q - 1);
+      const uint32_t v = egad_apply(a, plane, r0 + q - 1, ps, pl, ph);
+      if (lane == q) st = v;
     }
+    if (in) a.start[base + r] = (uint8_t)st;
+    const uint32_t n = min(64u, a.rows - r0);
+    const uint32_t ls = (uint32_t)__builtin_amdgcn_readlane((int)st, n - 1);
+    const uint32_t ll = (uint32_t)__builtin_amdgcn_readlane((int)lo, n - 1);
+    const uint32_t lh = (uint32_t)__builtin_amdgcn_readlane((int)hi, n - 1);
+    s = egad_apply(a, plane, r0 + n - 1, ls, ll, lh);
   }
 }
 
@@ -197,9 +221,7 @@ __global__ __launch_bounds__(1024) void k_egad_scan(EgadArgs a) {
   if (threadIdx.x == 0) a.bits[plane] = carry;
 }
 
-__global__ __launch_bounds__(256) void k_egad_emit(EgadArgs a) {
-  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (id >= (uint64_t)a.rows * a.nplanes) return;
+__device__ void egad_emit_row(const EgadArgs& a, uint64_t id) {
   const uint64_t L = a.len[id];
   if (L == 0) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
@@ -242,11 +264,259 @@ __global__ __launch_bounds__(256) void k_egad_emit(EgadArgs a) {
   });
   if (fill) flush();
 }
+__global__ __launch_bounds__(256) void k_egad_emit(EgadArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id < (uint64_t)a.rows * a.nplanes) egad_emit_row(a, id);
+}
+
+// ------------------------------------------------------------------------------------------
+// Wave-per-row form (rows of <= 256 words): lane l holds the WPL consecutive words l WPL .. and
+// the runs whose 1 lies in them (plus the end-of-row run on the lane of the row's last word), so a
+// lane's serial chain is ~WPL * 32 runs instead of the row's ~8,192. Each lane's map is walked from
+// 0 and from 31; maps are monotone, so equal ends make it constant, and the lanes' start states
+// follow from a few rounds of composition (a lane walks only when its map is not constant and its
+// start is neither 0 nor 31). The rows' maps then feed the per-plane resolve as before.
+constexpr uint32_t kEgImg = 384;   // u64 words of row image per wave (24,576 bits)
+
+template <int WPL>
+struct EgLane {
+  uint64_t R[WPL];
+  uint32_t w0;  // first word of the lane
+  int jp;       // column of the row's last 1 before the lane's words (-1: none)
+  bool eol;     // the lane holds the row's last word: it ends with the end-of-row run
+};
+
+template <int WPL>
+__device__ __forceinline__ EgLane<WPL> eg_lane_load(const EgadArgs& a, uint32_t plane, uint32_t row) {
+  EgLane<WPL> L;
+  const int lane = lane_id();
+  L.w0 = (uint32_t)lane * WPL;
+  const uint64_t* cur = a.planes + (uint64_t)plane * a.plane_words + (uint64_t)row * a.wpr;
+  const bool pr = a.predict && row;
+  uint64_t D[WPL];
+#pragma unroll
+  for (int i = 0; i < WPL; ++i) {
+    const uint32_t w = L.w0 + i;
+    const uint32_t wc = w < a.used ? w : a.used - 1;
+    const uint64_t p = cur[wc];
+    D[i] = pr ? p ^ (cur - a.wpr)[wc] : p;
+  }
+  const uint64_t dl = wave_shr1_u64(D[WPL - 1]);  // the D word left of the lane (lane 0: 0)
+  int last = -1;
+#pragma unroll
+  for (int i = 0; i < WPL; ++i) {
+    const uint32_t w = L.w0 + i;
+    uint64_t x = D[i];
+    if (a.predict) {
+      x = D[i] ^ ((D[i] >> 1) | ((i ? D[i - 1] : dl) << 63));
+      if (row == 0 && w == 0) x &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+    }
+    x = w < a.used ? (w == a.used - 1 ? x & a.trail : x) : 0ull;
+    L.R[i] = x;
+    if (x) last = (int)(w * 64 + 63 - __builtin_ctzll(x));
+  }
+  L.jp = dpp_or<0x138>(-1, wave_incl_max(last));
+  L.eol = (a.used - 1) / WPL == (uint32_t)lane;
+  return L;
+}
+
+// f(len, eol) for every run of the lane, in order
+template <int WPL, typename F>
+__device__ __forceinline__ void eg_lane_runs(const EgLane<WPL>& L, uint32_t cols, F&& f) {
+  int prev = L.jp;
+#pragma unroll
+  for (int i = 0; i < WPL; ++i) {
+    uint64_t x = L.R[i];
+    while (x) {
+      const int cz = __builtin_clzll(x);
+      x &= ~(BIC_MSB >> cz);
+      const int j = (int)((L.w0 + i) * 64) + cz;
+      f((uint32_t)(j - prev - 1), false);
+      prev = j;
+    }
+  }
+  if (L.eol) f((uint32_t)((int)cols - 1 - prev), true);
+}
+
+template <int WPL>
+__device__ __forceinline__ uint32_t eg_lane_walk(const EgLane<WPL>& L, uint32_t cols, uint32_t s) {
+  eg_lane_runs(L, cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    s = eg_run(s, len, eol, nb, m, g, rem);
+  });
+  return s;
+}
+
+// Every lane's start state for the row start s0 (lane 0 starts at s0): constant maps are known at
+// once; a round hands each known end to the next lane. Returns the lane's start; *end = its end.
+template <int WPL>
+__device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t cols, uint32_t lo, uint32_t hi,
+                                                  uint32_t s0, uint32_t* end) {
+  const int lane = lane_id();
+  const bool ident = lo == kIdent;
+  bool done = !ident && lo == hi;
+  uint32_t sout = done ? lo : kUnk;
+  uint32_t sin = lane == 0 ? s0 : kUnk;
+  for (;;) {
+    if (!done && sin != kUnk) {
+      if (ident) sout = sin;
+      else if (sin == 0 || sin == kFresh) sout = lo;  // (a fresh coder steps like index 0)
+      else if (sin == 31) sout = hi;
+      else sout = eg_lane_walk(L, cols, sin);
+      done = true;
+    }
+    const uint32_t prev = (uint32_t)dpp_or<0x138>((int)kUnk, (int)(done ? sout : kUnk));
+    if (lane > 0 && sin == kUnk) sin = prev;
+    if (__ballot(!done || sin == kUnk) == 0) break;
+  }
+  *end = sout;
+  return sin;
+}
+
+// The lanes' maps and the row's map F_r(0), F_r(31) (lane 63 carries the row's end).
+template <int WPL>
+__global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (id >= (uint64_t)a.rows * a.nplanes) return;  // whole wave
+  const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
+  const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
+  uint32_t lo = 0, hi = 31;
+  bool any = false;
+  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    any = true;
+    const bool same = hi == lo;  // met: one trajectory from here on (a branch: the wave skips the
+    lo = eg_run(lo, len, eol, nb, m, g, rem);  // second walk once every lane's two have met)
+    if (same) hi = lo;
+    else hi = eg_run(hi, len, eol, nb, m, g, rem);
+  });
+  if (!any) lo = hi = kIdent;
+  a.lane_lo[id * 64 + lane_id()] = (uint8_t)lo;
+  a.lane_hi[id * 64 + lane_id()] = (uint8_t)hi;
+  uint32_t e0, e31;
+  (void)eg_lane_chain(L, a.cols, lo, hi, 0, &e0);
+  (void)eg_lane_chain(L, a.cols, lo, hi, 31, &e31);
+  if (lane_id() == 63) {
+    a.lo_end[id] = (uint8_t)e0;
+    a.hi_end[id] = (uint8_t)e31;
+  }
+}
+
+// The row's bits from its start state: per lane its start and bits, the row's total.
+template <int WPL>
+__global__ __launch_bounds__(256) void k_egad_llen(EgadArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (id >= (uint64_t)a.rows * a.nplanes) return;
+  const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
+  const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
+  const uint32_t lo = a.lane_lo[id * 64 + lane_id()], hi = a.lane_hi[id * 64 + lane_id()];
+  uint32_t end;
+  const uint32_t s = eg_lane_chain(L, a.cols, lo, hi, a.start[id], &end);
+  uint32_t bits = 0, t = s;
+  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    t = eg_run(t, len, eol, nb, m, g, rem);
+    bits += nb;
+  });
+  a.lane_st[id * 64 + lane_id()] = (uint8_t)s;
+  a.lane_bits[id * 64 + lane_id()] = bits;
+  const uint64_t tot = wave_sum_u64(bits);
+  if (lane_id() == 0) a.len[id] = tot;
+}
+
+// Bits into a 64-bit LDS row image (MSB-first), words OR'd as a lane leaves them (lanes share at
+// most their first and last word).
+struct EgImgSink {
+  uint64_t* img;
+  uint32_t idx;
+  uint64_t cur;
+  __device__ __forceinline__ void flush() {
+    lds_or64(img, idx, cur);
+    cur = 0;
+  }
+  // the n (1..64) low bits of v at bit pos
+  __device__ __forceinline__ void put(uint32_t pos, uint64_t v, uint32_t n) {
+    const uint32_t i = pos >> 6, sh = pos & 63;
+    if (i != idx) {
+      flush();
+      idx = i;
+    }
+    if (n < 64) v &= (1ull << n) - 1ull;
+    if (sh + n <= 64) {
+      cur |= v << (64 - sh - n);
+    } else {
+      cur |= v >> (sh + n - 64);
+      flush();
+      idx = i + 1;
+      cur = v << (128 - sh - n);
+    }
+  }
+};
+
+template <int WPL>
+__global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
+  __shared__ __attribute__((aligned(16))) uint64_t imgs[4][kEgImg];
+  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (id >= (uint64_t)a.rows * a.nplanes) return;
+  const uint64_t Ltot = a.len[id];
+  if (Ltot == 0) return;  // past the slot (BIC_ENOSPC)
+  const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
+  const uint64_t G = a.boff[id];
+  if ((G & 63) + Ltot > (uint64_t)(kEgImg - 1) * 64) {  // too long for the image: the thread-per-row emission
+    if (lane_id() == 0) a.slow_ids[atomicAdd(a.slow_n, 1u)] = (uint32_t)id;
+    return;
+  }
+  uint64_t* img = imgs[threadIdx.x >> 6];
+  for (uint32_t i = lane_id(); i < kEgImg; i += 64) img[i] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
+  const uint32_t bits = a.lane_bits[id * 64 + lane_id()];
+  uint32_t pos = wave_incl_sum_u32(bits) - bits;  // the lane's first bit in the row
+  uint32_t s = a.lane_st[id * 64 + lane_id()];
+  EgImgSink k{img, 0, 0};
+  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    s = eg_run(s, len, eol, nb, m, g, rem);
+    while (m >= 64) {  // a '1' per full block
+      k.put(pos, ~0ull, 64);
+      pos += 64;
+      m -= 64;
+    }
+    if (m) {
+      k.put(pos, ~0ull, m);
+      pos += m;
+    }
+    if (eol) {
+      k.put(pos, 1ull, 1);  // end of row
+      pos += 1;
+    } else {
+      k.put(pos, (uint64_t)rem, 1 + g);  // '0' and the g-bit remainder
+      pos += 1 + g;
+    }
+  });
+  k.flush();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // image bit b = row bit b; write_row64 wants the row at bit G % 64 of image word 0's frame
+  write_row64(img, Ltot, G, a.out, a.frag + 2 * id);
+}
+
+// The rows too long for the LDS image, thread per row (k_egad_emit's body on a list).
+__device__ void egad_emit_row(const EgadArgs& a, uint64_t id);
+__global__ __launch_bounds__(256) void k_egad_emit_list(EgadArgs a) {
+  const uint32_t n = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) egad_emit_row(a, a.slow_ids[i]);
+}
 
 void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len, const uint64_t* frag, uint64_t* out,
                        uint32_t rows, uint64_t nrows);
 
-size_t egad_scratch_bytes(uint64_t nrows) { return nrows * (3 + 8 * 4) + 256; }
+// len, boff, frag[2] (u64), lo_end, hi_end, start (u8); per (row, lane): lane_lo, lane_hi, lane_st
+// (u8), lane_bits (u32); the slow-row list and its count
+size_t egad_scratch_bytes(uint64_t nrows) { return nrows * (3 + 8 * 4) + nrows * 64 * 7 + nrows * 4 + 512; }
 
 void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t nplanes,
                  int predict, uint64_t* out, uint64_t slot, uint64_t* bits, void* scratch, uint32_t* flags) {
@@ -268,17 +538,38 @@ void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t 
   uint8_t* b = reinterpret_cast<uint8_t*>(q);
   a.lo_end = b; b += n;
   a.hi_end = b; b += n;
-  a.start = b;
+  a.start = b; b += n;
+  a.lane_lo = b; b += n * 64;
+  a.lane_hi = b; b += n * 64;
+  a.lane_st = b; b += n * 64;
+  uintptr_t u = (reinterpret_cast<uintptr_t>(b) + 15) & ~(uintptr_t)15;
+  a.lane_bits = reinterpret_cast<uint32_t*>(u);
+  a.slow_ids = a.lane_bits + n * 64;
+  a.slow_n = a.slow_ids + n;
   a.out = out;
   a.slot = slot;
   a.bits = bits;
   a.flags = flags;
   const uint32_t grid = (uint32_t)((n + 255) / 256);
-  k_egad_map<<<grid, 256, 0, s>>>(a);
-  k_egad_resolve<<<nplanes, 64, 0, s>>>(a);
-  k_egad_len<<<grid, 256, 0, s>>>(a);
-  k_egad_scan<<<nplanes, 1024, 0, s>>>(a);
-  k_egad_emit<<<grid, 256, 0, s>>>(a);
+  if (a.used > 256) {  // rows wider than 16384 columns: thread per row
+    k_egad_map<<<grid, 256, 0, s>>>(a);
+    k_egad_resolve<<<nplanes, 64, 0, s>>>(a);
+    k_egad_len<<<grid, 256, 0, s>>>(a);
+    k_egad_scan<<<nplanes, 1024, 0, s>>>(a);
+    k_egad_emit<<<grid, 256, 0, s>>>(a);
+  } else {  // wave per row (4 rows per workgroup)
+    const uint32_t wgrid = (uint32_t)((n + 3) / 4);
+    (void)hipMemsetAsync(a.slow_n, 0, 4, s);
+#define BIC_EGAD(W)                                   \
+  k_egad_lmap<W><<<wgrid, 256, 0, s>>>(a);            \
+  k_egad_resolve<<<nplanes, 64, 0, s>>>(a);           \
+  k_egad_llen<W><<<wgrid, 256, 0, s>>>(a);            \
+  k_egad_scan<<<nplanes, 1024, 0, s>>>(a);            \
+  k_egad_lemit<W><<<wgrid, 256, 0, s>>>(a);           \
+  k_egad_emit_list<<<256, 256, 0, s>>>(a);
+    if (a.used <= 64) { BIC_EGAD(1) } else if (a.used <= 128) { BIC_EGAD(2) } else { BIC_EGAD(4) }
+#undef BIC_EGAD
+  }
   launch_fixup_rows(s, a.boff, a.len, a.frag, out, rows, n);
 }
 

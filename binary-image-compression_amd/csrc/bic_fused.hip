@@ -399,11 +399,6 @@ __device__ __forceinline__ LaneEnc encode_word_k1b(uint64_t x, uint32_t w, int j
   return e;
 }
 
-// A row image of 64-bit LDS words (bit 64 i + b at significance 63 - b of word i), OR'd with
-// ds_or_b64: a lane's string (<= 128 bits at any offset) lands in at most three words.
-__device__ __forceinline__ void lds_or64(uint64_t* img, uint32_t i, uint64_t v) {
-  if (v) atomicOr(reinterpret_cast<unsigned long long*>(img + i), (unsigned long long)v);
-}
 __device__ __forceinline__ void place128_64(uint64_t* img, uint32_t off, uint64_t A, uint64_t B, uint32_t tlen) {
   if (!tlen) return;
   const uint32_t i = off >> 6, sh = off & 63;
@@ -589,22 +584,6 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
     if (a < 0) v >>= -a;
     if (t != 0 && t != (uint32_t)nw - 1) out[w0 + t] = bswap64(v);
     else if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
-    else frag[t == 0 ? 0 : 1] = v;
-  }
-}
-
-// write_row for a 64-bit LDS image (place128_64): output word t of the row holds image bits
-// [64 t - G % 64, 64 t - G % 64 + 64): two LDS words and a funnel shift.
-__device__ __forceinline__ void write_row64(const uint64_t* img, uint64_t L, uint64_t G, uint64_t* out,
-                                            uint64_t* frag) {
-  const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6;
-  const uint32_t nw = (uint32_t)(w1 - w0 + 1), g = (uint32_t)(G & 63);
-  const bool head_whole = g == 0, tail_whole = ((G + L) & 63) == 0;
-  for (uint32_t t = lane_id(); t < nw; t += 64) {
-    const uint64_t cur = img[t], prev = t ? img[t - 1] : 0ull;
-    const uint64_t v = g ? (prev << (64 - g)) | (cur >> g) : cur;
-    const bool whole = (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
-    if (whole) out[w0 + t] = bswap64(v);
     else frag[t == 0 ? 0 : 1] = v;
   }
 }
