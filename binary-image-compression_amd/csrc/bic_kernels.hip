@@ -289,13 +289,163 @@ __global__ __launch_bounds__(kBlock) void k_med_kstat(Geom g, const uint64_t* __
   }
 }
 
+// Rows of <= 64 words (C4: 4096 columns): four rows per wave, one per 16-lane DPP row, lane q of a
+// group owning words 4q .. 4q + 3. The row's scans and reductions then run inside a DPP row (4
+// steps instead of 6, and one pass for four rows): ~4x fewer instructions per row than one row per
+// wave with one word per lane, where the record's scan and reductions dominate.
+template <int CTRL>
+__device__ __forceinline__ int dpp16(int old, int v) {  // inside a 16-lane row; invalid sources read old
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t row16_incl_sum(uint32_t x) {
+  x += (uint32_t)dpp16<0x111>(0, (int)x);
+  x += (uint32_t)dpp16<0x112>(0, (int)x);
+  x += (uint32_t)dpp16<0x114>(0, (int)x);
+  x += (uint32_t)dpp16<0x118>(0, (int)x);
+  return x;
+}
+__device__ __forceinline__ int row16_incl_max(int x) {
+  x = max(x, dpp16<0x111>(INT_MIN, x));
+  x = max(x, dpp16<0x112>(INT_MIN, x));
+  x = max(x, dpp16<0x114>(INT_MIN, x));
+  x = max(x, dpp16<0x118>(INT_MIN, x));
+  return x;
+}
+// every lane of the 16-lane row gets the row's max / min / sum (quad swaps, half mirror, mirror)
+__device__ __forceinline__ int row16_max(int x) {
+  x = max(x, dpp16<0xB1>(x, x));
+  x = max(x, dpp16<0x4E>(x, x));
+  x = max(x, dpp16<0x141>(x, x));
+  x = max(x, dpp16<0x140>(x, x));
+  return x;
+}
+__device__ __forceinline__ int row16_min(int x) {
+  x = min(x, dpp16<0xB1>(x, x));
+  x = min(x, dpp16<0x4E>(x, x));
+  x = min(x, dpp16<0x141>(x, x));
+  x = min(x, dpp16<0x140>(x, x));
+  return x;
+}
+__device__ __forceinline__ uint32_t row16_sum(uint32_t x) {
+  x += (uint32_t)dpp16<0xB1>(0, (int)x);
+  x += (uint32_t)dpp16<0x4E>(0, (int)x);
+  x += (uint32_t)dpp16<0x141>(0, (int)x);
+  x += (uint32_t)dpp16<0x140>(0, (int)x);
+  return x;
+}
+
+template <int RPW, bool PREDICT, bool V16>
+__global__ __launch_bounds__(kBlock) void k_med_kstat16(Geom g, const uint64_t* __restrict__ planes,
+                                                        uint32_t* __restrict__ sones, int4* __restrict__ krec,
+                                                        uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
+  if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
+  const int lane = lane_id(), q = lane & 15, grp = lane >> 4;
+  const uint32_t wpp = (g.rows + RPW - 1) / RPW;  // waves per plane
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  if (gw >= (uint64_t)wpp * g.nplanes) return;  // whole wave
+  const uint32_t plane = (uint32_t)(gw / wpp), r0 = (uint32_t)(gw % wpp) * RPW;
+  const uint64_t* pl = planes + (uint64_t)plane * g.plane_words;
+  const uint32_t w0 = 4 * (uint32_t)q;
+  const uint32_t nr = min((uint32_t)RPW, g.rows - r0);
+  // the group's row and the row above; the next four rows' loads are in flight while these are used
+  auto load = [&](uint32_t rb, uint64_t (&P)[4], uint64_t (&U)[4]) {
+    const uint32_t rr = rb + (uint32_t)grp < nr ? r0 + rb + (uint32_t)grp : r0;
+    if constexpr (V16) {  // 16-byte aligned rows holding whole lanes: two 16-byte loads per row
+      const uint32_t wc = w0 < g.used ? w0 : 0;
+      const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(pl + (uint64_t)rr * g.wpr + wc);
+      const ulonglong2 a = p2[0], b = p2[1];
+      P[0] = a.x; P[1] = a.y; P[2] = b.x; P[3] = b.y;
+      if (PREDICT && rr) {
+        const ulonglong2* u2 = reinterpret_cast<const ulonglong2*>(pl + (uint64_t)(rr - 1) * g.wpr + wc);
+        const ulonglong2 c = u2[0], d = u2[1];
+        U[0] = c.x; U[1] = c.y; U[2] = d.x; U[3] = d.y;
+      } else {
+        U[0] = U[1] = U[2] = U[3] = 0;
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t w = w0 + i, wc = w < g.used ? w : g.used - 1;
+      P[i] = pl[(uint64_t)rr * g.wpr + wc];
+      U[i] = (PREDICT && rr) ? pl[(uint64_t)(rr - 1) * g.wpr + wc] : 0ull;
+    }
+  };
+  uint64_t P[4], U[4];
+  load(0, P, U);
+  for (uint32_t rb = 0; rb < nr; rb += 4) {
+    const uint32_t row = r0 + rb + (uint32_t)grp;
+    const bool in = rb + (uint32_t)grp < nr;
+    const uint32_t rr = in ? row : r0;  // (out-of-range groups recompute a valid row, store nothing)
+    uint64_t NP[4], NU[4];
+    if (rb + 4 < nr) load(rb + 4, NP, NU);
+    uint64_t D[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) D[i] = P[i] ^ U[i];
+    // D word left of the lane: lane q - 1's last (q = 0: 0), inside the 16-lane row
+    const uint64_t dl = ((uint64_t)(uint32_t)dpp16<0x111>(0, (int)(uint32_t)(D[3] >> 32)) << 32) |
+                        (uint32_t)dpp16<0x111>(0, (int)(uint32_t)D[3]);
+    LaneK k;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t w = w0 + i;
+      uint64_t R = D[i];
+      if constexpr (PREDICT) {
+        R = D[i] ^ ((D[i] >> 1) | ((i ? D[i - 1] : dl) << 63));
+        if (rr == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+      }
+      R = w < g.used ? (w == g.used - 1 ? R & g.trail : R) : 0;
+      lanek_word(k, R, (int32_t)(w * 64));
+    }
+    // the row's record (lanek_store inside the 16-lane row)
+    const uint32_t inc = row16_incl_sum(k.ones);
+    const int32_t base = (int32_t)(inc - k.ones);
+    const int mx = row16_incl_max(k.last);
+    const int32_t before = dpp16<0x111>(-1, mx);  // the last 1 of the lanes before (-1: none)
+    uint32_t chg = k.chg;
+    int32_t first = -1;
+    if (k.ones) {
+      if (before >= 0) chg += (uint32_t)((before ^ k.first) & 1);
+      else first = k.first;
+    }
+    const int32_t q0 = row16_max(k.ones ? k.q0 - 2 * base : -kNoOnes);
+    const int32_t qh = row16_max(k.ones ? k.qh - 3 * base : -kNoOnes);
+    const int32_t ql = row16_min(k.ones ? k.ql - 2 * base : kNoOnes);
+    const uint32_t c = row16_sum(chg);
+    const int32_t f = row16_max(first);
+    const uint32_t tot = row16_sum(k.ones);
+    const int32_t last = row16_max(k.last);
+    if (q == 0 && in) {
+      const uint64_t id = (uint64_t)plane * g.rows + row;
+      krec[id] = make_int4(q0, qh, ql, (int32_t)(tot | (c << 16)));
+      kpos[id] = ((uint32_t)f & 0xffffu) | ((uint32_t)last << 16);
+      sones[id] = tot;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      P[i] = NP[i];
+      U[i] = NU[i];
+    }
+  }
+}
+
 void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint32_t* sones,
                      int4* krec, uint32_t* kpos, uint32_t* zero) {
   constexpr int RPW = 8;
   const uint32_t wpp = (g.rows + RPW - 1) / RPW;
   const uint32_t grid = (uint32_t)(((uint64_t)wpp * g.nplanes + kWaves - 1) / kWaves);
 #define BIC_KST(LW, P) k_med_kstat<LW, RPW, P><<<grid, kBlock, 0, s>>>(g, planes, sones, krec, kpos, zero)
-  if (g.used <= 64) { if (predict) BIC_KST(1, true); else BIC_KST(1, false); }
+  if (g.used <= 64) {  // four rows per wave
+    constexpr int R16 = 16;
+    const uint32_t wpp16 = (g.rows + R16 - 1) / R16;
+    const uint32_t grid16 = (uint32_t)(((uint64_t)wpp16 * g.nplanes + kWaves - 1) / kWaves);
+    // 16-byte loads when every lane's four words lie inside the row pitch at 16-byte alignment
+    const bool v16 = g.wpr % 4 == 0 && g.used % 4 == 0 && reinterpret_cast<uintptr_t>(planes) % 16 == 0;
+#define BIC_K16(P, V) k_med_kstat16<R16, P, V><<<grid16, kBlock, 0, s>>>(g, planes, sones, krec, kpos, zero)
+    if (predict) { if (v16) BIC_K16(true, true); else BIC_K16(true, false); }
+    else { if (v16) BIC_K16(false, true); else BIC_K16(false, false); }
+#undef BIC_K16
+  }
   else if (g.used <= 128) { if (predict) BIC_KST(2, true); else BIC_KST(2, false); }
   else { if (predict) BIC_KST(4, true); else BIC_KST(4, false); }
 #undef BIC_KST
