@@ -1334,12 +1334,12 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
   pre += btot;
   if constexpr (ONES) {
     bool walks[kScanPer];  // classify every row of the thread first: their record loads overlap
+    uint64_t p = pre;
 #pragma unroll
     for (uint32_t i = 0; i < kScanPer; ++i) {
       const uint32_t r = r0 + i;
-      const uint64_t p = pre + (i ? v[0] : 0) + (i > 1 ? v[1] : 0);
-      static_assert(kScanPer <= 2, "prefix above covers two rows");
       walks[i] = CLASSIFY && r < g.rows && row_class(a, base + r, r, (uint32_t)p);
+      p += v[i];
     }
 #pragma unroll
     for (uint32_t i = 0; i < kScanPer; ++i) {
