@@ -56,15 +56,33 @@ struct EgadArgs {
 };
 
 // One run from state i: bits of its codeword, the new state. (eg.cpp:20-37 with incBlockSize.)
+// The blocks go band by band: states with one block size (0-3: 1, 4-7: 2, ..., 16-17: 16, ...,
+// 24, 25, ...: one state each, 31 saturating) are crossed in one step of len >> J blocks, so a run
+// costs one step per band it crosses instead of one per block.
 __device__ __forceinline__ uint32_t eg_run(uint32_t i, uint32_t len, bool eol, uint32_t& nbits, uint32_t& m,
                                            uint32_t& g, uint32_t& rem) {
   m = 0;
-  for (;;) {
-    const uint32_t B = i == kFresh ? 1u : 1u << eg_j(i);
-    if (len < B) break;
-    len -= B;
-    ++m;
-    i = i == kFresh ? 1u : (i < 31 ? i + 1 : 31u);
+  if (i == kFresh && len) {  // a fresh coder's block is 1 zero, after which it is at index 1
+    --len;
+    m = 1;
+    i = 1;
+  }
+  if (i != kFresh) {
+    for (;;) {
+      const uint32_t j = eg_j(i);
+      const uint32_t end = i < 16 ? (i | 3u) + 1 : (i < 24 ? (i | 1u) + 1 : i + 1);  // first state past the band
+      const uint32_t q = len >> j;                                                     // blocks the run holds
+      if (i == 31) {  // saturated: every block is 2^15
+        m += q;
+        len -= q << j;
+        break;
+      }
+      const uint32_t room = end - i, k = min(q, room);
+      m += k;
+      len -= k << j;
+      i += k;
+      if (k < room) break;  // stopped inside the band: len < its block size
+    }
   }
   g = i == kFresh ? 1u : eg_j(i);
   rem = len;
