@@ -311,14 +311,17 @@ __device__ __forceinline__ EgLane<WPL> eg_lane_load(const EgadArgs& a, uint32_t 
   L.w0 = (uint32_t)lane * WPL;
   const uint64_t* cur = a.planes + (uint64_t)plane * a.plane_words + (uint64_t)row * a.wpr;
   const bool pr = a.predict && row;
-  uint64_t D[WPL];
+  const uint64_t* up = pr ? cur - a.wpr : cur;  // (row 0: loaded and not used, so no load sits in a branch)
+  uint64_t D[WPL], U[WPL];
 #pragma unroll
   for (int i = 0; i < WPL; ++i) {
     const uint32_t w = L.w0 + i;
     const uint32_t wc = w < a.used ? w : a.used - 1;
-    const uint64_t p = cur[wc];
-    D[i] = pr ? p ^ (cur - a.wpr)[wc] : p;
+    D[i] = cur[wc];
+    U[i] = up[wc];
   }
+#pragma unroll
+  for (int i = 0; i < WPL; ++i) D[i] = pr ? D[i] ^ U[i] : D[i];
   const uint64_t dl = wave_shr1_u64(D[WPL - 1]);  // the D word left of the lane (lane 0: 0)
   int last = -1;
 #pragma unroll
