@@ -307,3 +307,28 @@ def test_encode_gray_packed(ctx, oracle, staged, plane0, nplanes):
         exp, eoff = _packed_expect(oracle, P, cols, 1, coder)
         assert list(as_u64(off)) == eoff
         assert as_u64(out)[:eoff[-1]].tobytes() == exp
+
+
+@pytest.mark.parametrize("rows,cols,wpr", [(37, 4096, 72), (33, 3968, 64), (19, 4000, 63), (50, 256, 4)])
+@pytest.mark.parametrize("p", [0.5, 0.05])
+def test_narrow_rows_pitched(ctx, oracle, rows, cols, wpr, p):
+    """rows of <= 64 words through the staged encoder's four-rows-per-wave count pass: row pitches
+    wider than the row (16-byte loads when the pitch and the row are multiples of 4 words, single
+    words otherwise), row counts that leave partial 16-row wave blocks and 4-row groups"""
+    used = (cols + 63) // 64
+    P = np.stack([oracle.gen_plane(0x16 + rows + k, p, rows, cols) for k in range(3)])
+    Q = np.zeros((3, rows, wpr), np.uint64)
+    Q[:, :, :used] = P
+    Q[:, :, used:] = ONES  # pad words past the row must not be read as pixels
+    ctx.set_encoder("staged")
+    try:
+        (og, bg), (oe, be) = ctx.encode_planes2(ctx.to_dev(Q), cols, True)
+        ctx.sync()
+    finally:
+        ctx.set_encoder("auto")
+    for k in range(3):
+        for coder, out, bits in ((0, og, bg), (1, oe, be)):
+            eb, est, _ = oracle.encode_plane(P[k], cols, 1, coder)
+            nb = int(as_u64(bits)[k])
+            assert nb == eb, (k, coder)
+            assert stream_bytes(out[k], nb) == est.tobytes(), (k, coder)
