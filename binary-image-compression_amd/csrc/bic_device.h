@@ -547,6 +547,21 @@ struct LdsSink {
   __device__ __forceinline__ void bit(uint32_t off) { orw(off >> 5, 0x80000000u >> (off & 31)); }
 };
 
+// (hi:lo) >> sh, low 64 bits, for sh in 0..63: two v_alignbit_b32 (a 64-bit funnel shift) when sh
+// is wave-uniform, instead of two 64-bit shifts, an or and the sh == 0 select.
+__device__ __forceinline__ uint64_t funnel64(uint64_t hi, uint64_t lo, uint32_t sh) {
+  const uint32_t h1 = (uint32_t)(hi >> 32), h0 = (uint32_t)hi, l1 = (uint32_t)(lo >> 32), l0 = (uint32_t)lo;
+  uint32_t r1, r0;
+  if (sh < 32) {  // ({h0, l1, l0} >> sh)
+    r1 = __builtin_amdgcn_alignbit(h0, l1, sh);
+    r0 = __builtin_amdgcn_alignbit(l1, l0, sh);
+  } else {  // ({h1, h0, l1} >> (sh - 32))
+    r1 = __builtin_amdgcn_alignbit(h1, h0, sh - 32);
+    r0 = __builtin_amdgcn_alignbit(h0, l1, sh - 32);
+  }
+  return ((uint64_t)r1 << 32) | r0;
+}
+
 // A row image of 64-bit LDS words (bit 64 i + b at significance 63 - b of word i), OR'd with
 // ds_or_b64: a lane's string (<= 128 bits at any offset) lands in at most three words.
 __device__ __forceinline__ void lds_or64(uint64_t* img, uint32_t i, uint64_t v) {
@@ -561,7 +576,7 @@ __device__ __forceinline__ void write_row64(const uint64_t* img, uint64_t L, uin
   const bool head_whole = g == 0, tail_whole = ((G + L) & 63) == 0;
   for (uint32_t t = lane_id(); t < nw; t += 64) {
     const uint64_t cur = img[t], prev = t ? img[t - 1] : 0ull;
-    const uint64_t v = g ? (prev << (64 - g)) | (cur >> g) : cur;
+    const uint64_t v = funnel64(prev, cur, g);
     const bool whole = (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
     if (whole) out[w0 + t] = bswap64(v);
     else frag[t == 0 ? 0 : 1] = v;

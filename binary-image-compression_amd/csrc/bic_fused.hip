@@ -1102,6 +1102,7 @@ __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geo
   const uint64_t w0 = Ge >> 6, nw = ((Ge + Le - 1) >> 6) - w0 + 1;
   const uint32_t eolw = g.cols >> 6;
   const uint64_t eolbit = BIC_MSB >> (g.cols & 63);
+  const bool head_whole = sh == 0, tail_whole = ((Ge + Le) & 63) == 0;  // (only the first / last word can be shared)
   uint64_t carry = 0;
 #pragma unroll
   for (int t = 0; t <= WPL; ++t) {
@@ -1113,10 +1114,10 @@ __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geo
     uint64_t Xl = shfl_up_u64(X, 1);
     if (lane == 0) Xl = carry;
     carry = lane63_u64(X);
-    const uint64_t v = sh ? (Xl << (64 - sh)) | (X >> sh) : X;
+    const uint64_t v = funnel64(Xl, X, sh);
     if (j < nw) {
       const uint64_t wi = w0 + j;
-      if (word_complete(wi, Ge, Le)) out[wi] = bswap64(v);
+      if ((j != 0 || head_whole) && (j != nw - 1 || tail_whole)) out[wi] = bswap64(v);
       else frag[j == 0 ? 0 : 1] = v;
     }
   }
@@ -1898,7 +1899,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     // k_emit_rest (listed rows, latency bound: few workgroups) first, on the aux stream when there
     // is one, so that it can overlap the main launch, which skips the listed rows' parts
     const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
-    const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 16 / nwv);  // 16 waves per CU
+    const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 32 / nwv);  // 32 waves per CU (16: C4 +6 us; 4: C3 +30 us -- the listed rows are latency-bound)
     hipStream_t rs = s;
     if (kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
         hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
