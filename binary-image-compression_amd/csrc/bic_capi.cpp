@@ -5,6 +5,7 @@
 #include "bic.h"
 #include "bic_internal.h"
 
+#include <algorithm>
 #include <cctype>
 #include <cmath>
 #include <cstdio>
@@ -940,6 +941,94 @@ int bic_pbm_pack(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, 
   timed(ctx, "pbm_pack", [&] {
     bic::launch_pbm(ctx->cur, true, nullptr, raster, plane, nullptr, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr);
   });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+// ---- f4: GF(2) algebra -----------------------------------------------------------------------
+namespace {
+bool gf2_geom(size_t rows, size_t cols, size_t wpr) {
+  return rows <= 0x7fffffffu && cols <= 0x7fffff00u && wpr >= (cols + 63) / 64 && wpr <= 0xffffffffu;
+}
+}  // namespace
+
+int bic_gf2_transpose(bic_ctx* ctx, const uint64_t* src, size_t rows, size_t cols, size_t wpr, uint64_t* dst,
+                      size_t dst_wpr) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!gf2_geom(rows, cols, wpr) || !gf2_geom(cols, rows, dst_wpr)) return BIC_EINVAL;
+  if (!rows || !cols) return BIC_OK;
+  if (!src || !dst) return BIC_EINVAL;
+  timed(ctx, "gf2_transpose", [&] {
+    bic::launch_gf2_transpose(ctx->cur, src, (uint32_t)rows, (uint32_t)wpr, (uint32_t)((cols + 63) / 64),
+                              (uint32_t)cols, dst, (uint32_t)dst_wpr, (uint32_t)((rows + 63) / 64));
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+// mul_AB as the kernel; mul_AtB = transpose(A) then mul_AB; mul_ABt = A times the transpose of B's
+// whole words (its loop runs over A's blocks, binmat.cpp:586-588), stored for j < B.cols.
+int bic_gf2_mul(bic_ctx* ctx, int op, const uint64_t* A, size_t a_rows, size_t a_cols, size_t a_wpr,
+                const uint64_t* B, size_t b_rows, size_t b_cols, size_t b_wpr, uint64_t* C, size_t c_rows,
+                size_t c_cols, size_t c_wpr) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (!gf2_geom(a_rows, a_cols, a_wpr) || !gf2_geom(b_rows, b_cols, b_wpr) || !gf2_geom(c_rows, c_cols, c_wpr))
+    return BIC_EINVAL;
+  const uint32_t cw = (uint32_t)((c_cols + 63) / 64);
+  switch (op) {
+    case BIC_GF2_AB:
+      if (c_rows != a_rows || c_cols != b_cols || a_cols != b_rows) return BIC_EINVAL;
+      break;
+    case BIC_GF2_ATB:
+      if (c_rows != a_cols || c_cols != b_cols || a_rows != b_rows) return BIC_EINVAL;
+      break;
+    case BIC_GF2_ABT:
+      if (c_rows != a_rows || c_cols != b_rows || a_cols != b_cols) return BIC_EINVAL;
+      break;
+    case BIC_GF2_ATBT:
+      if (c_rows != a_cols || c_cols != b_rows || a_rows != b_cols) return BIC_EINVAL;
+      return BIC_OK;  // binmat.cpp:596-604: "FALTA!" -- C is returned unchanged
+    default:
+      return BIC_EINVAL;
+  }
+  if (!c_rows || !cw) return BIC_OK;
+  if (!A || !B || !C) return BIC_EINVAL;
+  if (op == BIC_GF2_AB) {
+    timed(ctx, "gf2_mul", [&] {
+      bic::launch_gf2_ab(ctx->cur, A, (uint32_t)a_rows, (uint32_t)a_wpr, (uint32_t)a_cols, B, (uint32_t)b_wpr, cw, C,
+                         (uint32_t)c_wpr, cw * 64u);
+    });
+    BIC_HIP(hipGetLastError());
+    return BIC_OK;
+  }
+  // the transposed operand: At (a_cols x a_rows) or B's whole words transposed (64 aw x b_rows)
+  const bool atb = op == BIC_GF2_ATB;
+  const uint32_t aw = (uint32_t)((a_cols + 63) / 64);
+  const uint64_t t_rows = atb ? a_cols : 64ull * aw, t_src_rows = atb ? a_rows : b_rows;
+  const uint32_t t_words = (uint32_t)((t_src_rows + 63) / 64);
+  uint64_t* T = nullptr;
+  if (t_rows && t_words) {
+    BIC_HIP(hipMallocAsync(reinterpret_cast<void**>(&T), (size_t)t_rows * t_words * 8, ctx->cur));
+    timed(ctx, "gf2_transpose", [&] {
+      if (atb)
+        bic::launch_gf2_transpose(ctx->cur, A, (uint32_t)a_rows, (uint32_t)a_wpr, aw, (uint32_t)a_cols, T, t_words,
+                                  t_words);
+      else
+        bic::launch_gf2_transpose(ctx->cur, B, (uint32_t)b_rows, (uint32_t)b_wpr, aw, (uint32_t)t_rows, T, t_words,
+                                  t_words);
+    });
+  }
+  timed(ctx, "gf2_mul", [&] {
+    if (atb)
+      bic::launch_gf2_ab(ctx->cur, T, (uint32_t)a_cols, t_words, (uint32_t)a_rows, B, (uint32_t)b_wpr, cw, C,
+                         (uint32_t)c_wpr, cw * 64u);
+    else  // cw == t_words (c_cols == b_rows); bits j >= b_rows of the product are 0
+      bic::launch_gf2_ab(ctx->cur, A, (uint32_t)a_rows, (uint32_t)a_wpr, (uint32_t)t_rows, T, t_words, cw, C,
+                         (uint32_t)c_wpr, (uint32_t)std::min<size_t>(b_cols, 64ull * cw));
+  });
+  if (T) (void)hipFreeAsync(T, ctx->cur);
   BIC_HIP(hipGetLastError());
   return BIC_OK;
 }

@@ -192,6 +192,12 @@ void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* ras
 void launch_raster_planes(hipStream_t s, const uint8_t* raster, int bpp, uint32_t rows, uint32_t cols, int plane0,
                           int nplanes, uint64_t* planes, uint32_t wpr);
 
+// GF(2) algebra (bic_gf2.hip)
+void launch_gf2_transpose(hipStream_t s, const uint64_t* src, uint32_t s_rows, uint32_t s_stride, uint32_t s_words,
+                          uint32_t ncols_out, uint64_t* dst, uint32_t d_stride, uint32_t d_words);
+void launch_gf2_ab(hipStream_t s, const uint64_t* A, uint32_t M, uint32_t a_stride, uint32_t kbits, const uint64_t* B,
+                   uint32_t b_stride, uint32_t nw, uint64_t* C, uint32_t c_stride, uint32_t nset);
+
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
 

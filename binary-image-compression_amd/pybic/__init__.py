@@ -29,7 +29,11 @@ EXPORTS = [
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
     "bic_bitplanes_u8_range", "bic_encode_gray_range", "bic_encode_planes_packed", "bic_encode_gray_packed",
     "bic_row_index", "bic_decode_planes", "bic_pgm_bitplanes", "bic_pnm_parse_header",
+    "bic_gf2_transpose", "bic_gf2_mul",
 ]
+
+# bic_gf2_mul ops (include/bic.h)
+GF2_AB, GF2_ATB, GF2_ABT, GF2_ATBT = 0, 1, 2, 3
 
 
 class PnmInfo(C.Structure):
@@ -110,6 +114,8 @@ def load(path=LIB_PATH):
     sig("bic_decode_planes", i32, [vp, i32, vp, sz, vp, vp, vp, i32, sz, sz, sz, i32, vp, vp])
     sig("bic_pgm_bitplanes", i32, [vp, vp, sz, sz, i32, i32, i32, vp, sz])
     sig("bic_pnm_parse_header", i32, [C.c_char_p, sz, C.POINTER(PnmInfo)])
+    sig("bic_gf2_transpose", i32, [vp, vp, sz, sz, sz, vp, sz])
+    sig("bic_gf2_mul", i32, [vp, i32, vp, sz, sz, sz, vp, sz, sz, sz, vp, sz, sz, sz])
     _lib = L
     return L
 
@@ -485,6 +491,22 @@ class Context:
         self._bind_stream()
         self._chk(self.lib.bic_pbm_pack(self.h, _p(plane), rows, cols, wpr, _p(raster)), "bic_pbm_pack")
         return raster
+
+    def gf2_transpose(self, M, cols, out=None):
+        """int64 matrix [rows, wpr] of `cols` bits -> its transpose [cols, ceil(rows/64)] (or `out`)."""
+        rows, wpr = M.shape
+        out = self.empty_i64(cols, (rows + 63) // 64) if out is None else out
+        self._bind_stream()
+        self._chk(self.lib.bic_gf2_transpose(self.h, _p(M), rows, cols, wpr, _p(out), out.shape[1]),
+                  "bic_gf2_transpose")
+        return out
+
+    def gf2_mul(self, op, A, a_cols, B, b_cols, C, c_cols):
+        """mul(A, At, B, Bt, C) over GF(2) in place on C (int64 [rows, wpr] device tensors)."""
+        self._bind_stream()
+        self._chk(self.lib.bic_gf2_mul(self.h, op, _p(A), A.shape[0], a_cols, A.shape[1], _p(B), B.shape[0], b_cols,
+                                       B.shape[1], _p(C), C.shape[0], c_cols, C.shape[1]), "bic_gf2_mul")
+        return C
 
     def pack_streams(self, slots, plane_bits, dst_words=None):
         n, slot_words = slots.shape

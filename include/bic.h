@@ -277,6 +277,27 @@ int bic_pnm_parse_header(const uint8_t* bytes, size_t n, bic_pnm_info* info);
 int bic_pgm_bitplanes(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, int maxval, int plane0,
                       int nplanes, uint64_t* planes, size_t wpr);
 
+/* ---- f4: binary_matrix algebra over GF(2) (binmat.cpp:199-214, 516-616) ---------------------
+ * Matrices are rows x cols bits in the plane layout (wpr >= ceil(cols/64) words per row, device
+ * memory). bic_gf2_transpose replaces transpose_to / get_transposed: dst (cols x rows, dst_wpr >=
+ * ceil(rows/64)) gets dst(j,i) = src(i,j); the ceil(rows/64) words of every dst row are written
+ * (bits past rows 0). bic_gf2_mul replaces mul(A, At, B, Bt, C) (binmat.cpp:606-616) with op =
+ * BIC_GF2_AB (mul_AB :516-542), BIC_GF2_ATB (mul_AtB :545-572), BIC_GF2_ABT (mul_ABt :575-594) or
+ * BIC_GF2_ATBT (mul_AtBt :596-604, not implemented there: C unchanged); the reference's asserts on
+ * the shapes become BIC_EINVAL. C's first ceil(c_cols/64) words per row are written; mul_ABt as
+ * written sets only bits j < b_cols of a row (0 for j >= b_rows) and keeps the others. Products
+ * over the whole words of their operands, as the reference's block loops (padding bits included
+ * where its loops include them). Scratch for the transposed operand is stream-ordered. */
+#define BIC_GF2_AB 0
+#define BIC_GF2_ATB 1
+#define BIC_GF2_ABT 2
+#define BIC_GF2_ATBT 3
+int bic_gf2_transpose(bic_ctx* ctx, const uint64_t* src, size_t rows, size_t cols, size_t wpr, uint64_t* dst,
+                      size_t dst_wpr);
+int bic_gf2_mul(bic_ctx* ctx, int op, const uint64_t* A, size_t a_rows, size_t a_cols, size_t a_wpr,
+                const uint64_t* B, size_t b_rows, size_t b_cols, size_t b_wpr, uint64_t* C, size_t c_rows,
+                size_t c_cols, size_t c_wpr);
+
 /* ---- kernel timing ------------------------------------------------------------------------
  * When enabled, every kernel launch of this ctx is bracketed by HIP events on the launch stream.
  * bic_prof_collect syncs, writes one line per kernel name ("name launches total_ms\n") into buf

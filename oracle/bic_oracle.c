@@ -700,3 +700,61 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
     if ((stream_match && bwm.overflow) || (stream_nomatch && bwn.overflow)) return -1;
     return 0;
 }
+
+/* ---- binary_matrix algebra over GF(2) ---------------------------------------------------- */
+
+static int gf2_bit(const uint64_t* M, size_t wpr, size_t i, size_t j) {
+    return (int)((M[i * wpr + j / 64] >> (63 - j % 64)) & 1u);
+}
+
+/* binmat.cpp:199-214: for every column j, copy_col_to (col cleared, bit i = A(i, j)) then set_row */
+void bo_gf2_transpose(const uint64_t* src, size_t rows, size_t cols, uint64_t* dst) {
+    const size_t swpr = (cols + 63) / 64, dwpr = (rows + 63) / 64;
+    for (size_t j = 0; j < cols; ++j) {
+        uint64_t* d = dst + j * dwpr;
+        for (size_t q = 0; q < dwpr; ++q) d[q] = 0;
+        for (size_t i = 0; i < rows; ++i)
+            if (gf2_bit(src, swpr, i, j)) d[i / 64] |= 0x8000000000000000ull >> (i % 64);
+    }
+}
+
+int bo_gf2_mul(int op, const uint64_t* A, size_t a_rows, size_t a_cols, const uint64_t* B, size_t b_rows,
+               size_t b_cols, uint64_t* C, size_t c_rows, size_t c_cols) {
+    const size_t aw = (a_cols + 63) / 64, bw = (b_cols + 63) / 64, cw = (c_cols + 63) / 64;
+    if (op == 0) {  /* mul_AB: C.clear(); for k, for i: if A(i,k) row i of C ^= row k of B */
+        if (c_rows != a_rows || c_cols != b_cols || a_cols != b_rows) return -1;
+        for (size_t q = 0; q < c_rows * cw; ++q) C[q] = 0;
+        for (size_t k = 0; k < b_rows; ++k)
+            for (size_t i = 0; i < a_rows; ++i)
+                if (gf2_bit(A, aw, i, k))
+                    for (size_t j = 0; j < bw; ++j) C[i * cw + j] ^= B[k * bw + j];
+        return 0;
+    }
+    if (op == 1) {  /* mul_AtB: for k < A.rows, for i < A.cols: if A(k,i) row i of C ^= row k of B */
+        if (c_rows != a_cols || c_cols != b_cols || a_rows != b_rows) return -1;
+        for (size_t q = 0; q < c_rows * cw; ++q) C[q] = 0;
+        for (size_t k = 0; k < a_rows; ++k)
+            for (size_t i = 0; i < a_cols; ++i)
+                if (gf2_bit(A, aw, k, i))
+                    for (size_t j = 0; j < bw; ++j) C[i * cw + j] ^= B[k * bw + j];
+        return 0;
+    }
+    if (op == 2) {  /* mul_ABt: C(i,j) = parity of XOR over A's blocks of A_ik & B_jk, j < B.cols */
+        if (c_rows != a_rows || c_cols != b_rows || a_cols != b_cols) return -1;
+        for (size_t i = 0; i < a_rows; ++i)
+            for (size_t j = 0; j < b_cols; ++j) {
+                uint64_t acc = 0;
+                for (size_t k = 0; k < aw; ++k) acc ^= A[i * aw + k] & (j < b_rows ? B[j * bw + k] : 0ull);
+                const size_t kc = i * cw + j / 64;
+                if (kc >= c_rows * cw) continue;  /* C.set past the storage: dropped */
+                const uint64_t m = 0x8000000000000000ull >> (j % 64);
+                if (__builtin_parityll(acc)) C[kc] |= m; else C[kc] &= ~m;
+            }
+        return 0;
+    }
+    if (op == 3) {  /* mul_AtBt: "FALTA!" */
+        if (c_rows != a_cols || c_cols != b_rows || a_rows != b_cols) return -1;
+        return 0;
+    }
+    return -1;
+}

@@ -177,6 +177,16 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
                     uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
                     uint8_t* stream_nomatch, size_t cap_bytes);
 
+/* ---- binary_matrix algebra over GF(2) ----------------- */
+/* Reference layout only: wpr = ceil(cols/64) for every operand (the loops index words flat).
+ * bo_gf2_transpose: binmat.cpp:199-214 (copy_col_to + set_row): dst (cols x rows). bo_gf2_mul:
+ * op 0 mul_AB binmat.cpp:516-542, 1 mul_AtB :545-572, 2 mul_ABt :575-594 (j < B.cols as written;
+ * rows of B past B.rows read 0, writes past C dropped), 3 mul_AtBt :596-604 (C unchanged). C is
+ * read (ABt keeps bits) and written in place. Returns 0, -1 on a shape the reference asserts. */
+void bo_gf2_transpose(const uint64_t* src, size_t rows, size_t cols, uint64_t* dst);
+int bo_gf2_mul(int op, const uint64_t* A, size_t a_rows, size_t a_cols, const uint64_t* B, size_t b_rows,
+               size_t b_cols, uint64_t* C, size_t c_rows, size_t c_cols);
+
 /* ---- CPU baseline (bench.py cpu_baseline leg) ---------------------------- */
 /* med + Golomb + EG over nplanes planes, OpenMP over planes when built with it.
  * Returns total Golomb bits + EG bits; *threads_used receives the thread count. */

@@ -472,3 +472,28 @@ extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr
   I.destroy();
   return 0;
 }
+
+// binary_matrix algebra on the reference's own objects (binmat.cpp:199-214, 516-616): C starts as
+// Cin (mul_ABt keeps bits), words in the reference layout (wpr = ceil(cols/64), padding bits 0).
+extern "C" int ref_gf2_mul(int op, const uint64_t* A, size_t a_rows, size_t a_cols, const uint64_t* B,
+                           size_t b_rows, size_t b_cols, uint64_t* C, size_t c_rows, size_t c_cols) {
+  binary_matrix Am = from_words(A, a_rows, a_cols, (a_cols + 63) / 64);
+  binary_matrix Bm = from_words(B, b_rows, b_cols, (b_cols + 63) / 64);
+  binary_matrix Cm = from_words(C, c_rows, c_cols, (c_cols + 63) / 64);
+  // mul_ABt's block_sum XORs the word's bytes into one shared variable from an OpenMP parallel for
+  // (binmat.cpp:48-52, a data race): with one thread it is the parity it is meant to be
+  const int nt = omp_get_max_threads();
+  omp_set_num_threads(1);
+  mul(Am, op == 1 || op == 3, Bm, op == 2 || op == 3, Cm);
+  omp_set_num_threads(nt);
+  to_words(Cm, C, (c_cols + 63) / 64);
+  return 0;
+}
+
+extern "C" int ref_gf2_transpose(const uint64_t* src, size_t rows, size_t cols, uint64_t* dst) {
+  binary_matrix Am = from_words(src, rows, cols, (cols + 63) / 64);
+  binary_matrix T(cols, rows);
+  Am.transpose_to(T);
+  to_words(T, dst, (rows + 63) / 64);
+  return 0;
+}

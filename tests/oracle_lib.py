@@ -55,6 +55,8 @@ class Oracle:
         _sig(L, "bo_baseline_planes", C.c_uint64, [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, C.POINTER(C.c_int)])
         _sig(L, "bo_patch_search", None, [u64p, sz, sz, sz, C.c_uint, u32p, u32p, u32p])
         _sig(L, "bo_patch_search_rows", None, [u64p, sz, sz, sz, C.c_uint, sz, sz, u32p, u32p, u32p])
+        _sig(L, "bo_gf2_transpose", None, [u64p, sz, sz, u64p])
+        _sig(L, "bo_gf2_mul", C.c_int, [C.c_int, u64p, sz, sz, u64p, sz, sz, u64p, sz, sz])
         _sig(L, "bo_match_encode", C.c_int,
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p,
               u8p, u8p, sz])
@@ -204,6 +206,22 @@ class Oracle:
                     modes=modes.raw[:n].decode(), residual=I, stream=stream)
 
 
+    def gf2_transpose(self, M, rows, cols):
+        """binmat.cpp:199-214 on reference-layout words [rows, ceil(cols/64)]"""
+        M = np.ascontiguousarray(M, np.uint64)
+        out = np.zeros((cols, (rows + 63) // 64), np.uint64)
+        self.lib.bo_gf2_transpose(ptr(M, u64p), rows, cols, ptr(out, u64p))
+        return out
+
+    def gf2_mul(self, op, A, a_rows, a_cols, B, b_rows, b_cols, C0, c_rows, c_cols):
+        """mul(A, At, B, Bt, C) (binmat.cpp:516-616) on reference-layout words; C0 = C's contents before"""
+        A, B = (np.ascontiguousarray(x, np.uint64) for x in (A, B))
+        Cm = np.array(C0, np.uint64, copy=True)
+        rc = self.lib.bo_gf2_mul(op, ptr(A, u64p), a_rows, a_cols, ptr(B, u64p), b_rows, b_cols, ptr(Cm, u64p),
+                                 c_rows, c_cols)
+        assert rc == 0
+        return Cm
+
     def patch_search(self, I, cols, W):
         """compress_test.cpp:73-111 search: (besti, bestj, bestd) per tile, raster order."""
         I = np.ascontiguousarray(I)
@@ -295,6 +313,8 @@ class Ref:
         _sig(L, "ref_patch_search", C.c_int, [u64p, sz, sz, sz, C.c_uint, u32p, u32p, u32p])
         _sig(L, "ref_match_loop", C.c_int,
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p])
+        _sig(L, "ref_gf2_mul", C.c_int, [C.c_int, u64p, sz, sz, u64p, sz, sz, u64p, sz, sz])
+        _sig(L, "ref_gf2_transpose", C.c_int, [u64p, sz, sz, u64p])
         _sig(L, "ref_baseline_planes", C.c_double,
              [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, C.c_int, u64p, C.POINTER(C.c_int)])
 
@@ -368,6 +388,19 @@ class Ref:
     def pbm_roundtrip(self, path, out_path):
         rc = np.zeros(2, np.uint64)
         return self.lib.ref_pbm_roundtrip(path.encode(), out_path.encode(), ptr(rc, u64p))
+
+    def gf2_transpose(self, M, rows, cols):
+        M = np.ascontiguousarray(M, np.uint64)
+        out = np.zeros((cols, (rows + 63) // 64), np.uint64)
+        self.lib.ref_gf2_transpose(ptr(M, u64p), rows, cols, ptr(out, u64p))
+        return out
+
+    def gf2_mul(self, op, A, a_rows, a_cols, B, b_rows, b_cols, C0, c_rows, c_cols):
+        A, B = (np.ascontiguousarray(x, np.uint64) for x in (A, B))
+        Cm = np.array(C0, np.uint64, copy=True)
+        self.lib.ref_gf2_mul(op, ptr(A, u64p), a_rows, a_cols, ptr(B, u64p), b_rows, b_cols, ptr(Cm, u64p),
+                             c_rows, c_cols)
+        return Cm
 
     def patch_search(self, I, cols, W):
         I = np.ascontiguousarray(I)

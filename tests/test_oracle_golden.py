@@ -146,3 +146,21 @@ def test_eg_adaptive_kat(oracle, golden, name):
     assert bits == meta["eg_adaptive"][name]
     assert np.array_equal(per, arr[f"egad_{name}_bits"])
     assert stream.tobytes() == arr[f"egad_{name}_stream"].tobytes()
+
+
+def test_gf2_algebra_golden(oracle):
+    """oracle bo_gf2_mul / bo_gf2_transpose vs mul() / transpose_to run on the reference's objects
+    (tests/golden/make_golden_gf2.py, binmat.cpp:199-214, 516-616)"""
+    import json
+    import os
+
+    g = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(g, "gf2.json")) as f:
+        meta = json.load(f)
+    A = np.load(os.path.join(g, "gf2.npz"), allow_pickle=False)
+    for n, m in enumerate(meta["mul"]):
+        (ar, ac), (br, bc), (cr, cc) = m["a"], m["b"], m["c"]
+        got = oracle.gf2_mul(m["op"], A[f"mul{n}_A"], ar, ac, A[f"mul{n}_B"], br, bc, A[f"mul{n}_C0"], cr, cc)
+        assert np.array_equal(got, A[f"mul{n}_C"]), (n, m)
+    for n, (rows, cols) in enumerate(meta["transpose"]):
+        assert np.array_equal(oracle.gf2_transpose(A[f"tr{n}_in"], rows, cols), A[f"tr{n}_out"]), n

@@ -84,3 +84,30 @@ def test_match_encode(oracle, ref, case):
         assert a[k] == b[k], k
     if spec[0] == "periodic":
         assert a["matches"] > 0  # the inputs exercise the match branch
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_gf2_algebra(oracle, ref, seed):
+    """bo_gf2_mul / bo_gf2_transpose vs the reference's mul() and transpose_to on fresh shapes
+    (mul_ABt with B.cols <= B.rows: past that the reference reads past B's buffer)"""
+    rng = np.random.default_rng(900 + seed)
+    op = seed % 4
+    ar, ac = int(rng.integers(1, 150)), int(rng.integers(1, 150))
+    if op == 0:
+        br, bc = ac, int(rng.integers(1, 150))
+        cr, cc = ar, bc
+    elif op == 1:
+        br, bc = ar, int(rng.integers(1, 150))
+        cr, cc = ac, bc
+    elif op == 2:
+        br, bc = int(rng.integers(ac, 200)), ac
+        cr, cc = ar, br
+    else:
+        br, bc = int(rng.integers(1, 150)), ar
+        cr, cc = ac, br
+    A = oracle.gen_plane(7000 + seed, 0.5, ar, ac)
+    B = oracle.gen_plane(7100 + seed, float(rng.choice([0.5, 0.1, 0.9])), br, bc)
+    C0 = oracle.gen_plane(7200 + seed, 0.5, cr, cc)
+    exp = ref.gf2_mul(op, A, ar, ac, B, br, bc, C0, cr, cc)
+    assert np.array_equal(oracle.gf2_mul(op, A, ar, ac, B, br, bc, C0, cr, cc), exp)
+    assert np.array_equal(oracle.gf2_transpose(A, ar, ac), ref.gf2_transpose(A, ar, ac))
