@@ -91,6 +91,8 @@ __device__ __forceinline__ int wave_incl_max(int x) {
   x = max(x, dpp_or<0x143, 0xC>(INT_MIN, x));
   return x;
 }
+// (the old operand of every DPP step is the operation's identity, never x itself: with old = x the
+// compiler keeps a v_mov_b32_dpp plus a copy of x per step instead of one v_max_i32_dpp)
 // reductions (wave-uniform results): quad swaps and the two mirrors give every lane its row's
 // total (wave_sum_u64: the four rows are combined from readlanes); the 32-bit ones carry the row
 // totals into row 3 with row_bcast:15 / row_bcast:31 and read lane 63 once
@@ -116,19 +118,19 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
   return lane63_u32(x);
 }
 __device__ __forceinline__ int wave_max(int x) {
-  x = max(x, dpp_or<0xB1>(x, x));
-  x = max(x, dpp_or<0x4E>(x, x));
-  x = max(x, dpp_or<0x141>(x, x));
-  x = max(x, dpp_or<0x140>(x, x));
+  x = max(x, dpp_or<0xB1>(INT_MIN, x));
+  x = max(x, dpp_or<0x4E>(INT_MIN, x));
+  x = max(x, dpp_or<0x141>(INT_MIN, x));
+  x = max(x, dpp_or<0x140>(INT_MIN, x));
   x = max(x, dpp_or<0x142, 0xA>(INT_MIN, x));
   x = max(x, dpp_or<0x143, 0xC>(INT_MIN, x));
   return __builtin_amdgcn_readlane(x, 63);
 }
 __device__ __forceinline__ int wave_min(int x) {
-  x = min(x, dpp_or<0xB1>(x, x));
-  x = min(x, dpp_or<0x4E>(x, x));
-  x = min(x, dpp_or<0x141>(x, x));
-  x = min(x, dpp_or<0x140>(x, x));
+  x = min(x, dpp_or<0xB1>(INT_MAX, x));
+  x = min(x, dpp_or<0x4E>(INT_MAX, x));
+  x = min(x, dpp_or<0x141>(INT_MAX, x));
+  x = min(x, dpp_or<0x140>(INT_MAX, x));
   x = min(x, dpp_or<0x142, 0xA>(INT_MAX, x));
   x = min(x, dpp_or<0x143, 0xC>(INT_MAX, x));
   return __builtin_amdgcn_readlane(x, 63);

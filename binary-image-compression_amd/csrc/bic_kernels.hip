@@ -473,12 +473,34 @@ __device__ __forceinline__ void perm_t4(uint32_t w0, uint32_t w1, uint32_t w2, u
   out[3] = __builtin_amdgcn_perm(b01, b23, 0x05040100u);
 }
 
+// transpose8x8 of bswap64(x1 << 32 | x0) on 32-bit halves with v_bitop3 (gfx950): the first two
+// stages stay inside each half, the third moves nibbles between them; 21 VALU + 2 v_perm instead of
+// the 64-bit form's ~29 (whose last stage the compiler turns into a 64-bit multiply).
+__device__ __forceinline__ uint64_t transpose8x8_bs(uint32_t x0, uint32_t x1) {
+  uint32_t hi = __builtin_bswap32(x0), lo = __builtin_bswap32(x1);
+  uint32_t t;
+  t = __builtin_amdgcn_bitop3_b32(lo, lo >> 7, 0x00AA00AAu, 0x28);  // (a ^ b) & c
+  lo = __builtin_amdgcn_bitop3_b32(lo, t, t << 7, 0x96);           // a ^ b ^ c
+  t = __builtin_amdgcn_bitop3_b32(hi, hi >> 7, 0x00AA00AAu, 0x28);
+  hi = __builtin_amdgcn_bitop3_b32(hi, t, t << 7, 0x96);
+  t = __builtin_amdgcn_bitop3_b32(lo, lo >> 14, 0x0000CCCCu, 0x28);
+  lo = __builtin_amdgcn_bitop3_b32(lo, t, t << 14, 0x96);
+  t = __builtin_amdgcn_bitop3_b32(hi, hi >> 14, 0x0000CCCCu, 0x28);
+  hi = __builtin_amdgcn_bitop3_b32(hi, t, t << 14, 0x96);
+  t = __builtin_amdgcn_bitop3_b32(lo, hi << 4, 0xF0F0F0F0u, 0x28);
+  lo ^= t;
+  hi ^= t >> 4;
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// FULL: every lane's word lies inside the row and the row has no pad bits (no mask)
+template <bool FULL = false>
 __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&pw)[8], uint64_t mask) {
   uint64_t T[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    T[2 * i] = transpose8x8(bswap64((uint64_t)v[i].x | ((uint64_t)v[i].y << 32)));
-    T[2 * i + 1] = transpose8x8(bswap64((uint64_t)v[i].z | ((uint64_t)v[i].w << 32)));
+    T[2 * i] = transpose8x8_bs(v[i].x, v[i].y);
+    T[2 * i + 1] = transpose8x8_bs(v[i].z, v[i].w);
   }
   // byte b of T[g8] -> byte 7 - g8 of pw[b]: four 4x4 byte transposes, 8 v_perm_b32 each
   uint32_t XL[4], YL[4], XH[4], YH[4];
@@ -488,28 +510,25 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
   perm_t4((uint32_t)(T[4] >> 32), (uint32_t)(T[5] >> 32), (uint32_t)(T[6] >> 32), (uint32_t)(T[7] >> 32), YH);
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    pw[b] = (((uint64_t)XL[b] << 32) | YL[b]) & mask;
-    pw[4 + b] = (((uint64_t)XH[b] << 32) | YH[b]) & mask;
+    pw[b] = ((uint64_t)XL[b] << 32) | YL[b];
+    pw[4 + b] = ((uint64_t)XH[b] << 32) | YH[b];
+    if constexpr (!FULL) {
+      pw[b] &= mask;
+      pw[4 + b] &= mask;
+    }
   }
 }
 
-template <bool PREDICT>
-__global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
-                                                        uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
-                                                        uint32_t* __restrict__ sones, int4* __restrict__ krec,
-                                                        uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
-  __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
-  if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
+template <bool PREDICT, bool FULL>
+__device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray, size_t pitch, const Geom& g,
+                                                uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
+                                                uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
+                                                int4* __restrict__ krec, uint32_t* __restrict__ kpos, uint32_t* tw) {
   const int lane = lane_id();
-  uint32_t* tw = tab[threadIdx.x >> 6];
-  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
-  const uint32_t s = (uint32_t)(gw % ns);  // the strips of one row block are neighbouring waves
-  const uint32_t r0 = (uint32_t)(gw / ns) * kGrayRows;
-  if (r0 >= g.rows) return;  // whole wave
   const int np = (int)g.nplanes;
   const uint32_t w = s * 64 + lane;
-  const bool in = w < g.used;
-  const uint64_t mask = in ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
+  const bool in = FULL || w < g.used;
+  const uint64_t mask = FULL ? ~0ull : in ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
   // the word's 64 pixels, and (lane 0 of strips s > 0) the pixel before the strip
   auto load = [&](uint32_t row, uint4 (&v)[4], uint32_t& lb) {
     const uint8_t* src = gray + (uint64_t)row * pitch + (uint64_t)w * 64;
@@ -532,7 +551,7 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
   uint32_t clb;
   if (PREDICT && r0) {
     load(r0 - 1, cur, ulb);
-    gray_to_planes(cur, up, mask);
+    gray_to_planes<FULL>(cur, up, mask);
     ulast = cur[3].w >> 24;
   }
   load(r0, cur, clb);
@@ -551,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
     ulast = cl;
     ulb = clb;
     uint64_t pw[8];
-    gray_to_planes(cur, pw, mask);
+    gray_to_planes<FULL>(cur, pw, mask);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       if (b >= np) break;
@@ -559,7 +578,8 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
       uint64_t R = pw[b];
       if constexpr (PREDICT) {
         const uint64_t D = pw[b] ^ up[b];
-        R = (D ^ ((D >> 1) | ((uint64_t)((left >> b) & 1u) << 63))) & mask;
+        R = D ^ ((D >> 1) | ((uint64_t)((left >> b) & 1u) << 63));
+        if constexpr (!FULL) R &= mask;
         if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
         up[b] = pw[b];
       }
@@ -574,6 +594,25 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
     clb = nlb;
   }
+}
+
+template <bool PREDICT>
+__global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
+                                                        uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
+                                                        uint32_t* __restrict__ sones, int4* __restrict__ krec,
+                                                        uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
+  if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
+  uint32_t* tw = tab[threadIdx.x >> 6];
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  const uint32_t s = (uint32_t)(gw % ns);  // the strips of one row block are neighbouring waves
+  const uint32_t r0 = (uint32_t)(gw / ns) * kGrayRows;
+  if (r0 >= g.rows) return;  // whole wave
+  // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
+  if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
+    gray_strip_rows<PREDICT, true>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+  else
+    gray_strip_rows<PREDICT, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
 }
 
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes) {

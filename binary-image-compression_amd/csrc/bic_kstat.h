@@ -113,11 +113,9 @@ __device__ __forceinline__ void lanek_store(const LaneK& k, int4* rec, uint32_t*
 // pass instead of eight wave-wide scan-and-reduce chains.
 __device__ __forceinline__ void strip_word_put(uint32_t* t, int b, uint64_t x, int32_t c0) {
   const int lane = lane_id();
-  uint32_t m = 0, c = 0;
-  if (x) {
-    m = (uint32_t)__popcll(x) | (parity_changes(x) << 8);
-    c = (uint32_t)(c0 + __builtin_clzll(x)) | ((uint32_t)(c0 + 63 - __builtin_ctzll(x)) << 16);
-  }
+  // branch-free: x = 0 gives m = 0 (strip_records then ignores c)
+  const uint32_t m = (uint32_t)__popcll(x) | (parity_changes(x) << 8);
+  const uint32_t c = (uint32_t)(c0 + __clzll((long long)x)) | ((uint32_t)(c0 + 64 - __ffsll((long long)x)) << 16);
   // lane l's value is value i = l & 7 of part 8b + (l >> 3): stored at word (i >> 2) * 256 +
   // 4 * part + (i & 3), so that strip_records' 16-byte reads (lane L: words 4L..4L+3 of each
   // quarter) are bank-conflict free
@@ -127,7 +125,8 @@ __device__ __forceinline__ void strip_word_put(uint32_t* t, int b, uint64_t x, i
 }
 template <int CTRL>
 __device__ __forceinline__ int dpp_same(int v) {  // every source lane valid (quad perms, mirrors)
-  return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false);
+  // no old operand (bound_ctrl): the step folds into the max / min / add that uses it
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);
 }
 __device__ __forceinline__ void strip_records(const uint32_t* t, int np, int4* krec, uint32_t* kpos, uint32_t* sones,
                                               uint64_t id0, uint64_t pstride) {
