@@ -1746,15 +1746,25 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
   }
   const uint64_t id = (uint64_t)(blockIdx.x >= second ? blockIdx.x - second : blockIdx.x) * 256 + threadIdx.x;
   if (id >= nrows) return;
+  const uint64_t pend = (id / rows + 1) * (uint64_t)rows;
+  // every load this row usually needs is issued at once (the row, its two fragments, the next row's
+  // offset, length and head fragment): one memory round trip instead of three dependent ones
+  const bool nx = id + 1 < pend;
   const uint64_t G = boff[id], L = len[id] & kLenMask;  // (the staged encoder's glen carries row flags)
+  const uint64_t f0 = frag[2 * id], f1 = frag[2 * id + 1];
+  const uint64_t G1 = nx ? boff[id + 1] : 0, L1 = nx ? len[id + 1] & kLenMask : 0, h1 = nx ? frag[2 * id + 2] : 0;
   if (L == 0) return;
   const uint64_t wt = (G + L - 1) >> 6, wh = G >> 6;
   const uint64_t wb = wt * 64;
   if (wb < G) return;                     // the word's first bit belongs to an earlier row
   if (wb + 64 <= G + L) return;           // a whole word of this row: already stored
-  uint64_t v = (wh == wt) ? frag[2 * id] : frag[2 * id + 1];
-  const uint64_t pend = (id / rows + 1) * (uint64_t)rows;
-  for (uint64_t r2 = id + 1; r2 < pend; ++r2) {
+  uint64_t v = (wh == wt) ? f0 : f1;
+  if (!nx || L1 == 0 || G1 >= wb + 64) {
+    out[wt] = bswap64(v);
+    return;
+  }
+  v |= h1;
+  for (uint64_t r2 = id + 2; r2 < pend; ++r2) {
     if ((len[r2] & kLenMask) == 0 || boff[r2] >= wb + 64) break;
     v |= frag[2 * r2];
   }
