@@ -1496,12 +1496,86 @@ __global__ __launch_bounds__(kBlock) void k_patch_search(FlatImage img, uint32_t
   }
 }
 
+// k_patch_search for W <= 8: a thread owns columns j2 and slides down them, so each window costs
+// ONE new row word (its W rows in registers, shifted by one per step) instead of W; the same
+// windows, keys and reduction.
+template <int WT>
+__global__ __launch_bounds__(kBlock) void k_patch_search_w(FlatImage img, uint32_t cols, uint32_t nx,
+                                                           uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+  __shared__ unsigned long long red[kWaves];
+  constexpr uint32_t W = WT;
+  const uint32_t tile = blockIdx.x, ti = tile / nx, tj = tile % nx;
+  const uint32_t i0 = ti * W, j0 = tj * W;
+  const uint64_t topW = ~(~0ull >> W);
+  uint64_t p[WT];
+#pragma unroll
+  for (int r = 0; r < WT; ++r) p[r] = img.window(i0 + r, j0) & topW;
+  const int lim1 = (int)(i0 - W), lim2 = (int)(j0 - W);
+  const uint32_t rows1 = lim1 >= 0 ? (uint32_t)lim1 + 1 : 0;
+  const uint32_t ncol2 = lim2 >= 0 ? (uint32_t)lim2 + 1 : 0;
+  const uint64_t n1 = (uint64_t)rows1 * cols;
+  unsigned long long best = ~0ull;  // (distance << 40) | scan index
+  // rows [ra, rb) of column j2, scan index base + (i2 - ra) * stride + j2
+  auto column = [&](uint32_t j2, uint32_t ra, uint32_t rb, uint64_t base, uint64_t stride) {
+    uint64_t win[WT];
+#pragma unroll
+    for (int r = 0; r < WT - 1; ++r) win[r] = img.window(ra + r, j2);
+    for (uint32_t i2 = ra; i2 < rb; ++i2) {
+      win[WT - 1] = img.window(i2 + W - 1, j2);
+      uint32_t d = 0;
+#pragma unroll
+      for (int r = 0; r < WT; ++r) d += (uint32_t)__popcll((p[r] ^ win[r]) & topW);
+      const unsigned long long key = ((unsigned long long)d << 40) | (base + (uint64_t)(i2 - ra) * stride + j2);
+      best = key < best ? key : best;
+#pragma unroll
+      for (int r = 0; r < WT - 1; ++r) win[r] = win[r + 1];
+    }
+  };
+  if (rows1)
+    for (uint32_t j2 = threadIdx.x; j2 < cols; j2 += kBlock) column(j2, 0, rows1, 0, cols);
+  if (ncol2)
+    for (uint32_t j2 = threadIdx.x; j2 < ncol2; j2 += kBlock) column(j2, rows1, i0 + 1, n1, ncol2);
+#pragma unroll
+  for (int dd = 32; dd >= 1; dd >>= 1) {
+    const unsigned long long o = shfl_u64(best, lane_id() ^ dd);
+    best = o < best ? o : best;
+  }
+  if (lane_id() == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < kWaves; ++q) best = red[q] < best ? red[q] : best;
+    uint32_t bi = 0, bj = 0, bd = W * W;
+    if (best != ~0ull && (uint32_t)(best >> 40) < W * W) {
+      const uint64_t idx = best & ((1ull << 40) - 1);
+      bd = (uint32_t)(best >> 40);
+      if (idx < n1) {
+        bi = (uint32_t)(idx / cols);
+        bj = (uint32_t)(idx % cols);
+      } else {
+        bi = rows1 + (uint32_t)((idx - n1) / ncol2);
+        bj = (uint32_t)((idx - n1) % ncol2);
+      }
+    }
+    besti[tile] = bi;
+    bestj[tile] = bj;
+    bestd[tile] = bd;
+  }
+}
+
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
                          uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
   const uint32_t nx = (W - 1 + cols) / W, ny = (W - 1 + rows) / W;
   if (!nx || !ny) return;
   FlatImage img{plane, rows, (cols + 63) / 64, wpr};
-  k_patch_search<<<nx * ny, kBlock, 0, s>>>(img, cols, W, nx, besti, bestj, bestd);
+  const uint32_t g = nx * ny;
+  switch (W) {
+#define BIC_PSW(N) \
+  case N: k_patch_search_w<N><<<g, kBlock, 0, s>>>(img, cols, nx, besti, bestj, bestd); return;
+    BIC_PSW(1) BIC_PSW(2) BIC_PSW(3) BIC_PSW(4) BIC_PSW(5) BIC_PSW(6) BIC_PSW(7) BIC_PSW(8)
+#undef BIC_PSW
+    default:
+      k_patch_search<<<g, kBlock, 0, s>>>(img, cols, W, nx, besti, bestj, bestd);
+  }
 }
 
 // ------------------------------------------------------------------------------------

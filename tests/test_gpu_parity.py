@@ -296,7 +296,9 @@ def test_pbm_raster_pack_unpack(ctx, oracle, rows, cols):
 
 
 @pytest.mark.parametrize("W,rows,cols,p", [(5, 37, 70, 0.3), (3, 20, 33, 0.5), (8, 40, 128, 0.1), (5, 26, 64, 0.02),
-                                           (4, 16, 50, 0.0), (32, 96, 200, 0.2), (5, 120, 300, 0.05)])
+                                           (4, 16, 50, 0.0), (32, 96, 200, 0.2), (5, 120, 300, 0.05),
+                                           (1, 9, 40, 0.5), (2, 17, 65, 0.3), (6, 31, 100, 0.4), (7, 50, 90, 0.1),
+                                           (9, 45, 130, 0.2)])
 def test_patch_search(ctx, oracle, W, rows, cols, p):
     """compress_test.cpp's search (tiles past the edges wrap into the next row; sparse images give
     perfect matches; p = 0 gives ties everywhere)"""
