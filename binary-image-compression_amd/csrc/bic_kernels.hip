@@ -1439,6 +1439,18 @@ struct FlatImage {
     else if (i + 1 < rows) b = I[(uint64_t)(i + 1) * wpr];
     return (a << sh) | (b >> (64 - sh));
   }
+  // the first 32 of those bits (window(i, j) >> 32): the next word is read only when they cross
+  // into it (sh > 32)
+  __device__ __forceinline__ uint32_t window32(uint32_t i, uint32_t j) const {
+    if (i >= rows) return 0;
+    const uint32_t w = j >> 6, sh = j & 63;
+    const uint64_t a = I[(uint64_t)i * wpr + w];
+    if (sh <= 32) return (uint32_t)(a >> (32 - sh));
+    uint64_t b = 0;
+    if (w + 1 < used) b = I[(uint64_t)i * wpr + w + 1];
+    else if (i + 1 < rows) b = I[(uint64_t)(i + 1) * wpr];
+    return __builtin_amdgcn_alignbit((uint32_t)a, (uint32_t)(b >> 32), 64 - sh);
+  }
 };
 
 __global__ __launch_bounds__(kBlock) void k_patch_search(FlatImage img, uint32_t cols, uint32_t W, uint32_t nx,
@@ -1506,10 +1518,10 @@ __global__ __launch_bounds__(kBlock) void k_patch_search_w(FlatImage img, uint32
   constexpr uint32_t W = WT;
   const uint32_t tile = blockIdx.x, ti = tile / nx, tj = tile % nx;
   const uint32_t i0 = ti * W, j0 = tj * W;
-  const uint64_t topW = ~(~0ull >> W);
-  uint64_t p[WT];
+  const uint32_t topW = ~(~0u >> W);  // W <= 8: the window's bits are the top of window32
+  uint32_t p[WT];
 #pragma unroll
-  for (int r = 0; r < WT; ++r) p[r] = img.window(i0 + r, j0) & topW;
+  for (int r = 0; r < WT; ++r) p[r] = img.window32(i0 + r, j0) & topW;
   const int lim1 = (int)(i0 - W), lim2 = (int)(j0 - W);
   const uint32_t rows1 = lim1 >= 0 ? (uint32_t)lim1 + 1 : 0;
   const uint32_t ncol2 = lim2 >= 0 ? (uint32_t)lim2 + 1 : 0;
@@ -1517,14 +1529,14 @@ __global__ __launch_bounds__(kBlock) void k_patch_search_w(FlatImage img, uint32
   unsigned long long best = ~0ull;  // (distance << 40) | scan index
   // rows [ra, rb) of column j2, scan index base + (i2 - ra) * stride + j2
   auto column = [&](uint32_t j2, uint32_t ra, uint32_t rb, uint64_t base, uint64_t stride) {
-    uint64_t win[WT];
+    uint32_t win[WT];
 #pragma unroll
-    for (int r = 0; r < WT - 1; ++r) win[r] = img.window(ra + r, j2);
+    for (int r = 0; r < WT - 1; ++r) win[r] = img.window32(ra + r, j2);
     for (uint32_t i2 = ra; i2 < rb; ++i2) {
-      win[WT - 1] = img.window(i2 + W - 1, j2);
+      win[WT - 1] = img.window32(i2 + W - 1, j2);
       uint32_t d = 0;
 #pragma unroll
-      for (int r = 0; r < WT; ++r) d += (uint32_t)__popcll((p[r] ^ win[r]) & topW);
+      for (int r = 0; r < WT; ++r) d += (uint32_t)__popc((p[r] ^ win[r]) & topW);
       const unsigned long long key = ((unsigned long long)d << 40) | (base + (uint64_t)(i2 - ra) * stride + j2);
       best = key < best ? key : best;
 #pragma unroll
