@@ -8,12 +8,15 @@ rows*cols*planes. N GPUs = N independent images (weak scaling, no data-path coll
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
 
-Multi-GPU: launched by torch.distributed.run, one rank per GPU (RCCL = backend "nccl").
-Rank 0 prints ONE JSON line.
+Multi-GPU: one rank per GPU (RCCL = backend "nccl"). Under torch.distributed.run (WORLD_SIZE set) this
+process is one rank; `bench.py --gpus N` without a launcher starts the N ranks itself, as a child
+torch.distributed.run of the same command, and exits with its code. Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,9 +51,28 @@ def parse():
                          "(strong scaling; the gather is in the timed step)")
     ap.add_argument("--separate", action="store_true",
                     help="c3: bic_bitplanes_u8 then bic_encode_planes2 instead of the one-call bic_encode_gray")
+    ap.add_argument("--plane-count", type=int, default=8,
+                    help="c3 --shard planes: encode planes 0..P-1 of the image (split over the ranks); P = 1 or 2 at "
+                         "N = 1 measures the per-rank step of a plane-sharded 8- or 4-GPU run")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks of this same command
+    under torch.distributed.run as a CHILD process (never exec) before anything here touches the
+    GPU, and return its exit code. Under a launcher (WORLD_SIZE set) this returns None and the
+    process is one rank."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8")))
 
 
 def dist_setup(args):
@@ -92,6 +114,32 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
+def allgather_i64(vals, world, dev):
+    """every rank's list of ints (same length on every rank), in rank order"""
+    if world == 1:
+        return [list(vals)]
+    import torch
+    import torch.distributed as dist
+    host = dist.get_backend() == "gloo"
+    t = torch.tensor(list(vals), dtype=torch.int64, device="cpu" if host else dev)
+    outs = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    return [o.cpu().tolist() for o in outs]
+
+
+def checksum(t):
+    """order-independent 64-bit fingerprint of a device tensor's words (wrapping sum and xor)"""
+    import torch
+    w = t.reshape(-1).view(torch.int64)
+    x = w.clone()
+    n = x.numel()
+    while n > 1:  # xor-reduce by halves (torch has no xor reduction)
+        h = n // 2
+        x[:h] ^= x[n - h:n]
+        n -= h
+    return [int(w.sum().item()), int(x[0].item()) if x.numel() else 0]
+
+
 def sum_over_ranks(x, world, dev):
     if world == 1:
         return x
@@ -103,8 +151,23 @@ def sum_over_ranks(x, world, dev):
 
 
 def load_pmc(workload, kernel):
-    """HBM bytes per launch from the newest round's committed rocprofv3 PMC summary
-    (profiles/rNN/pmc_<workload>.json), or None."""
+    """(HBM bytes per launch, note) from the newest round's committed rocprofv3 PMC summary
+    (profiles/rNN/pmc_<workload>.json). The summary carries the hash of the kernel sources it
+    profiled (pybic.sources_hash): a summary of other sources than the ones built here does not
+    describe this run's kernels, so it gives no traffic (None) and a note saying so."""
+    import pybic
+    got = _load_pmc(workload, kernel)
+    if got is None:
+        return None, "no PMC summary for this workload"
+    v, path, src = got
+    if src != pybic.sources_hash():
+        print(f"bench.py: {path} profiled other kernel sources ({src}); roofline.traffic left null",
+              file=sys.stderr)
+        return None, f"{os.path.relpath(path, ROOT)} profiled other kernel sources: traffic not reported"
+    return v, f"{os.path.relpath(path, ROOT)} (PMC FETCH_SIZE/WRITE_SIZE passes of these kernel sources)"
+
+
+def _load_pmc(workload, kernel):
     pdir = os.path.join(ROOT, "profiles")
     try:
         rounds = sorted((d for d in os.listdir(pdir) if d.startswith("r") and d[1:].isdigit()), reverse=True)
@@ -120,7 +183,7 @@ def load_pmc(workload, kernel):
         for sec in ("timers", "kernels"):
             v = d.get(sec, {}).get(kernel, {}).get("hbm_bytes_per_launch")
             if v is not None:
-                return v
+                return v, path, d.get("sources_sha256")
         return None
     return None
 
@@ -244,7 +307,9 @@ class C3Planes(C3):
         self.ctx, self.pybic, self.rank, self.world = ctx, pybic, rank, world
         self.rows = args.rows or 16384
         self.cols = args.cols or 16384
-        self.lo, self.hi = rank * 8 // world, (rank + 1) * 8 // world
+        self.total_planes = max(1, min(8, args.plane_count))
+        P = self.total_planes
+        self.lo, self.hi = rank * P // world, (rank + 1) * P // world
         self.nplanes = self.hi - self.lo
         g = t.Generator(device=ctx.dev)
         g.manual_seed(0x5EED0000)  # the same image on every rank
@@ -257,14 +322,15 @@ class C3Planes(C3):
         n = max(1, self.nplanes)
         self.out_g, self.out_e = ctx.empty_i64(n * self.slot_g), ctx.empty_i64(n * self.slot_e)  # packed
         self.bits_g, self.bits_e = ctx.empty_i64(n), ctx.empty_i64(n)
-        self.off_g, self.off_e = ctx.empty_i64(n + 1), ctx.empty_i64(n + 1)
+        # a rank with no plane (N > P) sends an empty stream: its offsets stay zero
+        self.off_g, self.off_e = (ctx.torch.zeros(n + 1, dtype=t.int64, device=ctx.dev) for _ in range(2))
         self.gathered = (None, None)
         ctx.reserve(n, self.rows, self.cols)
         self.k = 0
         self.separate = False
         self.pixels = self.rows * self.cols * self.nplanes
-        self.workload = (f"c3 sharded by planes: one {self.rows}x{self.cols} 8-bit gray image per step, its 8 "
-                         f"planes split over {world} GPU(s) -> med -> Golomb + EG, packed streams gathered to "
+        self.workload = (f"c3 sharded by planes: one {self.rows}x{self.cols} 8-bit gray image per step, its {P} "
+                         f"plane(s) split over {world} GPU(s) -> med -> Golomb + EG, packed streams gathered to "
                          f"rank 0")
 
     def step(self):
@@ -313,7 +379,8 @@ class C3Planes(C3):
         """rank 0, after collect(): the gathered streams of all 8 planes == the oracle's streams of
         bitplane_tool's planes of the last step's image"""
         gray = self.gray[(self.k - 1) & 1].cpu().numpy()
-        exp_planes = oracle.bitplanes_par(gray, 8)
+        P = self.total_planes
+        exp_planes = oracle.bitplanes_par(gray, P)
         exp = oracle.encode_planes_par(exp_planes, self.cols, 1)
         ok = True
         for coder in (0, 1):
@@ -322,7 +389,7 @@ class C3Planes(C3):
                 offs = [0, int(self.pybic.as_u64(offs)[-1])]
             W = self.pybic.as_u64(words)
             for r in range(self.world):
-                a, b = r * 8 // self.world, (r + 1) * 8 // self.world
+                a, b = r * P // self.world, (r + 1) * P // self.world
                 o = offs[r]
                 for k in range(a, b):
                     nb = int(self.allbits[coder][r][k - a])
@@ -441,60 +508,98 @@ class C4(C3):
     """64 independent 4096x4096 frames sharded over the ranks (strong scaling), med + Golomb,
     streams packed per rank and gathered to rank 0 over RCCL."""
 
+    TOTAL = 64
+
     def __init__(self, ctx, args, rank, world):
         import pybic
         t = ctx.torch
         self.ctx, self.pybic, self.rank, self.world = ctx, pybic, rank, world
         self.rows = args.rows or 4096
         self.cols = args.cols or 4096
-        total = 64
-        lo, hi = rank * total // world, (rank + 1) * total // world
-        self.nplanes = hi - lo
+        self.nplanes = len(self.share(rank))
         self.wpr = (self.cols + 63) // 64
-        g = t.Generator(device=ctx.dev)
-        g.manual_seed(0x5EED0000 + rank)
-        self.planes = rand_words(t, (self.nplanes, self.rows, self.wpr), ctx.dev, g)
+        self.planes = self.frames_of(rank)
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
-        self.out_g = ctx.empty_i64(self.nplanes, self.slot_g)
-        self.bits_g = ctx.empty_i64(self.nplanes)
+        self.out_g = ctx.empty_i64(max(1, self.nplanes), self.slot_g)
+        self.bits_g = ctx.torch.zeros(max(1, self.nplanes), dtype=t.int64, device=ctx.dev)
         self.bits_e = ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
-        self.packed = ctx.empty_i64(self.nplanes * self.slot_g)  # the streams, word-aligned back to back
-        self.word_off = ctx.empty_i64(self.nplanes + 1)
-        self.gathered = None
-        ctx.reserve(self.nplanes, self.rows, self.cols)
+        self.packed = ctx.empty_i64(max(1, self.nplanes) * self.slot_g)  # the streams, word-aligned back to back
+        self.word_off = ctx.torch.zeros(self.nplanes + 1, dtype=t.int64, device=ctx.dev)
+        self.gathered = (None, None)
+        ctx.reserve(max(1, self.nplanes), self.rows, self.cols)
         self.k = 0
         self.pixels = self.rows * self.cols * self.nplanes
         self.workload = (f"c4: 64 frames {self.rows}x{self.cols} sharded over ranks, med -> Golomb, "
                          f"per-rank packed streams gathered to rank 0 (RCCL)")
 
+    def share(self, r):
+        return range(r * self.TOTAL // self.world, (r + 1) * self.TOTAL // self.world)
+
+    def frames_of(self, r):
+        """rank r's frames (seeded per rank on the device: rank 0 regenerates any rank's for the check)"""
+        t = self.ctx.torch
+        g = t.Generator(device=self.ctx.dev)
+        g.manual_seed(0x5EED0000 + r)
+        return rand_words(t, (max(1, len(self.share(r))), self.rows, self.wpr), self.ctx.dev, g)
+
     def step(self):
         from pybic.parallel import gather_streams
-        c, p = self.ctx, self.pybic
+        c = self.ctx
         # packed output: the encoder writes each frame's stream at its packed word offset (no slots, no
         # pack kernel), ready for the gather
-        c.encode_planes_packed(self.planes, self.cols, True, golomb=True, eg=False, slots=(self.slot_g, None),
-                               outs=(self.packed, None), bits=(self.bits_g, None), offs=(self.word_off, None))
+        if self.nplanes:
+            c.encode_planes_packed(self.planes[:self.nplanes], self.cols, True, golomb=True, eg=False,
+                                   slots=(self.slot_g, None), outs=(self.packed, None), bits=(self.bits_g, None),
+                                   offs=(self.word_off, None))
         if self.world > 1:
             self.gathered = gather_streams(self.packed, self.word_off[-1:], self.world, self.rank)
         self.k += 1
 
+    def collect(self):
+        """after the timed steps (collective): every rank's per-frame bit counts and a fingerprint of
+        its input frames, on every rank"""
+        per = (self.TOTAL + self.world - 1) // self.world
+        b = [int(x) for x in self.pybic.as_u64(self.bits_g[:self.nplanes])] + [0] * (per - self.nplanes)
+        self.allbits = allgather_i64(b, self.world, self.ctx.dev)
+        self.sums = allgather_i64(checksum(self.planes[:self.nplanes]), self.world, self.ctx.dev)
+
     def kernel_bytes(self):
         plane_b = self.nplanes * self.rows * self.wpr * 8
-        g = int(self.pybic.as_u64(self.bits_g).astype(np.int64).sum()) // 8
+        g = int(self.pybic.as_u64(self.bits_g[:self.nplanes]).astype(np.int64).sum()) // 8
         return {"med_count": plane_b, "golomb_bits": plane_b, "golomb_emit": plane_b + g,
                 "encode_rows_golomb": plane_b + g}
 
     def check(self, oracle):
-        """every frame of rank 0's share: its stream at its packed offset == the oracle's"""
-        P = self.pybic.as_u64(self.planes)
-        exp = oracle.encode_planes_par(P, self.cols, 1, coders=(0,))
-        B, O, D = (self.pybic.as_u64(x) for x in (self.bits_g, self.word_off, self.packed))
+        """rank 0, after collect(): every one of the 64 frames' streams -- rank 0's own at its packed
+        offsets at N = 1, the buffer rank 0 RECEIVED from the gather at N > 1 -- == the oracle's
+        stream of that frame. Rank 0 regenerates the other ranks' frames from their seeds and
+        checks them against the fingerprints those ranks sent."""
+        if self.world == 1:
+            W = self.pybic.as_u64(self.packed)
+            offs = [0, int(self.pybic.as_u64(self.word_off)[-1])]
+        else:
+            W = self.pybic.as_u64(self.gathered[0])
+            offs = self.gathered[1]
         ok = True
-        for k in range(self.nplanes):
-            eb, est = exp[(k, 0)]
-            nw = (eb + 63) // 64
-            ok &= int(B[k]) == eb and int(O[k + 1] - O[k]) == nw and D[O[k]:O[k] + nw].tobytes() == est.tobytes()
-        return bool(ok)
+        nframes = 0
+        for r in range(self.world):
+            n = len(self.share(r))
+            if n == 0:
+                ok &= offs[r + 1] == offs[r]
+                continue
+            fr = self.planes if r == self.rank else self.frames_of(r)
+            ok &= checksum(fr[:n]) == self.sums[r]
+            P = self.pybic.as_u64(fr[:n])
+            exp = oracle.encode_planes_par(P, self.cols, 1, coders=(0,))
+            o = offs[r]
+            for k in range(n):
+                eb, est = exp[(k, 0)]
+                nw = (eb + 63) // 64
+                ok &= int(self.allbits[r][k]) == eb and W[o:o + nw].tobytes() == est.tobytes()
+                o += nw
+                nframes += 1
+            ok &= o == offs[r + 1]
+        return bool(ok and nframes == self.TOTAL)
 
 
 class C5(C3):
@@ -512,12 +617,8 @@ class C5(C3):
         self.W = 32
         self.nplanes = 1
         self.wpr = (self.cols + 63) // 64
-        ny = self.rows // self.W
-        lo, hi = rank * ny // world, (rank + 1) * ny // world
-        self.band_rows = (hi - lo) * self.W
-        g = t.Generator(device=ctx.dev)
-        g.manual_seed(0x5EED0000 + rank)
-        self.planes = rand_words(t, (1, self.band_rows, self.wpr), ctx.dev, g)
+        self.band_rows = self.band(rank)
+        self.planes = self.band_plane(rank)
         self.lt = pybic.lentab(self.W)
         self.res = None
         self.own_bits = 0
@@ -527,6 +628,20 @@ class C5(C3):
         self.bits_e = ctx.torch.zeros(1, dtype=t.int64, device=ctx.dev)
         self.workload = (f"c5: {self.rows}x{self.cols} plane, 32x32 tiles, per-tile med/mode + Golomb over weights"
                          + (f", tile-row bands over {world} GPUs" if world > 1 else ""))
+
+    def band(self, r):
+        ny = self.rows // self.W
+        return ((r + 1) * ny // self.world - r * ny // self.world) * self.W
+
+    def band_plane(self, r):
+        """rank r's band of tile rows (seeded per rank on the device; rank 0 regenerates any rank's)"""
+        t = self.ctx.torch
+        g = t.Generator(device=self.ctx.dev)
+        g.manual_seed(0x5EED0000 + r)
+        return rand_words(t, (1, self.band(r), self.wpr), self.ctx.dev, g)
+
+    def collect(self):
+        self.sums = allgather_i64(checksum(self.planes), self.world, self.ctx.dev)
 
     def step(self):
         c = self.ctx
@@ -541,7 +656,9 @@ class C5(C3):
                 nb = int(self.pybic.as_u64(bits)[0])
                 self.own_bits = nb
                 return out, nb
-            self.merged, _ = sharded_golomb(enc, wts.numel(), total, c.dev)
+            def lengths(n0, a0):
+                return int(self.pybic.as_u64(c.golomb_lengths(wts, n0=n0, a0=a0))[0])
+            self.merged, self.merged_bits = sharded_golomb(enc, wts.numel(), total, c.dev, lengths=lengths)
         self.k += 1
 
     def out_bytes(self):
@@ -553,11 +670,27 @@ class C5(C3):
         return {"tiles": 2 * self.band_rows * self.wpr * 8}
 
     def check(self, oracle):
-        P = self.pybic.as_u64(self.planes[0])
+        """N = 1: the plane's stream, bit count and L == the oracle's. N > 1 (rank 0, after
+        collect()): the MERGED stream rank 0 assembled from every band (one adaptive coder continued
+        across the ranks) == the oracle's stream of the whole plane; rank 0 regenerates the other
+        bands from their seeds and checks them against the fingerprints those ranks sent."""
+        if self.world == 1:
+            P = self.pybic.as_u64(self.planes[0])
+            exp = oracle.patch_encode(P, self.cols, self.W, self.lt, want_stream=True)
+            st = self.pybic.as_u64(self.res["stats"])
+            return (int(st[0]) == exp["bits"] and int(st[2]) == exp["L"] and
+                    self.pybic.stream_bytes(self.res["stream"], exp["bits"]) == exp["stream"].tobytes())
+        bands = []
+        ok = True
+        for r in range(self.world):
+            b = self.planes if r == self.rank else self.band_plane(r)
+            ok &= checksum(b) == self.sums[r]
+            bands.append(self.pybic.as_u64(b[0]))
+        P = np.ascontiguousarray(np.concatenate(bands, axis=0))
         exp = oracle.patch_encode(P, self.cols, self.W, self.lt, want_stream=True)
-        st = self.pybic.as_u64(self.res["stats"])
-        # on N > 1 ranks this checks rank 0's band (its tiles, L and its own fresh-state stream)
-        return int(st[0]) == exp["bits"] and int(st[2]) == exp["L"]
+        ok &= self.merged_bits == exp["bits"]
+        ok &= self.pybic.stream_bytes(self.merged, exp["bits"]) == exp["stream"].tobytes()
+        return bool(ok)
 
 
 class C1(C3):
@@ -746,6 +879,9 @@ def cpu_baseline(wl, args):
 
 def main():
     args = parse()
+    rc = spawn_ranks(args)  # before torch / HIP are touched in this process
+    if rc is not None:
+        sys.exit(rc)
     import torch
     world, rank, local = dist_setup(args)
     import pybic
@@ -812,8 +948,9 @@ def main():
         n, ms = timed[dom]
         avg_s = ms / 1e3 / n
         ach = kb[dom] / avg_s / 1e9
+        traffic, tnote = load_pmc(args.workload, dom)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc(args.workload, dom), "kernel": dom,
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tnote, "kernel": dom,
                 "algorithmic_bytes_per_launch": kb[dom], "avg_launch_us": round(avg_s * 1e6, 2)}
     pred_pass = wl.predictor_pass(max(args.steps, 5)) if hasattr(wl, "predictor_pass") and type(wl) is C3 else None
     if pred_pass is not None and "bitplanes_count" in per_kernel:

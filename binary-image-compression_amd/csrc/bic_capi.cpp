@@ -392,14 +392,24 @@ size_t bic_encode_slot_words(size_t rows, size_t cols, int coder) {
 
 namespace {
 // Packed output where the encoder cannot write it in place (encoders other than the staged one, the
-// multi-pass path): encode into slots in a stream-ordered temporary, then bic_pack_streams' kernel.
-int pack_after(bic_ctx* ctx, int nplanes, uint64_t* out, size_t slot, uint64_t* bits, uint64_t* off,
-               const std::function<int(uint64_t*)>& encode) {
-  uint64_t* tmp = nullptr;
-  BIC_HIP(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)nplanes * slot * 8, ctx->cur));
-  const int rc = encode(tmp);
-  if (rc == BIC_OK) timed(ctx, "pack", [&] { bic::launch_pack(ctx->cur, tmp, nplanes, slot, bits, out, off); });
-  (void)hipFreeAsync(tmp, ctx->cur);
+// multi-pass path): ONE encode of both coders into slots in stream-ordered temporaries, then
+// bic_pack_streams' kernel once per coder.
+int pack_after(bic_ctx* ctx, int nplanes, uint64_t* out_g, size_t slot_g, uint64_t* bits_g, uint64_t* off_g,
+               uint64_t* out_e, size_t slot_e, uint64_t* bits_e, uint64_t* off_e,
+               const std::function<int(uint64_t*, uint64_t*)>& encode) {
+  uint64_t *tg = nullptr, *te = nullptr;
+  if (out_g) BIC_HIP(hipMallocAsync(reinterpret_cast<void**>(&tg), (size_t)nplanes * slot_g * 8, ctx->cur));
+  if (out_e && hipMallocAsync(reinterpret_cast<void**>(&te), (size_t)nplanes * slot_e * 8, ctx->cur) != hipSuccess) {
+    if (tg) (void)hipFreeAsync(tg, ctx->cur);
+    return BIC_EDEVICE;
+  }
+  const int rc = encode(tg, te);
+  if (rc == BIC_OK && tg)
+    timed(ctx, "pack", [&] { bic::launch_pack(ctx->cur, tg, nplanes, slot_g, bits_g, out_g, off_g); });
+  if (rc == BIC_OK && te)
+    timed(ctx, "pack", [&] { bic::launch_pack(ctx->cur, te, nplanes, slot_e, bits_e, out_e, off_e); });
+  if (tg) (void)hipFreeAsync(tg, ctx->cur);
+  if (te) (void)hipFreeAsync(te, ctx->cur);
   BIC_HIP(hipGetLastError());
   return rc;
 }
@@ -440,19 +450,12 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
         return rc;
       return bic_row_index(ctx, planes, nplanes, rows, cols, wpr, predict, row_index);
     }
-    if ((off_golomb || off_eg) && mode != bic::kEncStaged) {  // packed output via slots + pack
-      if (off_golomb && (rc = pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, [&](uint64_t* t) {
-            return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, t, slot_golomb, bits_golomb,
-                                      nullptr, nullptr, 0, nullptr, nullptr);
-          })))
-        return rc;
-      if (off_eg)
-        return pack_after(ctx, nplanes, out_eg, slot_eg, bits_eg, off_eg, [&](uint64_t* t) {
-          return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, nullptr, 0, nullptr, nullptr, t,
-                                    slot_eg, bits_eg, nullptr);
-        });
-      return BIC_OK;
-    }
+    if ((off_golomb || off_eg) && mode != bic::kEncStaged)  // packed output via slots + pack
+      return pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, out_eg, slot_eg, bits_eg,
+                        off_eg, [&](uint64_t* tg, uint64_t* te) {
+                          return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, tg, slot_golomb,
+                                                    bits_golomb, nullptr, te, slot_eg, bits_eg, nullptr);
+                        });
     fs.off_g = off_golomb;
     fs.off_e = off_eg;
     fs.index = row_index;
@@ -472,19 +475,12 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
   }
   // rows wider than 16384 columns: multi-pass chunk kernels (bic_kernels.hip)
   if (row_index) return BIC_EINVAL;  // (the decoders take rows of up to 16384 columns)
-  if (off_golomb || off_eg) {  // packed output via slots + pack
-    if (off_golomb && (rc = pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, [&](uint64_t* t) {
-          return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, t, slot_golomb, bits_golomb, nullptr,
-                                    nullptr, 0, nullptr, nullptr);
-        })))
-      return rc;
-    if (off_eg)
-      return pack_after(ctx, nplanes, out_eg, slot_eg, bits_eg, off_eg, [&](uint64_t* t) {
-        return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, nullptr, 0, nullptr, nullptr, t,
-                                  slot_eg, bits_eg, nullptr);
-      });
-    return BIC_OK;
-  }
+  if (off_golomb || off_eg)  // packed output via slots + pack
+    return pack_after(ctx, nplanes, out_golomb, slot_golomb, bits_golomb, off_golomb, out_eg, slot_eg, bits_eg, off_eg,
+                      [&](uint64_t* tg, uint64_t* te) {
+                        return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, tg, slot_golomb,
+                                                  bits_golomb, nullptr, te, slot_eg, bits_eg, nullptr);
+                      });
   if ((rc = ensure_scratch(ctx, bic::chunk_scratch_bytes(g)))) return rc;
   const bic::ChunkScratch cs = bic::carve_chunk_scratch(ctx->scratch, g);
   timed(ctx, "med_count", [&] { bic::launch_count(ctx->cur, g, planes, pr, cs, nullptr, nullptr); });
@@ -684,7 +680,8 @@ int bic_golomb_encode_samples(bic_ctx* ctx, const uint32_t* samples, size_t n, u
                               uint64_t* bits_out) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if ((!samples && n) || !out || !bits_out || bit0 >= 64 || cap_words == 0) return BIC_EINVAL;
+  // out == NULL with cap_words == 0: the lengths only (bits_out), no stream written
+  if ((!samples && n) || !bits_out || bit0 >= 64 || (out ? cap_words == 0 : cap_words != 0)) return BIC_EINVAL;
   if (n0 + n >= 0x80000000ull || a0 >= 0x80000000ull) return BIC_EINVAL;
   if ((rc = ensure_scratch(ctx, bic::sample_scratch_bytes(n)))) return rc;
   const bic::SampleScratch ss = bic::carve_sample_scratch(ctx->scratch, n);

@@ -44,6 +44,17 @@ __device__ __forceinline__ const uint64_t* plane_stream(const DecArgs& a, uint32
   return a.streams + (a.slot ? (uint64_t)plane * a.slot : a.word_off[plane]);
 }
 
+// Words of plane p's stream the decoder may read: ceil(plane_bits / 64), capped at the plane's
+// capacity (its slot, or word_off[p + 1] - word_off[p] when packed). A stated length past the
+// capacity is a malformed stream (`over`): nothing past the plane's own words is ever read.
+__device__ __forceinline__ uint64_t plane_words(const DecArgs& a, uint32_t plane, bool& over) {
+  const uint64_t want = (a.plane_bits[plane] + 63) >> 6;
+  const uint64_t lo = a.slot ? 0 : a.word_off[plane];
+  const uint64_t cap = a.slot ? a.slot : (a.word_off[plane + 1] >= lo ? a.word_off[plane + 1] - lo : 0);
+  over = want > cap;
+  return over ? cap : want;
+}
+
 // The residual row (lane words w = 64 t + lane, t < 4) -> the row's output words: D (the prefix
 // XOR along the row, P(0, 0) in place of R(0, 0) on row 0) when predicting, R itself otherwise.
 __device__ __forceinline__ void store_row(const DecArgs& a, uint32_t plane, uint32_t row, uint64_t (&r)[4]) {
@@ -93,9 +104,10 @@ __global__ __launch_bounds__(256) void k_dec_golomb_lanes(DecArgs a) {
   const uint64_t* st = plane_stream(a, plane);
   const uint64_t G = a.index[2 * id], O = a.index[2 * id + 1];
   const uint64_t E = row + 1 < a.rows ? a.index[2 * id + 2] : a.plane_bits[plane];
-  const uint64_t maxw = (a.plane_bits[plane] + 63) >> 6;  // words of this plane's stream
+  bool over;
+  const uint64_t maxw = plane_words(a, plane, over);  // words of this plane's stream
   uint64_t* dst = a.out + ((uint64_t)plane * a.rows + row) * a.wpr;
-  bool bad = E < G + 1;  // every row has at least its end-of-row codeword
+  bool bad = over || E < G + 1;  // every row has at least its end-of-row codeword
   const uint64_t len = bad ? 0 : E - G;
   auto ld = [&](uint64_t i) -> uint64_t { return i < maxw ? bswap64(st[i]) : 0ull; };
   uint64_t* my = ring + threadIdx.x;
@@ -213,7 +225,9 @@ __global__ __launch_bounds__(256) void k_dec_eg_first(DecArgs a) {
   if (gw >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(gw / a.rows), row = (uint32_t)(gw % a.rows);
   const uint64_t* st = plane_stream(a, plane);
-  const uint64_t off = (uint64_t)row * (a.cols + 1), bits = a.plane_bits[plane];
+  const uint64_t off = (uint64_t)row * (a.cols + 1);
+  bool over;
+  const uint64_t maxw = plane_words(a, plane, over);
   const uint32_t nw = (a.cols + 1 + 63) / 64;
   bool ones = true;
   for (uint32_t t = lane_id(); t < nw; t += 64) {
@@ -221,7 +235,6 @@ __global__ __launch_bounds__(256) void k_dec_eg_first(DecArgs a) {
     const uint32_t nb = min(64u, a.cols + 1 - 64 * t);
     const uint64_t i = p >> 6;
     const uint32_t sh = (uint32_t)(p & 63);
-    const uint64_t maxw = (bits + 63) >> 6;
     const uint64_t hi = i < maxw ? bswap64(st[i]) : 0ull;
     uint64_t v = hi << sh;
     if (sh) v |= (i + 1 < maxw ? bswap64(st[i + 1]) : 0ull) >> (64 - sh);
@@ -242,7 +255,9 @@ __global__ __launch_bounds__(256) void k_dec_eg_rows(DecArgs a) {
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const uint64_t* st = plane_stream(a, plane);
   const uint32_t f = a.first_row[plane];
-  const uint64_t bits = a.plane_bits[plane], maxw = (bits + 63) >> 6;
+  const uint64_t bits = a.plane_bits[plane];
+  bool over;
+  const uint64_t maxw = plane_words(a, plane, over);
   const uint64_t off = (uint64_t)row * (a.cols + 1) + (row > f ? 1 : 0);
   auto get64 = [&](uint64_t p) -> uint64_t {
     const uint64_t i = p >> 6;
@@ -253,7 +268,7 @@ __global__ __launch_bounds__(256) void k_dec_eg_rows(DecArgs a) {
   uint64_t x[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) x[t] = (uint32_t)(t * 64 + lane) < a.used ? get64(off + 64ull * (t * 64 + lane)) : ~0ull;
-  bool bad = false;
+  bool bad = over;
   uint64_t ins = ~0ull;  // row bit after which the stream carries the inserted '0'
   if (row == f) {  // first residual 1 of the plane: the first '0' of the row
     int fc = INT_MAX;

@@ -1118,6 +1118,7 @@ __global__ __launch_bounds__(kBlock) void k_samp_scan(const uint32_t* __restrict
   __syncthreads();
   // zero the words this block's codewords touch (within the caller's capacity); the words it
   // shares with its neighbours may be zeroed by either -- all of it before any codeword is OR'd
+  if (!out) return;  // lengths only (bic_golomb_encode_samples with no output)
   const uint64_t B0 = sh[1];
   const uint64_t w_lo = blk == 0 ? 0 : B0 / 64, w_hi = (B0 + tot_b + 63) / 64;
   if (w_hi > cap_words && threadIdx.x == 0) atomicOr(&flags[0], 1u);
@@ -1194,7 +1195,7 @@ void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uin
   }
   (void)hipMemsetAsync(ss.counter, 0, ss.zero_bytes, s);
   k_samp_scan<<<nblk, kBlock, 0, s>>>(samples, n, n0, a0, bit0, ss, out, cap_words, bits_out, flags, nblk);
-  k_samp_emit<<<nblk, kBlock, 0, s>>>(samples, n, n0, ss, out, bits_out, bit0, cap_words);
+  if (out) k_samp_emit<<<nblk, kBlock, 0, s>>>(samples, n, n0, ss, out, bits_out, bit0, cap_words);
 }
 
 // ------------------------------------------------------------------------------------

@@ -395,6 +395,14 @@ class Context:
         """the two-pass row encoder instead of the default staged one"""
         self._chk(self.lib.bic_ctx_set_option(self.h, 2, int(on)), "bic_ctx_set_option")
 
+    def golomb_lengths(self, samples, n0=0, a0=0):
+        """bic_golomb_encode_samples without an output: -> bits int64[2] (codeword bits, sum of samples)"""
+        bits = self.empty_i64(2)
+        self._bind_stream()
+        self._chk(self.lib.bic_golomb_encode_samples(self.h, _p(samples), samples.numel(), n0, a0, 0, None, 0,
+                                                     _p(bits)), "bic_golomb_encode_samples")
+        return bits
+
     def golomb_encode_samples(self, samples, n0=0, a0=0, bit0=0, cap_words=None, out=None):
         """samples: int32 device tensor (uint32 values) -> (stream int64 [cap], bits int64[2])."""
         n = samples.numel()
@@ -545,6 +553,21 @@ def lentab(W):
     if rc != BIC_OK:
         raise BicError(rc, "bic_tile_lentab")
     return out
+
+
+def sources_hash():
+    """sha256 of the HIP/C++ sources libbic.so is built from (csrc/*): PMC summaries under profiles/
+    carry the hash of the sources they profiled, so bench.py can tell whether they describe the
+    kernels it is running."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(PKG, "csrc")
+    for name in sorted(os.listdir(d)):
+        if name.endswith((".hip", ".cpp", ".h")):
+            h.update(name.encode())
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()
 
 
 def device_count():

@@ -80,20 +80,27 @@ def merge_bit_streams(parts, bit_offsets, total_bits, device):
     return out
 
 
-def sharded_golomb(encode, count, total, device, dst=0):
+def sharded_golomb(encode, count, total, device, dst=0, lengths=None):
     """One adaptive Golomb coder over a sample sequence split across the ranks in rank order
     (C5: each rank holds a band of tile rows). encode(n0, a0, bit0) -> (words, bits) codes this
     rank's samples from coder state (n0 samples, accumulated error a0) with its first codeword at
-    bit bit0 of words[0]. Exchanges: all-gather of (count, total), all-gather of the bit lengths,
-    point-to-point gather of the words. Returns (words, total_bits) on `dst`, (None, total_bits)
-    elsewhere."""
+    bit bit0 of words[0]; lengths(n0, a0) -> bits gives the same bit count without writing a
+    stream. Exchanges: all-gather of (count, total), all-gather of the bit lengths, point-to-point
+    gather of the words. Each rank's stream is written ONCE, at its global bit alignment: the
+    length comes first (`lengths`, a scan without the emission; without it, the words are written
+    at alignment 0 and written again only when the rank's offset is not a multiple of 64).
+    Returns (words, total_bits) on `dst`, (None, total_bits) elsewhere."""
     world, rank = dist.get_world_size(), dist.get_rank()
     n0, a0 = shard_state(count, total, device)
-    words, bits = encode(n0, a0, 0)
+    words = None
+    if lengths is not None:
+        bits = int(lengths(n0, a0))
+    else:
+        words, bits = encode(n0, a0, 0)
     lens = [x[0] for x in _allgather_i64([int(bits)], device)]
     b0s = [sum(lens[:r]) for r in range(world)]
     total_bits = sum(lens)
-    if b0s[rank] % 64:
+    if words is None or b0s[rank] % 64:
         words, _ = encode(n0, a0, b0s[rank] % 64)
     nwords = (b0s[rank] % 64 + int(bits) + 63) // 64
     gathered, offs = gather_streams(words, nwords, world, rank, dst)

@@ -165,7 +165,9 @@ int bic_encode_gray_packed(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size
 int bic_row_index(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
                   int predict, uint64_t* index);
 /* streams -> planes (device): slot_words > 0: plane p's stream at streams + p * slot_words;
- * slot_words == 0: packed, at streams + word_off[p]. plane_bits: each stream's length. Golomb needs
+ * slot_words == 0: packed, at streams + word_off[p], word_off[0..nplanes] as the packed encoders write
+ * it (plane p owns words word_off[p] .. word_off[p + 1]). plane_bits: each stream's length; a length
+ * past the plane's slot or packed words is malformed (nothing beyond them is read). Golomb needs
  * row_index (rows decode independently); EG finds the row of the plane's first 1 itself. predict:
  * the streams code the med residual; P(0, 0), which med discards, comes from p00 (device, one byte
  * per plane; nullable: 0). cols <= 16384. A malformed stream (bad codeword, wrong length, missing
@@ -182,7 +184,9 @@ size_t bic_encode_slot_words(size_t rows, size_t cols, int coder);
  * Coder state on entry: n0 samples already coded with accumulated error a0 (n0 = a0 = 0 is a
  * fresh GolombCoder). The stream is written starting at bit `bit0` of out (0 <= bit0 < 64;
  * lets a shard start at its global bit alignment); out[0 .. cap_words) must be writable.
- * bits_out (device, 2 x u64): [0] = codeword bits (= GolombCoder::bitcount), [1] = sum of samples. */
+ * bits_out (device, 2 x u64): [0] = codeword bits (= GolombCoder::bitcount), [1] = sum of samples.
+ * out = NULL with cap_words = 0 computes bits_out only (no stream): a shard learns its length
+ * before its bit offset is known, then encodes once at that offset. */
 int bic_golomb_encode_samples(bic_ctx* ctx, const uint32_t* samples, size_t n, uint64_t n0,
                               uint64_t a0, unsigned bit0, uint64_t* out, size_t cap_words,
                               uint64_t* bits_out);

@@ -129,7 +129,10 @@ def tiles(ctx, oracle, world, rank):
         out, bits = ctx.golomb_encode_samples(wts, n0=n0, a0=a0, bit0=bit0)
         return out, int(as_u64(bits)[0])
 
-    merged, total_bits = sharded_golomb(enc, wts.numel(), total, ctx.dev)
+    def lengths(n0, a0):
+        return int(as_u64(ctx.golomb_lengths(wts, n0=n0, a0=a0))[0])
+
+    merged, total_bits = sharded_golomb(enc, wts.numel(), total, ctx.dev, lengths=lengths)
     if rank:
         return True
     exp = oracle.patch_encode(I, cols, W, lt)

@@ -296,7 +296,9 @@ class Oracle:
 
 
 class Ref:
-    """The reference's own objects (oracle/_ref/libref.so), this container only."""
+    """The reference's own objects (oracle/_ref/libref.so): compiled in the build container from the
+    reference's sources (oracle/Makefile ref); the built library travels to the GPU box with the
+    tree (git-ignored, never committed), where bench.py times it as the CPU baseline. Test-side only."""
 
     def __init__(self, path=REF_SO):
         self.lib = L = C.CDLL(path)

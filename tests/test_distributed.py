@@ -85,7 +85,7 @@ def _golomb_py(samples, n0, a0, bit0):
     return torch.tensor(words, dtype=torch.int64), nbits
 
 
-def _sharded_worker(rank, world, port, q, samples):
+def _sharded_worker(rank, world, port, q, samples, use_lengths=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "binary-image-compression_amd"))
@@ -98,15 +98,21 @@ def _sharded_worker(rank, world, port, q, samples):
     try:
         lo, hi = rank * len(samples) // world, (rank + 1) * len(samples) // world
         mine = samples[lo:hi]
-        words, total = sharded_golomb(lambda n0, a0, b0: _golomb_py(mine, n0, a0, b0), len(mine), sum(mine),
-                                      torch.device("cpu"))
-        q.put((rank, None if words is None else words.tolist(), total))
+        calls = []
+
+        def enc(n0, a0, b0):
+            calls.append(b0)
+            return _golomb_py(mine, n0, a0, b0)
+        lengths = (lambda n0, a0: _golomb_py(mine, n0, a0, 0)[1]) if use_lengths else None
+        words, total = sharded_golomb(enc, len(mine), sum(mine), torch.device("cpu"), lengths=lengths)
+        q.put((rank, None if words is None else words.tolist(), total, calls))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("use_lengths", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_golomb_matches_one_coder(world):
+def test_sharded_golomb_matches_one_coder(world, use_lengths):
     """C5's exchange: the tile-weight sequence split over ranks, coded with the exchanged coder state
     and bit offsets, reassembled on rank 0 == one coder over the whole sequence"""
     import random
@@ -115,7 +121,7 @@ def test_sharded_golomb_matches_one_coder(world):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, samples)) for r in range(world)]
+    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, samples, use_lengths)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
@@ -128,3 +134,10 @@ def test_sharded_golomb_matches_one_coder(world):
     exp, nbits = _golomb_py(samples, 0, 0, 0)
     assert res[0][2] == nbits and all(res[r][1] is None for r in range(1, world))
     assert res[0][1] == exp.tolist()
+    if use_lengths:  # with a lengths-only call, each rank writes its stream exactly once, at its alignment
+        offs = [0]
+        for r in range(world):
+            lo, hi = r * len(samples) // world, (r + 1) * len(samples) // world
+            n0, a0 = lo, sum(samples[:lo])
+            offs.append(offs[-1] + _golomb_py(samples[lo:hi], n0, a0, 0)[1])
+        assert all(res[r][3] == [offs[r] % 64] for r in range(world)), [res[r][3] for r in range(world)]

@@ -88,6 +88,39 @@ def test_malformed_stream(ctx, oracle, coder):
     ctx.sync()  # the good stream decodes cleanly afterwards
 
 
+@pytest.mark.parametrize("coder", [CODER_GOLOMB, CODER_EG])
+@pytest.mark.parametrize("packed", [True, False])
+def test_inflated_length(ctx, oracle, coder, packed):
+    """a stated length past the plane's own words (its slot, or its packed words) is BIC_EDATA, and
+    nothing past them is read: plane 0's inflated length must not reach into plane 1's stream"""
+    rows, cols, n = 30, 500, 2
+    P = _planes(oracle, n, rows, cols, (0.3, 0.5))
+    d = ctx.to_dev(P)
+    idx = ctx.empty_i64(n * rows * 2)
+    if packed:
+        outs = ctx.encode_planes_packed(d, cols, True, golomb=coder == CODER_GOLOMB, eg=coder == CODER_EG,
+                                        row_index=idx)
+        out, bits, off = outs[0] if coder == CODER_GOLOMB else outs[1]
+        ctx.sync()
+        cap = int(as_u64(off)[1] - as_u64(off)[0])
+    else:
+        out, bits = ctx.encode_planes(d, cols, True, coder)
+        off = None
+        if coder == CODER_GOLOMB:
+            idx = ctx.row_index(d, cols, True)
+        ctx.sync()
+        cap = out.shape[1]
+    bad_bits = bits.clone()
+    bad_bits[0] = 64 * cap + 64 * 1000  # far past the plane's capacity
+    ctx.decode_planes(coder, out, bad_bits, n, rows, cols, True, word_off=off, row_index=idx)
+    with pytest.raises(pybic.BicError) as e:
+        ctx.sync()
+    assert e.value.code == pybic.BIC_EDATA
+    back = ctx.decode_planes(coder, out, bits, n, rows, cols, True, word_off=off, row_index=idx, p00=_p00(ctx, P))
+    ctx.sync()
+    assert np.array_equal(as_u64(back), P)
+
+
 def test_decode_rejects(ctx):
     t = ctx.empty_i64(4, 8)
     b = ctx.empty_i64(4)

@@ -56,18 +56,34 @@ def test_sharded_staged_encoder():
     assert "'frames': True" in out and "'planes': True" in out, out
 
 
-def test_bench_shard_planes_rehearsal():
-    """bench.py's plane-sharded C3 (--shard planes) at 2 ranks on one GPU over gloo: the gathered
-    streams of all 8 planes must pass its own bit_exact_check"""
-    port = _free_port()
+@pytest.mark.parametrize("workload", [
+    ["--workload", "c3", "--shard", "planes", "--rows", "512", "--cols", "4096"],
+    ["--workload", "c4", "--rows", "256", "--cols", "1024"],
+    ["--workload", "c5", "--rows", "1024", "--cols", "2048"],
+], ids=["c3-planes", "c4", "c5"])
+def test_bench_gpus2_spawns_ranks(workload):
+    """the plain command `bench.py --gpus 2 ...` (no launcher in the command: bench.py starts the two
+    ranks itself, as a child torch.distributed.run) on the one GPU over gloo: rank 0 prints one line
+    with n_gpus 2, and its bit_exact_check covers what rank 0 RECEIVED -- the gathered C3 plane
+    streams / all 64 C4 frames' streams, the merged C5 stream of the whole plane"""
+    import json
     env = dict(os.environ, BIC_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--workload", "c3", "--shard", "planes", "--rows", "512", "--cols", "4096",
-           "--steps", "2", "--warmup", "1"]
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *workload, "--steps", "2", "--warmup", "1"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
-    import json
-    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
-    j = json.loads(line)
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    j = json.loads(lines[0])
     assert j["bit_exact_check"] is True and j["n_gpus"] == 2 and j["scaling"] == "strong", j
+
+
+def test_bench_plane_count_one_rank():
+    """--plane-count 1 at N = 1: the per-rank step of an 8-GPU plane-sharded run, bit-exact"""
+    import json
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c3", "--shard", "planes", "--plane-count",
+           "1", "--rows", "512", "--cols", "4096", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    j = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert j["bit_exact_check"] is True and j["config"]["planes_per_gpu"] == 1, j

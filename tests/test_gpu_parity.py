@@ -1,5 +1,7 @@
 """HIP path (libbic.so, through the C ABI) against the CPU oracle and the golden vectors
 produced by the reference's own objects. Bit-exact everywhere (integer/bit work)."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -222,6 +224,13 @@ def test_golomb_samples_stream_and_shards(ctx, oracle):
     pre[w0 + 1:] = 0
     pre[w0:w0 + len(mine)] |= mine
     assert np.array_equal(pre, whole)
+    # the lengths-only call (no output) gives the same counts from the same coder state
+    b3 = ctx.golomb_lengths(ctx.to_dev(s[cut:]), n0=n0, a0=a0)
+    ctx.sync()
+    assert [int(x) for x in as_u64(b3)] == [int(x) for x in as_u64(b2)]
+    with pytest.raises(pybic.BicError):
+        ctx._chk(ctx.lib.bic_golomb_encode_samples(ctx.h, C.c_void_p(s.ctypes.data), 4, 0, 0, 0, None, 5,
+                                                   C.c_void_p(b3.data_ptr())), "no output with a capacity")
 
 
 # ------------------------------------------------------------------------------------------

@@ -44,6 +44,11 @@ def main():
     res = {"source": d, "method": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / WRITE_SIZE passes; "
                                  "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 read correction)",
            "kernels": {}}
+    try:
+        with open(f"{d}/sources.sha256") as f:
+            res["sources_sha256"] = f.read().strip()
+    except OSError:
+        res["sources_sha256"] = None
     for k, s in sorted(stats.items(), key=lambda kv: -kv[1]["total_ns"]):
         f = fetch.get((k, "FETCH_SIZE"), [])
         w = write.get((k, "WRITE_SIZE"), [])
