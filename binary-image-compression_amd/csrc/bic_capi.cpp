@@ -770,10 +770,11 @@ int bic_patch_search(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
   return BIC_OK;
 }
 
-int bic_match_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
-                     unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
-                     uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid,
-                     uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats) {
+static int match_encode_impl(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                             unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                             uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid,
+                             uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats,
+                             int invert, uint8_t* inverted) {
   int rc = bind(ctx);
   if (rc) return rc;
   if (!plane || !resid || !enuml || !stream_match || !stream_nomatch || !stats || cap_words == 0)
@@ -828,6 +829,8 @@ int bic_match_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
   a.weights = weights;
   a.modes = modes;
   a.flags = ctx->flags;
+  a.inv = invert ? 1u : 0u;
+  a.inverted = inverted;
   timed(ctx, "match_tiles", [&] { bic::launch_match_tiles(ctx->cur, a, sched, ctx->scratch); });
   timed(ctx, "match_code", [&] {
     bic::launch_match_code(ctx->cur, a, reinterpret_cast<unsigned long long*>(stream_match),
@@ -835,6 +838,22 @@ int bic_match_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
   });
   BIC_HIP(hipGetLastError());
   return BIC_OK;
+}
+
+int bic_match_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                     unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                     uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid,
+                     uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats) {
+  return match_encode_impl(ctx, plane, rows, cols, wpr, W, T, R, enuml, besti, bestj, bestd, weights, modes, resid,
+                           stream_match, stream_nomatch, cap_words, stats, 0, nullptr);
+}
+
+int bic_match_encode_inv(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                         unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                         uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint8_t* inverted, uint64_t* resid,
+                         uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats) {
+  return match_encode_impl(ctx, plane, rows, cols, wpr, W, T, R, enuml, besti, bestj, bestd, weights, modes, resid,
+                           stream_match, stream_nomatch, cap_words, stats, 1, inverted);
 }
 
 int bic_set_match_parts(bic_ctx* ctx, unsigned parts) {
@@ -849,6 +868,23 @@ int bic_pbm_unpack(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols
   if (!geom_ok(rows, cols, wpr) || (rows && (!raster || !plane))) return BIC_EINVAL;
   timed(ctx, "pbm_unpack", [&] {
     bic::launch_pbm(ctx->cur, false, raster, nullptr, nullptr, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
+}
+
+int bic_planes_to_gray(bic_ctx* ctx, const uint64_t* planes, int plane0, int nplanes, size_t rows, size_t cols,
+                       size_t wpr, int sample_bytes, void* gray, size_t pitch) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if ((sample_bytes != 1 && sample_bytes != 2) || plane0 < 0 || nplanes < 1 || plane0 + nplanes > 8 * sample_bytes)
+    return BIC_EINVAL;
+  if (!geom_ok(rows, cols, wpr) || pitch < cols * (size_t)sample_bytes || (rows && (!planes || !gray)))
+    return BIC_EINVAL;
+  if (rows == 0) return BIC_OK;
+  timed(ctx, "planes_to_gray", [&] {
+    bic::launch_planes_gray(ctx->cur, planes, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, plane0, nplanes,
+                            sample_bytes, static_cast<uint8_t*>(gray), (uint64_t)pitch);
   });
   BIC_HIP(hipGetLastError());
   return BIC_OK;

@@ -174,6 +174,8 @@ struct MatchArgs {
   uint32_t *besti, *bestj, *bestd, *weights;
   uint8_t* modes;
   uint32_t* flags;
+  uint32_t inv;                     // compress8_test.cpp's patch inversion (0: compress7_test.cpp)
+  uint8_t* inverted;                // per tile: the patch was flipped (nullable)
 };
 constexpr uint32_t kSchedTiles = 0, kSchedRows = 1, kSchedTeam = 2;
 struct MatchSched {
@@ -191,6 +193,8 @@ void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* ras
 // P5 samples (1 or 2 bytes, any alignment) -> planes plane0.. (bic_raster.hip)
 void launch_raster_planes(hipStream_t s, const uint8_t* raster, int bpp, uint32_t rows, uint32_t cols, int plane0,
                           int nplanes, uint64_t* planes, uint32_t wpr);
+void launch_planes_gray(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, int plane0,
+                        int nplanes, int bps, uint8_t* gray, uint64_t pitch);
 
 // GF(2) algebra (bic_gf2.hip)
 void launch_gf2_transpose(hipStream_t s, const uint64_t* src, uint32_t s_rows, uint32_t s_stride, uint32_t s_words,

@@ -58,6 +58,27 @@ __device__ __forceinline__ unsigned long long make_key(uint32_t d, uint32_t T, u
   return ((unsigned long long)(d <= T ? 0u : d) << kDpShift) | ((unsigned long long)pos << kIdxShift) | d;
 }
 __device__ __forceinline__ uint64_t key_pos(unsigned long long key) { return (key >> kIdxShift) & kIdxMask; }
+// compress8_test.cpp:156-161: with inversion a window's distance is min(d, M - d) (M - d taken when
+// strictly smaller: that window is inverted). The distance field keeps d (13 bits) or, inverted
+// mode, min(d, M - d) <= M / 2 <= 2048 in 12 bits and the window's inversion in bit 12 (the field
+// is below the scan index: it never decides between keys).
+__device__ __forceinline__ unsigned long long win_key(uint32_t d, uint32_t T, uint64_t pos, uint32_t M, uint32_t inv) {
+  if (!inv) return make_key(d, T, pos);
+  const bool f = M - d < d;
+  const uint32_t e = f ? M - d : d;
+  return ((unsigned long long)(e <= T ? 0u : e) << kDpShift) | ((unsigned long long)pos << kIdxShift) | e |
+         (f ? 0x1000ull : 0ull);
+}
+__device__ __forceinline__ uint32_t key_dist(unsigned long long key, uint32_t inv) {
+  return (uint32_t)(key & (inv ? 0xfffu : 0x1fffu));
+}
+__device__ __forceinline__ int key_flip(unsigned long long key, uint32_t inv) { return inv ? (int)((key >> 12) & 1) : 0; }
+// compress8_test.cpp:137: a tile of weight <= T or >= M - T (idx_t arithmetic) is a "perfect match"
+// before any window is searched
+__device__ __forceinline__ bool perfect_before(const MatchArgs& a, uint32_t w0) {
+  const uint64_t M = (uint64_t)a.W * a.W;
+  return a.inv && (w0 <= a.T || (uint64_t)w0 >= M - (uint64_t)a.T);
+}
 
 struct Region {
   int i0, j0, mini, minj, maxj, mini2, maxj2;
@@ -156,10 +177,17 @@ __device__ __forceinline__ uint64_t row_bits(const MatchArgs& a, const Region& g
 // The tile's decision (:184-272), one lane per tile row r (lanes r >= W pass p = b = 0): p = tile
 // row, b = row of the best window (0 when the region is empty), both MSB-aligned W bits. Writes the
 // per-tile outputs and returns the row of the residual that is written back.
+// flip: the best window's inversion, -1 without a window (compress8: bestinv then stays
+// (P.weight() - M) < P.weight(), :136: the tile is all 1s); always -1 / ignored without inversion.
 __device__ uint64_t decide_tile(const MatchArgs& a, const double* enuml, const Region& g, uint32_t t, int bi,
-                                int bj, uint32_t bd, uint64_t p, uint64_t b, int r) {
+                                int bj, uint32_t bd, int flip, uint64_t p, uint64_t b, int r) {
   const int W = (int)a.W;
   const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
+  bool inv = false;
+  if (a.inv) {  // compress8_test.cpp:136, :163, :207-210
+    inv = flip >= 0 ? flip != 0 : wave_total_u32((uint32_t)__popcll(p)) == (uint32_t)(W * W);
+    if (inv && r < W) p = ~p & topW;
+  }
   const uint64_t p3 = p ^ b;
   // med inside the tile (compress7_test.cpp:43-55; (0,0) is never written: 0 here)
   const uint64_t pu = wave_shr1_u64(p), p3u = wave_shr1_u64(p3);  // the row above (0 for row 0)
@@ -175,8 +203,9 @@ __device__ uint64_t decide_tile(const MatchArgs& a, const double* enuml, const R
   uint64_t mn_len = ~0ull, mp_len = ~0ull;  // search_win_size <= 0: log2 -> 2^63, never a match
   if (g.swin >= 1) {
     const uint64_t idx_len = g.swin == 1 ? 0 : 64 - (uint64_t)__clzll((unsigned long long)(g.swin - 1));
-    mn_len = (uint64_t)((double)(2 + idx_len) + enuml[w_mn]);
-    mp_len = (uint64_t)((double)(2 + idx_len) + enuml[w_mp]);
+    const uint64_t fixed = a.inv ? 3 : 2;  // compress8_test.cpp:250-251: one more bit (invert / not)
+    mn_len = (uint64_t)((double)(fixed + idx_len) + enuml[w_mn]);
+    mp_len = (uint64_t)((double)(fixed + idx_len) + enuml[w_mp]);
   }
   const bool mpred = mn_len > mp_len, npred = nn_len > np_len;  // :232, :243
   const uint64_t match_len = mpred ? mp_len : mn_len, nomatch_len = npred ? np_len : nn_len;
@@ -188,6 +217,7 @@ __device__ uint64_t decide_tile(const MatchArgs& a, const double* enuml, const R
     a.weights[t] = take ? (mpred ? w_mp : w_mn) : (npred ? w_np : w_nn);
     a.lens[t] = (uint32_t)(take ? match_len : nomatch_len);
     a.modes[t] = take ? (mpred ? 'X' : 'x') : (npred ? 'O' : 'o');
+    if (a.inverted) a.inverted[t] = inv ? 1 : 0;
   }
   return take ? (mpred ? dp3 : p3) : (npred ? dp : p);
 }
@@ -212,9 +242,16 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
   }
   if (tid < (uint32_t)W) Pl[tid] = row_bits<LDS>(a, g, S, g.i0 + (int)tid, g.j0) & topW;
   __syncthreads();
+  bool skip = false;
+  if (a.inv) {  // compress8_test.cpp:137: no search at all for a nearly empty / full tile
+    uint32_t w0 = 0;
+    for (int r = 0; r < W; ++r) w0 += (uint32_t)__popcll(Pl[r]);
+    skip = perfect_before(a, w0);
+  }
+  const uint32_t M = (uint32_t)(W * W);
 
   // this part's share of the scan, in chunks; a window at distance <= T ends the search
-  const uint64_t lo = part * g.n / a.G, hi = (part + 1) * g.n / a.G;
+  const uint64_t lo = part * g.n / a.G, hi = skip ? lo : (part + 1) * g.n / a.G;
   unsigned long long best = ~0ull;
   uint32_t chunk = 0;
   for (uint64_t base = lo; base < hi; base += kChunk, ++chunk) {
@@ -227,7 +264,7 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
         pos_window(g, W, pos, i2, j2);
         uint32_t d = 0;
         for (int r = 0; r < W; ++r) d += (uint32_t)__popcll((row_bits<LDS>(a, g, S, i2 + r, j2) ^ Pl[r]) & topW);
-        const unsigned long long key = make_key(d, a.T, pos);
+        const unsigned long long key = win_key(d, a.T, pos, M, a.inv);
         best = key < best ? key : best;
       }
     }
@@ -255,16 +292,16 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
   // ---- the last workgroup finishes the tile (one lane per tile row) ----
   const unsigned long long key = __hip_atomic_load(&a.key[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int r = (int)tid;
-  const uint32_t M = (uint32_t)(W * W);
   uint32_t bd = M + 1;
-  int bi = 0, bj = 0;
+  int bi = 0, bj = 0, flip = -1;
   if (key != ~0ull) {  // :184-189 (any window at all beats M + 1)
-    bd = (uint32_t)(key & 0x1fff);
+    bd = key_dist(key, a.inv);
+    flip = key_flip(key, a.inv);
     pos_window(g, W, key_pos(key), bi, bj);
   }
   const uint64_t p = r < W ? Pl[r] : 0ull;
   const uint64_t b = (key != ~0ull && r < W) ? (row_bits<LDS>(a, g, S, bi + r, bj) & topW) : 0ull;
-  const uint64_t res = decide_tile(a, a.enuml, g, t, bi, bj, bd, p, b, r);
+  const uint64_t res = decide_tile(a, a.enuml, g, t, bi, bj, bd, flip, p, b, r);
   // residual write-back (:266 / :272): W bits at (i0 + r, j0), one or two words
   if (r < W) {
     uint64_t* row = a.I + (uint64_t)(g.i0 + r) * a.wpr + (g.j0 >> 6);
@@ -375,8 +412,8 @@ __device__ __forceinline__ void band_load(uint32_t* L, const Band& b, const Matc
 // every window left (every window a later call of this workgroup scans has a larger index).
 template <int KW, int kGK>
 __device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, const uint32_t* PW, uint32_t T,
-                                           int i_top, uint32_t nrows, int j_top, uint32_t ncols, uint32_t loop,
-                                           uint32_t t0, uint32_t t1, uint32_t skip_a, uint32_t skip_c,
+                                           uint32_t inv, int i_top, uint32_t nrows, int j_top, uint32_t ncols,
+                                           uint32_t loop, uint32_t t0, uint32_t t1, uint32_t skip_a, uint32_t skip_c,
                                            unsigned long long& best, bool& stop) {
   // 32/KW consecutive rows of KW bits share one 32-bit word, so a window's distance is KW/(32/KW)
   // xor + popcount pairs (PW: the tile's rows packed the same way)
@@ -418,7 +455,7 @@ __device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, co
 #pragma unroll
             for (int r = 0; r < kNW; ++r)
               d += (uint32_t)__popc(pk[kGK - 1 - u + r * kPack] ^ (kHoist ? Pr[kHoist ? r : 0] : PW[r]));
-            const unsigned long long key = make_key(d, T, scan_pos(loop, a0 + (uint32_t)u, c));
+            const unsigned long long key = win_key(d, T, scan_pos(loop, a0 + (uint32_t)u, c), KW * KW, inv);
             best = key < best ? key : best;
           }
         }
@@ -440,7 +477,7 @@ __device__ __forceinline__ void scan_tasks(const uint32_t* L, const Band& bd, co
 // any W <= 64: one window per task
 __device__ __forceinline__ void scan_loop_any(const uint32_t* L, const Band& bd, const uint64_t* P, int W,
                                               int i_top, uint32_t nrows, int j_top, uint32_t ncols, uint32_t loop,
-                                              uint32_t T, unsigned long long& best, bool& stop) {
+                                              uint32_t T, uint32_t inv, unsigned long long& best, bool& stop) {
   if (stop || nrows == 0 || ncols == 0) return;
   const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
   const uint32_t n = nrows * ncols;
@@ -451,7 +488,7 @@ __device__ __forceinline__ void scan_loop_any(const uint32_t* L, const Band& bd,
       const int i2 = i_top - (int)q, j2 = j_top - (int)(i - q * ncols);
       uint32_t d = 0;
       for (int r = 0; r < W; ++r) d += (uint32_t)__popcll((band_bits64(L, bd, i2 + r, j2) ^ P[r]) & topW);
-      const unsigned long long key = make_key(d, T, scan_pos(loop, q, i - q * ncols));
+      const unsigned long long key = win_key(d, T, scan_pos(loop, q, i - q * ncols), (uint32_t)(W * W), inv);
       best = key < best ? key : best;
     }
     const uint32_t nt = base + kRB;
@@ -519,12 +556,17 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
     __syncthreads();
     unsigned long long best = ~0ull;
     bool stop = false;
+    if (a.inv) {  // compress8_test.cpp:137
+      uint32_t w0 = 0;
+      for (int r = 0; r < W; ++r) w0 += (uint32_t)__popcll(P64[r]);
+      stop = perfect_before(a, w0);
+    }
     // loop 1: i2 = i0 .. mini2, j2 = maxj2 .. minj; loop 2: i2 = i0-W .. mini, j2 = maxj .. minj
     const uint32_t n1r = (uint32_t)(g.i0 - g.mini2 + 1);
     const int n2r_ = g.i0 - W - g.mini + 1;
     const uint32_t n2r = n2r_ > 0 ? (uint32_t)n2r_ : 0;
-    scan_loop_any(L, bd, P64, W, g.i0, n1r, g.maxj2, g.n1c, 0, a.T, best, stop);
-    scan_loop_any(L, bd, P64, W, g.i0 - W, n2r, g.maxj, g.n2c, 1, a.T, best, stop);
+    scan_loop_any(L, bd, P64, W, g.i0, n1r, g.maxj2, g.n1c, 0, a.T, a.inv, best, stop);
+    scan_loop_any(L, bd, P64, W, g.i0 - W, n2r, g.maxj, g.n2c, 1, a.T, a.inv, best, stop);
     best = wave_min_u64(best);
     if (lane_id() == 0) red[tid >> 6] = best;
     __syncthreads();
@@ -533,14 +575,15 @@ __global__ __launch_bounds__(kRB) void k_match_rows(MatchArgs a, uint32_t* progr
       for (int w = 1; w < kRB / 64; ++w) key = red[w] < key ? red[w] : key;
       const int r = (int)tid;
       uint32_t bdist = (uint32_t)(W * W) + 1;
-      int bi = 0, bj = 0;
+      int bi = 0, bj = 0, flip = -1;
       if (key != ~0ull) {
-        bdist = (uint32_t)(key & 0x1fff);
+        bdist = key_dist(key, a.inv);
+        flip = key_flip(key, a.inv);
         pos_window(g, W, key_pos(key), bi, bj);
       }
       const uint64_t p = r < W ? P64[r] : 0ull;
       const uint64_t b = (key != ~0ull && r < W) ? (band_bits64(L, bd, bi + r, bj) & topW) : 0ull;
-      const uint64_t res = decide_tile(a, a.enuml, g, t, bi, bj, bdist, p, b, r);
+      const uint64_t res = decide_tile(a, a.enuml, g, t, bi, bj, bdist, flip, p, b, r);
       if (r < W) {
         // write-back: the plane (for the rows below) and the band image (for the tiles to the right)
         uint64_t* row = a.I + (uint64_t)(g.i0 + r) * a.wpr + (g.j0 >> 6);
@@ -676,26 +719,32 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
     if (role == 0 && tid == 0) MSTAMP(t, 3);
     unsigned long long best = ~0ull;
     bool stop = false;
+    if (a.inv) {  // compress8_test.cpp:137 (main and helpers alike: no window is searched)
+      uint32_t w0 = 0;
+#pragma unroll
+      for (int r = 0; r < W; ++r) w0 += (uint32_t)__popcll(P64[r]);
+      stop = perfect_before(a, w0);
+    }
     const uint32_t n1r = (uint32_t)(g.i0 - g.mini2 + 1);
     const int n2r_ = g.i0 - W - g.mini + 1;
     const uint32_t n2r = n2r_ > 0 ? (uint32_t)n2r_ : 0;
     const uint32_t N1 = (n1r + kGK - 1) / kGK * g.n1c, N2 = (n2r + kGK - 1) / kGK * g.n2c;
     if (role == 0) {
       if (H == 0) {
-        scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0, n1r, g.maxj2, g.n1c, 0, 0, N1, 0, 0, best, stop);
-        scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0 - W, n2r, g.maxj, g.n2c, 1, 0, N2, 0, 0, best, stop);
+        scan_tasks<KW, kGK>(L, bd, PW, a.T, a.inv, g.i0, n1r, g.maxj2, g.n1c, 0, 0, N1, 0, 0, best, stop);
+        scan_tasks<KW, kGK>(L, bd, PW, a.T, a.inv, g.i0 - W, n2r, g.maxj, g.n2c, 1, 0, N2, 0, 0, best, stop);
       } else {  // the windows over the K tiles to the left (loop 1, a < W, c < K*W), one per thread
         const uint32_t fa = min(n1r, (uint32_t)W), fc = min(g.n1c, KWc);
         if (tid == 0) MSTAMP(t, 8);
-        scan_tasks<KW, 4>(L, bd, PW, a.T, g.i0, fa, g.maxj2, fc, 0, 0, (fa + 3) / 4 * fc, 0, 0, best, stop);
+        scan_tasks<KW, 4>(L, bd, PW, a.T, a.inv, g.i0, fa, g.maxj2, fc, 0, 0, (fa + 3) / 4 * fc, 0, 0, best, stop);
         if (tid == 0) MSTAMP(t, 9);
       }
     } else {
       const uint32_t h = role - 1, N = N1 + N2;
       const uint32_t lo = (uint32_t)((uint64_t)h * N / H), hi = (uint32_t)((uint64_t)(h + 1) * N / H);
-      scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0, n1r, g.maxj2, g.n1c, 0, lo, min(hi, N1), W, KWc, best, stop);
-      scan_tasks<KW, kGK>(L, bd, PW, a.T, g.i0 - W, n2r, g.maxj, g.n2c, 1, max(lo, N1) - N1, hi > N1 ? hi - N1 : 0,
-                          0, 0, best, stop);
+      scan_tasks<KW, kGK>(L, bd, PW, a.T, a.inv, g.i0, n1r, g.maxj2, g.n1c, 0, lo, min(hi, N1), W, KWc, best, stop);
+      scan_tasks<KW, kGK>(L, bd, PW, a.T, a.inv, g.i0 - W, n2r, g.maxj, g.n2c, 1, max(lo, N1) - N1,
+                          hi > N1 ? hi - N1 : 0, 0, 0, best, stop);
     }
     best = wave_min_u64(best);
     if (role == 0 && tid == 0) MSTAMP(t, 10);
@@ -732,14 +781,15 @@ __global__ __launch_bounds__(kRB) void k_match_team(MatchArgs a, uint32_t* progr
         }
         if (tid == 0) MSTAMP(t, 5);
         uint32_t bdist = (uint32_t)(W * W) + 1;
-        int bi = 0, bj = 0;
+        int bi = 0, bj = 0, flip = -1;
         if (key != ~0ull) {
-          bdist = (uint32_t)(key & 0x1fff);
+          bdist = key_dist(key, a.inv);
+          flip = key_flip(key, a.inv);
           pos_window(g, W, key_pos(key), bi, bj);
         }
         const uint64_t p = r < W ? P64[r] : 0ull;
         const uint64_t b = (key != ~0ull && r < W) ? (band_bits64(L, bd, bi + r, bj) & topW) : 0ull;
-        const uint64_t res = decide_tile(a, E, g, t, bi, bj, bdist, p, b, r);
+        const uint64_t res = decide_tile(a, E, g, t, bi, bj, bdist, flip, p, b, r);
         if (r < W) {
           uint32_t* q = L + (uint32_t)(g.i0 + r - bd.lo) * bd.pitch + ((uint32_t)g.j0 >> 5);
           const int s32 = g.j0 & 31;

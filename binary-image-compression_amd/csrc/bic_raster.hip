@@ -128,6 +128,77 @@ __global__ __launch_bounds__(256) void k_raster_planes(const uint8_t* __restrict
       for (uint32_t q = used; q < wpr; ++q) planes[b * plane_words + (uint64_t)row * wpr + q] = 0;  // pad words
 }
 
+// planes plane0 .. plane0 + nplanes - 1 -> gray samples (plane2pgm_tool.cpp:33-52: sample |= mask
+// for every set bit of plane b, mask = 1 << b; bits no plane covers are 0). Lane = word w of a row
+// (64 samples): byte (plane0 + b) & 7 of each group's 8x8 block holds plane b's byte, the 8x8 bit
+// transpose (an involution) turns it back into 8 samples' bytes. BPS 1: one byte per sample; BPS 2:
+// two bytes big-endian (the P5 layout write_p5_data uses for maxval >= 256, pnm.cpp:111-124).
+// 16-byte stores when the row's bytes are 16-byte aligned (VEC), byte stores otherwise.
+template <int BPS, bool VEC>
+__global__ __launch_bounds__(256) void k_planes_gray(const uint64_t* __restrict__ planes, uint32_t rows, uint32_t cols,
+                                                     uint32_t wpr, int plane0, int nplanes, uint8_t* __restrict__ gray,
+                                                     uint64_t pitch) {
+  const uint32_t groups = (cols + 4095) / 4096;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= (uint64_t)rows * groups) return;
+  const uint32_t row = (uint32_t)(gw / groups), w = (uint32_t)(gw % groups) * 64 + lane_id();
+  const uint32_t used = (cols + 63) / 64;
+  if (w >= used) return;
+  const uint64_t plane_words = (uint64_t)rows * wpr;
+  const uint64_t* src = planes + (uint64_t)row * wpr + w;
+  uint64_t TL[8], TH[8];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) TL[g] = TH[g] = 0;
+  for (int b = 0; b < nplanes; ++b) {
+    const uint64_t v = src[b * plane_words];
+    const int sb = b + plane0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const uint64_t byte = ((v >> (56 - 8 * g)) & 0xffull) << (8 * (sb & 7));
+      if (sb < 8) TL[g] |= byte;
+      else TH[g] |= byte;
+    }
+  }
+  uint32_t out[BPS * 16];  // the 64 samples' bytes in file order
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const uint64_t lo = bswap64(transpose8x8_r(TL[g]));  // byte k = sample 8g + k's low byte
+    if constexpr (BPS == 1) {
+      out[2 * g] = (uint32_t)lo;
+      out[2 * g + 1] = (uint32_t)(lo >> 32);
+    } else {
+      const uint64_t hi = bswap64(transpose8x8_r(TH[g]));
+      // big-endian samples: hi0 lo0 hi1 lo1 ...
+      const uint32_t l0 = (uint32_t)lo, l1 = (uint32_t)(lo >> 32), h0 = (uint32_t)hi, h1 = (uint32_t)(hi >> 32);
+      out[4 * g] = __builtin_amdgcn_perm(l0, h0, 0x05010400u);
+      out[4 * g + 1] = __builtin_amdgcn_perm(l0, h0, 0x07030602u);
+      out[4 * g + 2] = __builtin_amdgcn_perm(l1, h1, 0x05010400u);
+      out[4 * g + 3] = __builtin_amdgcn_perm(l1, h1, 0x07030602u);
+    }
+  }
+  uint8_t* dst = gray + (uint64_t)row * pitch + (uint64_t)w * 64 * BPS;
+  const uint32_t valid = min(64u, cols - 64 * w);
+  if (VEC && valid == 64) {
+#pragma unroll
+    for (int q = 0; q < BPS * 4; ++q)
+      reinterpret_cast<uint4*>(dst)[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+    return;
+  }
+  for (uint32_t i = 0; i < valid * BPS; ++i) dst[i] = (uint8_t)(out[i >> 2] >> (8 * (i & 3)));
+}
+
+void launch_planes_gray(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, int plane0,
+                        int nplanes, int bps, uint8_t* gray, uint64_t pitch) {
+  const uint64_t waves = (uint64_t)rows * ((cols + 4095) / 4096);
+  const uint32_t grid = (uint32_t)((waves + 3) / 4);
+  if (!grid) return;
+  const bool vec = reinterpret_cast<uintptr_t>(gray) % 16 == 0 && pitch % 16 == 0;
+#define BIC_PG(B, V) k_planes_gray<B, V><<<grid, 256, 0, s>>>(planes, rows, cols, wpr, plane0, nplanes, gray, pitch)
+  if (bps == 1) { if (vec) BIC_PG(1, true); else BIC_PG(1, false); }
+  else { if (vec) BIC_PG(2, true); else BIC_PG(2, false); }
+#undef BIC_PG
+}
+
 void launch_pbm(hipStream_t s, bool pack, const uint8_t* raster_in, uint8_t* raster_out, const uint64_t* plane_in,
                 uint64_t* plane_out, uint32_t rows, uint32_t cols, uint32_t wpr) {
   if (!pack) {

@@ -29,7 +29,7 @@ EXPORTS = [
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
     "bic_bitplanes_u8_range", "bic_encode_gray_range", "bic_encode_planes_packed", "bic_encode_gray_packed",
     "bic_row_index", "bic_decode_planes", "bic_pgm_bitplanes", "bic_pnm_parse_header",
-    "bic_gf2_transpose", "bic_gf2_mul",
+    "bic_gf2_transpose", "bic_gf2_mul", "bic_planes_to_gray", "bic_match_encode_inv",
 ]
 
 # bic_gf2_mul ops (include/bic.h)
@@ -105,6 +105,7 @@ def load(path=LIB_PATH):
     sig("bic_patch_search", i32, [vp, vp, sz, sz, sz, u32, vp, vp, vp])
     sig("bic_match_encode", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_set_match_parts", i32, [vp, u32])
+    sig("bic_match_encode_inv", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_encode_gray", i32, [vp, vp, sz, sz, sz, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
     sig("bic_bitplanes_u8_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz])
     sig("bic_encode_gray_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
@@ -116,6 +117,7 @@ def load(path=LIB_PATH):
     sig("bic_pnm_parse_header", i32, [C.c_char_p, sz, C.POINTER(PnmInfo)])
     sig("bic_gf2_transpose", i32, [vp, vp, sz, sz, sz, vp, sz])
     sig("bic_gf2_mul", i32, [vp, i32, vp, sz, sz, sz, vp, sz, sz, sz, vp, sz, sz, sz])
+    sig("bic_planes_to_gray", i32, [vp, vp, i32, i32, sz, sz, sz, i32, vp, sz])
     _lib = L
     return L
 
@@ -450,8 +452,9 @@ class Context:
                   "bic_patch_search")
         return tuple(out)
 
-    def match_encode(self, plane, cols, W, T=0, R=128, enuml=None, cap_words=None, resid=None):
-        """compress7_test.cpp's tile loop with search window R and threshold T (bic_match_encode).
+    def match_encode(self, plane, cols, W, T=0, R=128, enuml=None, cap_words=None, resid=None, invert=False):
+        """compress7_test.cpp's tile loop with search window R and threshold T (bic_match_encode);
+        invert: compress8_test.cpp's patch-inversion variant (bic_match_encode_inv, `inverted` per tile).
         plane: int64 [rows, wpr] device tensor (not modified); enuml: numpy float64 [W*W+1] (host),
         default enumL from this build. Returns device tensors per tile and the two streams."""
         rows, wpr = plane.shape
@@ -464,13 +467,20 @@ class Context:
         sm, sn = self.empty_i64(cap_words), self.empty_i64(cap_words)
         stats = self.empty_i64(4)
         e = enum_table(W) if enuml is None else np.ascontiguousarray(enuml, np.float64)
+        inv = t.empty(nt, dtype=t.uint8, device=self.dev) if invert else None
         self._bind_stream()
-        self._chk(self.lib.bic_match_encode(self.h, _p(plane), rows, cols, wpr, W, T, R,
-                                            e.ctypes.data_as(C.c_void_p), _p(bi), _p(bj), _p(bd), _p(wt),
-                                            _p(modes), _p(resid), _p(sm), _p(sn), cap_words, _p(stats)),
-                  "bic_match_encode")
+        if invert:
+            self._chk(self.lib.bic_match_encode_inv(self.h, _p(plane), rows, cols, wpr, W, T, R,
+                                                    e.ctypes.data_as(C.c_void_p), _p(bi), _p(bj), _p(bd), _p(wt),
+                                                    _p(modes), _p(inv), _p(resid), _p(sm), _p(sn), cap_words,
+                                                    _p(stats)), "bic_match_encode_inv")
+        else:
+            self._chk(self.lib.bic_match_encode(self.h, _p(plane), rows, cols, wpr, W, T, R,
+                                                e.ctypes.data_as(C.c_void_p), _p(bi), _p(bj), _p(bd), _p(wt),
+                                                _p(modes), _p(resid), _p(sm), _p(sn), cap_words, _p(stats)),
+                      "bic_match_encode")
         return dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes, resid=resid, stream_match=sm,
-                    stream_nomatch=sn, stats=stats)
+                    stream_nomatch=sn, stats=stats, inverted=inv)
 
     def set_match_parts(self, parts):
         self._chk(self.lib.bic_set_match_parts(self.h, parts), "bic_set_match_parts")
@@ -482,6 +492,18 @@ class Context:
         self._bind_stream()
         self._chk(self.lib.bic_pgm_bitplanes(self.h, _p(raster), rows, cols, maxval, plane0, nplanes, _p(out), wpr),
                   "bic_pgm_bitplanes")
+        return out
+
+    def planes_to_gray(self, planes, cols, plane0=0, sample_bytes=1, out=None, pitch=None):
+        """bic_planes_to_gray: planes int64 [n, rows, wpr] -> uint8 device tensor [rows, pitch] of samples
+        (sample_bytes 2: big-endian 16-bit, as a P5 raster with maxval >= 256)"""
+        planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
+        n, rows, wpr = planes.shape
+        pitch = pitch or cols * sample_bytes
+        out = self.torch.zeros(rows, pitch, dtype=self.torch.uint8, device=self.dev) if out is None else out
+        self._bind_stream()
+        self._chk(self.lib.bic_planes_to_gray(self.h, _p(planes), plane0, n, rows, cols, wpr, sample_bytes, _p(out),
+                                              pitch), "bic_planes_to_gray")
         return out
 
     def pbm_unpack(self, raster, rows, cols, wpr=None):

@@ -236,6 +236,20 @@ int bic_match_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
                      unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
                      uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid,
                      uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats);
+/* compress8_test.cpp:126-272's loop (patch inversion), otherwise as bic_match_encode:
+ *   - a window's distance d becomes M - d when (M - d) < d, the window then inverted (:156-161);
+ *     bestd is that min(d, M - d);
+ *   - before any search a tile of weight <= T or >= M - T is a perfect match (:137: no window);
+ *   - bestinv starts as (P.weight() - M) < P.weight() (:136, idx_t: the tile is all 1s) and takes
+ *     the inversion of each better window (:163); an inverted tile is flipped (P.flip(), :207-210)
+ *     before P3 and all four weights are formed;
+ *   - the match lengths are 3 + idx_len + enumL (one bit more, :250-251).
+ * inverted (device, per tile, nullable): bestinv. The driver leaves a non-inverted window's `inv`
+ * uninitialised (:157); here it is false. T is the caller's (the driver's default is its goodT, :73). */
+int bic_match_encode_inv(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t cols, size_t wpr, unsigned W,
+                         unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                         uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint8_t* inverted, uint64_t* resid,
+                         uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats);
 /* Schedule of bic_match_encode (every schedule gives the same result): 0 (default) = automatic;
  * N in 1..256 = N workgroups per tile, tiles in raster order with flags between them;
  * 0x10000 | H = one workgroup per tile row walking its tiles, plus H helper workgroups that search
@@ -280,6 +294,15 @@ int bic_pnm_parse_header(const uint8_t* bytes, size_t n, bic_pnm_info* info);
  * sample when maxval < 256 else 2 bytes big-endian (pnm.cpp:71-74), rows of cols samples. */
 int bic_pgm_bitplanes(bic_ctx* ctx, const uint8_t* raster, size_t rows, size_t cols, int maxval, int plane0,
                       int nplanes, uint64_t* planes, size_t wpr);
+/* planes -> gray samples on the device (replaces plane2pgm_tool.cpp:33-52, the reassembly loop
+ * `gray_img[li] |= mask` over planes 0, 1, ... with mask = 1 << plane): plane b sets bit plane0 + b
+ * of each sample, bits no plane covers are 0. sample_bytes 1: one byte per sample (plane0 + nplanes
+ * <= 8); 2: two bytes big-endian, the P5 raster write_p5_data writes for maxval >= 256
+ * (pnm.cpp:111-124; plane0 + nplanes <= 16). gray: device, rows of `pitch` bytes (any alignment);
+ * only the rows' first cols * sample_bytes bytes are written. The device round trip is then
+ * gray -> bic_encode_gray_packed -> bic_decode_planes -> bic_planes_to_gray. */
+int bic_planes_to_gray(bic_ctx* ctx, const uint64_t* planes, int plane0, int nplanes, size_t rows, size_t cols,
+                       size_t wpr, int sample_bytes, void* gray, size_t pitch);
 
 /* ---- f4: binary_matrix algebra over GF(2) (binmat.cpp:199-214, 516-616) ---------------------
  * Matrices are rows x cols bits in the plane layout (wpr >= ceil(cols/64) words per row, device

@@ -86,6 +86,18 @@ void bo_bitplanes(const void* gray, int bytes_per_px, size_t rows, size_t cols,
     }
 }
 
+void bo_planes_to_gray(const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
+                       uint32_t* gray) {
+    memset(gray, 0, sizeof(uint32_t) * rows * cols);       /* plane2pgm_tool.cpp:27 */
+    unsigned mask = 0x01;                                    /* plane2pgm_tool.cpp:32 */
+    for (int b = 0; b < nplanes; ++b, mask <<= 1) {         /* :33-50, one plane per pass */
+        const uint64_t* A = planes + (size_t)b * rows * wpr;
+        for (size_t i = 0, li = 0; i < rows; ++i)            /* :35-41 */
+            for (size_t j = 0; j < cols; ++j, ++li)
+                if (bo_get(A, wpr, i, j)) gray[li] |= mask;
+    }
+}
+
 void bo_med(const uint64_t* P, uint64_t* R, size_t rows, size_t cols, size_t wpr) {
     memset(R, 0, sizeof(uint64_t) * rows * wpr);
     if (rows == 0 || cols == 0) return;
@@ -615,6 +627,23 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
                     const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
                     uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
                     uint8_t* stream_nomatch, size_t cap_bytes) {
+    return bo_match_encode_v(I, rows, cols, wpr, W, T, R, enumL, besti, bestj, bestd, weights, modes, stats,
+                             stream_match, stream_nomatch, cap_bytes, 0, NULL);
+}
+
+/* invert = 0: compress7_test.cpp:117-275; invert = 1: compress8_test.cpp:126-272, which differs in
+ *  - bestinv = (P.weight() - M) < P.weight() (:136; idx_t arithmetic: true iff the tile is all 1s);
+ *  - perfect_match = P.weight() <= T || P.weight() >= M - T before any search (:137);
+ *  - per window d = dist(P, P2) replaced by M - d when (M - d) < d, that window's inv = true (:156-161;
+ *    the driver leaves inv uninitialised otherwise: defined here as false) and bestinv = inv with
+ *    every improvement (:163);
+ *  - P.flip() when bestinv (:207-210) before P3 and both weights are formed;
+ *  - the match lengths carry one more bit (3 + idx_len + enumL, :250-251).
+ * inverted (nullable): bestinv per tile. */
+int bo_match_encode_v(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T, unsigned R,
+                      const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
+                      uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
+                      uint8_t* stream_nomatch, size_t cap_bytes, int invert, uint8_t* inverted) {
     if (W == 0 || W > 64 || rows % W || cols % W) return -1;
     const size_t Ny = rows / W, Nx = cols / W, M = (size_t)W * W;
     const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
@@ -633,7 +662,12 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
             const int i0 = (int)(i * W), j0 = (int)(j * W);
             bo_get_submatrix(I, rows, cols, wpr, (size_t)i0, (size_t)i0 + W, (size_t)j0, (size_t)j0 + W, P, 1);
             size_t bi = 0, bj = 0, bd = M + 1;
-            int perfect = 0;
+            int perfect = 0, bestinv = 0;
+            if (invert) {                                                /* compress8_test.cpp:136-137 */
+                const uint64_t w0 = bo_weight(P, W, W, 1);
+                bestinv = (uint64_t)(w0 - M) < w0;
+                perfect = w0 <= T || w0 >= (uint64_t)M - (uint64_t)T;
+            }
             const int mini = i0 > iR ? i0 - iR : 0;
             const int minj = j0 > iR ? j0 - iR : 0;
             const int maxj = (j0 + iR > icols - iW) ? icols - iW : j0 + iR;
@@ -647,10 +681,14 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
                         bo_get_submatrix(I, rows, cols, wpr, (size_t)i2, (size_t)i2 + W, (size_t)j2, (size_t)j2 + W, P2, 1);
                         size_t d = 0;
                         for (unsigned r = 0; r < W; r++) d += (size_t)__builtin_popcountll((P[r] ^ P2[r]) & topW);
-                        if (d < bd) { bd = d; bi = (size_t)i2; bj = (size_t)j2; }
+                        int inv = 0;
+                        if (invert && M - d < d) { inv = 1; d = M - d; }    /* compress8_test.cpp:156-161 */
+                        if (d < bd) { bd = d; bi = (size_t)i2; bj = (size_t)j2; bestinv = inv; }
                         if (bd <= T) { perfect = 1; break; }
                     }
             }
+            if (bestinv)                                                 /* compress8_test.cpp:207-210 */
+                for (unsigned r = 0; r < W; r++) P[r] = ~P[r];
             if (bd <= M) {                                               /* :185-190 */
                 bo_get_submatrix(I, rows, cols, wpr, bi, bi + W, bj, bj + W, P2, 1);
                 for (unsigned r = 0; r < W; r++) P3[r] = (P[r] ^ P2[r]) & topW;
@@ -666,9 +704,9 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
             if (swin >= 1) idx_len = swin == 1 ? 0 : 64 - (uint64_t)__builtin_clzll((uint64_t)(swin - 1));
             const uint64_t nn_len = (uint64_t)(2.0 + enumL[w_nn]), np_len = (uint64_t)(2.0 + enumL[w_np]);
             uint64_t mn_len = ~0ull, mp_len = ~0ull;
-            if (swin >= 1) {
-                mn_len = (uint64_t)((double)(2 + idx_len) + enumL[w_mn]);
-                mp_len = (uint64_t)((double)(2 + idx_len) + enumL[w_mp]);
+            if (swin >= 1) {  /* compress8_test.cpp:250-251: one more bit (invert / not) */
+                mn_len = (uint64_t)((double)(2 + (invert ? 1 : 0) + idx_len) + enumL[w_mn]);
+                mp_len = (uint64_t)((double)(2 + (invert ? 1 : 0) + idx_len) + enumL[w_mp]);
             }
             const int mpred = mn_len > mp_len, npred = nn_len > np_len;  /* :232, :243 */
             const uint64_t match_len = mpred ? mp_len : mn_len, match_w = mpred ? w_mp : w_mn;
@@ -690,6 +728,7 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
             if (bestd) bestd[li] = (uint32_t)bd;
             if (weights) weights[li] = (uint32_t)w;
             if (modes) modes[li] = take ? (mpred ? 'X' : 'x') : (npred ? 'O' : 'o');
+            if (inverted) inverted[li] = (uint8_t)bestinv;
         }
     if (stats) {
         stats[0] = matches;

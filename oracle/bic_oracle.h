@@ -54,6 +54,10 @@ void bo_set(uint64_t* P, size_t wpr, size_t i, size_t j, int v);
  * gray is 8-bit (bytes_per_px = 1) or 16-bit host-order (bytes_per_px = 2). */
 void bo_bitplanes(const void* gray, int bytes_per_px, size_t rows, size_t cols,
                   int nplanes, uint64_t* planes, size_t wpr);
+/* plane2pgm_tool.cpp:26-41 -- gray[li] |= 1 << b for every set bit of plane b (samples as the
+ * tool's pixel_t, 32-bit; bits no plane covers are 0). */
+void bo_planes_to_gray(const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
+                       uint32_t* gray);
 /* number of planes bitplane_tool.cpp:24 extracts: #{bi : 2^bi < maxval} */
 int bo_num_planes(int maxval);
 /* pred.cpp:3-15, bit-serial. R(0,0) and the trailing pad bits are left 0
@@ -176,6 +180,12 @@ int bo_match_encode(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned 
                     const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
                     uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
                     uint8_t* stream_nomatch, size_t cap_bytes);
+/* the same loop, invert = 1: compress8_test.cpp's variant (patch inversion, see bic_oracle.c);
+ * inverted (nullable): per tile, whether the patch was flipped. */
+int bo_match_encode_v(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T, unsigned R,
+                      const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
+                      uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
+                      uint8_t* stream_nomatch, size_t cap_bytes, int invert, uint8_t* inverted);
 
 /* ---- binary_matrix algebra over GF(2) ----------------- */
 /* Reference layout only: wpr = ceil(cols/64) for every operand (the loops index words flat).

@@ -473,6 +473,118 @@ extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr
   return 0;
 }
 
+// compress8_test.cpp:126-272's tile loop over the reference's own objects (get_submatrix, dist,
+// flip, add, med, weight, set_submatrix, GolombCoder); enumL from the caller (GSL is absent). As
+// written except that a window's `inv` (left uninitialised by the driver when the window is not
+// inverted, :157) is false. inverted (nullable): bestinv per tile.
+extern "C" int ref_match_loop8(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
+                               unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                               uint32_t* bestd, uint32_t* weights, char* modes, uint8_t* inverted,
+                               uint64_t* stats) {
+  binary_matrix I = from_words(Iw, rows, cols, wpr);
+  const int iW = (int)W, iR = (int)R;
+  const idx_t M = (idx_t)W * W;
+  const idx_t Tt = T;
+  const idx_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+  binary_matrix P, P2;
+  binary_matrix P3(W, W);
+  GolombCoder golomb_match, golomb_nomatch;
+  uint64_t L = 0, matches = 0;
+  idx_t li = 0;
+  for (idx_t i = 0; i < Ny; i++)
+    for (idx_t j = 0; j < Nx; j++, li++) {
+      const int i0 = i * W, j0 = j * W;
+      int i2;
+      P = I.get_submatrix(i0, i0 + W, j0, j0 + W);
+      idx_t bi = 0, bj = 0, bd = M + 1;
+      bool bestinv = (P.weight() - M) < (P.weight());
+      bool perfect = (P.weight() <= Tt) || (P.weight() >= (M - Tt));
+      const int mini = i0 > iR ? (i0 - iR) : 0;
+      const int minj = (j0 > iR) ? (j0 - iR) : 0;
+      const int maxj = ((j0 + iR) > (int(cols) - iW)) ? (cols - W) : (j0 + iR);
+      const int mini2 = (i0 > iW) ? (i0 - iW) : 0;
+      const int maxj2 = (j0 > iW) ? (j0 - iW) : 0;
+      const int swin = (i0 - mini2) * (maxj2 - minj) + (mini2 - mini) * (maxj - minj);
+      for (int loop = 0; loop < 2; ++loop) {
+        const int ihi = loop ? i0 - iW : i0, ilo = loop ? mini : mini2, jhi = loop ? maxj : maxj2;
+        for (i2 = ihi; (i2 >= ilo) && !perfect; i2--)
+          for (int j2 = jhi; j2 >= minj; j2--) {
+            P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+            idx_t d = dist(P, P2);
+            bool inv = false;
+            if ((M - d) < d) {
+              inv = true;
+              d = M - d;
+            }
+            if (d < bd) {
+              bestinv = inv;
+              bd = d;
+              bi = i2;
+              bj = j2;
+              if (bd <= Tt) {
+                perfect = true;
+                break;
+              }
+            }
+          }
+      }
+      if (bestinv) P.flip();
+      if (bd <= M) {
+        P2 = I.get_submatrix(bi, bi + W, bj, bj + W);
+        add(P, P2, P3);
+      } else {
+        P3 = P.get_copy();
+      }
+      const idx_t w_mn = P3.weight(), w_nn = P.weight();
+      binary_matrix dP(W, W), dP3(W, W);
+      dP.clear();
+      dP3.clear();
+      med(P, dP);
+      med(P3, dP3);
+      const idx_t w_mp = dP3.weight(), w_np = dP.weight();
+      const bool ok = swin > 0;
+      const idx_t idx_len = ok ? (idx_t)ceil(log2(swin)) : 0;
+      const idx_t nn_len = 2 + enuml[w_nn], np_len = 2 + enuml[w_np];
+      const idx_t mn_len = ok ? (idx_t)(3 + idx_len + enuml[w_mn]) : ~(idx_t)0;
+      const idx_t mp_len = ok ? (idx_t)(3 + idx_len + enuml[w_mp]) : ~(idx_t)0;
+      const bool mpred = mn_len > mp_len, npred = nn_len > np_len;
+      const idx_t match_len = mpred ? mp_len : mn_len, nomatch_len = npred ? np_len : nn_len;
+      const bool take = nomatch_len > match_len;
+      idx_t w;
+      if (take) {
+        w = mpred ? w_mp : w_mn;
+        golomb_match.codeSample(w);
+        matches++;
+        L += match_len;
+        I.set_submatrix(i0, j0, mpred ? dP3 : P3);
+      } else {
+        w = npred ? w_np : w_nn;
+        golomb_nomatch.codeSample(w);
+        L += nomatch_len;
+        I.set_submatrix(i0, j0, npred ? dP : P);
+      }
+      if (besti) besti[li] = (uint32_t)bi;
+      if (bestj) bestj[li] = (uint32_t)bj;
+      if (bestd) bestd[li] = (uint32_t)bd;
+      if (weights) weights[li] = (uint32_t)w;
+      if (modes) modes[li] = take ? (mpred ? 'X' : 'x') : (npred ? 'O' : 'o');
+      if (inverted) inverted[li] = bestinv ? 1 : 0;
+      dP.destroy();
+      dP3.destroy();
+    }
+  to_words(I, Iw, wpr);
+  if (stats) {
+    stats[0] = matches;
+    stats[1] = (uint64_t)golomb_match.bitcount;
+    stats[2] = (uint64_t)golomb_nomatch.bitcount;
+    stats[3] = L;
+  }
+  P.destroy();
+  P2.destroy();
+  I.destroy();
+  return 0;
+}
+
 // binary_matrix algebra on the reference's own objects (binmat.cpp:199-214, 516-616): C starts as
 // Cin (mul_ABt keeps bits), words in the reference layout (wpr = ceil(cols/64), padding bits 0).
 extern "C" int ref_gf2_mul(int op, const uint64_t* A, size_t a_rows, size_t a_cols, const uint64_t* B,

@@ -35,6 +35,7 @@ class Oracle:
         _sig(L, "bo_gen_plane", None, [C.c_uint64, C.c_double, sz, sz, sz, u64p])
         _sig(L, "bo_gen_bytes", None, [C.c_uint64, sz, u8p])
         _sig(L, "bo_bitplanes", None, [C.c_void_p, C.c_int, sz, sz, C.c_int, u64p, sz])
+        _sig(L, "bo_planes_to_gray", None, [u64p, C.c_int, sz, sz, sz, u32p])
         _sig(L, "bo_num_planes", C.c_int, [C.c_int])
         _sig(L, "bo_med", None, [u64p, u64p, sz, sz, sz])
         _sig(L, "bo_weight", C.c_uint64, [u64p, sz, sz, sz])
@@ -60,6 +61,9 @@ class Oracle:
         _sig(L, "bo_match_encode", C.c_int,
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p,
               u8p, u8p, sz])
+        _sig(L, "bo_match_encode_v", C.c_int,
+             [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p,
+              u8p, u8p, sz, C.c_int, u8p])
 
     # -- inputs ----------------------------------------------------------
     def gen_plane(self, seed, p, rows, cols, wpr=None):
@@ -80,6 +84,14 @@ class Oracle:
         gray = np.ascontiguousarray(gray)
         out = np.zeros((nplanes, rows, wpr), np.uint64)
         self.lib.bo_bitplanes(gray.ctypes.data, gray.dtype.itemsize, rows, cols, nplanes, ptr(out, u64p), wpr)
+        return out
+
+    def planes_to_gray(self, planes, cols):
+        """plane2pgm_tool.cpp:26-41: planes [n, rows, wpr] -> uint32 samples [rows, cols]"""
+        planes = np.ascontiguousarray(planes, np.uint64)
+        n, rows, wpr = planes.shape
+        out = np.zeros((rows, cols), np.uint32)
+        self.lib.bo_planes_to_gray(ptr(planes, u64p), n, rows, cols, wpr, ptr(out, u32p))
         return out
 
     def med(self, P, cols):
@@ -271,8 +283,9 @@ class Oracle:
         M = W * W
         return np.array([self.enumL(M, w) for w in range(M + 1)], np.float64)
 
-    def match_encode(self, I, cols, W, T=0, R=128, enuml=None, want_stream=True):
-        """compress7_test.cpp:117-275 with search window R, threshold T (bo_match_encode)."""
+    def match_encode(self, I, cols, W, T=0, R=128, enuml=None, want_stream=True, invert=False):
+        """compress7_test.cpp:117-275 with search window R, threshold T (bo_match_encode); invert:
+        compress8_test.cpp's patch-inversion variant (bo_match_encode_v), with `inverted` per tile."""
         I = np.array(I, copy=True)
         rows, wpr = I.shape
         enuml = self.enum_table(W) if enuml is None else np.ascontiguousarray(enuml, np.float64)
@@ -283,12 +296,15 @@ class Oracle:
         cap = n * 8 + 4096
         bm = np.zeros(cap, np.uint8) if want_stream else None
         bn = np.zeros(cap, np.uint8) if want_stream else None
-        rc = self.lib.bo_match_encode(ptr(I, u64p), rows, cols, wpr, W, T, R, ptr(enuml, dp), ptr(bi, u32p),
-                                      ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(stats, u64p),
-                                      ptr(bm, u8p), ptr(bn, u8p), cap if want_stream else 0)
+        inv = np.zeros(n, np.uint8)
+        rc = self.lib.bo_match_encode_v(ptr(I, u64p), rows, cols, wpr, W, T, R, ptr(enuml, dp), ptr(bi, u32p),
+                                        ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(stats, u64p),
+                                        ptr(bm, u8p), ptr(bn, u8p), cap if want_stream else 0, int(invert),
+                                        ptr(inv, u8p))
         assert rc == 0, rc
         out = dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes.raw[:n].decode(), residual=I,
-                   matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]))
+                   matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]),
+                   inverted=inv)
         if want_stream:
             out["stream_match"] = bm[: ((out["bits_match"] + 63) // 64) * 8].copy()
             out["stream_nomatch"] = bn[: ((out["bits_nomatch"] + 63) // 64) * 8].copy()
@@ -315,10 +331,20 @@ class Ref:
         _sig(L, "ref_patch_search", C.c_int, [u64p, sz, sz, sz, C.c_uint, u32p, u32p, u32p])
         _sig(L, "ref_match_loop", C.c_int,
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p])
+        _sig(L, "ref_match_loop8", C.c_int,
+             [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u8p, u64p])
         _sig(L, "ref_gf2_mul", C.c_int, [C.c_int, u64p, sz, sz, u64p, sz, sz, u64p, sz, sz])
         _sig(L, "ref_gf2_transpose", C.c_int, [u64p, sz, sz, u64p])
         _sig(L, "ref_baseline_planes", C.c_double,
              [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, C.c_int, u64p, C.POINTER(C.c_int)])
+
+    def planes_to_gray(self, planes, cols):
+        """plane2pgm_tool.cpp:26-41: planes [n, rows, wpr] -> uint32 samples [rows, cols]"""
+        planes = np.ascontiguousarray(planes, np.uint64)
+        n, rows, wpr = planes.shape
+        out = np.zeros((rows, cols), np.uint32)
+        self.lib.bo_planes_to_gray(ptr(planes, u64p), n, rows, cols, wpr, ptr(out, u32p))
+        return out
 
     def med(self, P, cols):
         P = np.ascontiguousarray(P)
@@ -425,6 +451,22 @@ class Ref:
         return dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes.raw[:n].decode(), residual=I,
                     matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]))
 
+    def match_loop8(self, I, cols, W, T, R, enuml):
+        """compress8_test.cpp:126-272 over the reference's objects (ref_match_loop8)"""
+        I = np.array(I, copy=True)
+        rows, wpr = I.shape
+        enuml = np.ascontiguousarray(enuml, np.float64)
+        n = (rows // W) * (cols // W)
+        bi, bj, bd, wt = (np.zeros(n, np.uint32) for _ in range(4))
+        inv = np.zeros(n, np.uint8)
+        modes = C.create_string_buffer(n + 1)
+        stats = np.zeros(4, np.uint64)
+        self.lib.ref_match_loop8(ptr(I, u64p), rows, cols, wpr, W, T, R, ptr(enuml, dp), ptr(bi, u32p),
+                                 ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(inv, u8p), ptr(stats, u64p))
+        return dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes.raw[:n].decode(), residual=I,
+                    matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]),
+                    inverted=inv)
+
     def baseline(self, planes, rows, cols, predict=1, do_eg=1, threads=0):
         planes = np.ascontiguousarray(planes)
         nplanes = planes.shape[0]
@@ -474,6 +516,23 @@ def periodic_plane(seed, rows, cols, ph, pw, p=0.5, flip=0.0):
     bits = np.tile(blk, (rows // ph + 1, cols // pw + 1))[:rows, :cols]
     if flip:
         bits ^= rng.random((rows, cols)) < flip
+    return pack_rows(bits)
+
+
+def inverted_plane(seed, rows, cols, ph, pw, p=0.5, flip=0.0, ones_tiles=0):
+    """periodic_plane with every other period block (checkerboard) complemented, plus `ones_tiles`
+    all-1 blocks of ph x pw: inputs on which compress8's search prefers inverted windows and meets
+    tiles whose weight is M (its initial bestinv)."""
+    rng = np.random.default_rng(seed)
+    blk = rng.random((ph, pw)) < p
+    bits = np.tile(blk, (rows // ph + 1, cols // pw + 1))[:rows, :cols]
+    ii, jj = np.meshgrid(np.arange(rows) // ph, np.arange(cols) // pw, indexing="ij")
+    bits ^= ((ii + jj) & 1).astype(bool)
+    if flip:
+        bits ^= rng.random((rows, cols)) < flip
+    for _ in range(ones_tiles):
+        i0, j0 = int(rng.integers(0, rows // ph)) * ph, int(rng.integers(0, cols // pw)) * pw
+        bits[i0:i0 + ph, j0:j0 + pw] = True
     return pack_rows(bits)
 
 

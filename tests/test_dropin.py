@@ -137,3 +137,27 @@ def test_bitplane_and_plane2pgm(drivers, tmp_path):
                     f.write(b)
         res2 = run_both(drivers, str(tmp_path), "plane2pgm_tool", ["data/plane_%02d.pbm", "rec.pgm"], setup)
         assert_same(res2, f"plane2pgm_tool/{key}")
+        # The tool reads plane 0's header only (plane2pgm_tool.cpp:24) and planes 1.. with
+        # read_pbm_data from the start of their files (:47), so on real PBM files it misreads them (the
+        # quirk both builds reproduce above). Given plane 0 as a PBM and the other planes as bare
+        # rasters, its loop (:33-41) reassembles the image: that output pins the oracle's
+        # restatement bo_planes_to_gray, which the device's bic_planes_to_gray is checked against.
+        from oracle_lib import Oracle
+        from pnm_io import plane_to_p4_rows, read_pbm_bytes
+        names = sorted(planes)
+        rows_, cols_, _ = read_pbm_bytes(planes[names[0]])
+        P = np.stack([read_pbm_bytes(planes[n])[2] for n in names])
+
+        def bare(d, names=names, P=P):
+            for k, n in enumerate(names):
+                with open(os.path.join(d, "data", n), "wb") as f:
+                    f.write(planes[n] if k == 0 else plane_to_p4_rows(P[k], cols_).tobytes())
+        res3 = run_both(drivers, str(tmp_path), "plane2pgm_tool", ["data/plane_%02d.pbm", "rec.pgm"], bare)
+        assert_same(res3, f"plane2pgm_tool/bare/{key}")
+        rec = res3["drv_ref"][2]["rec.pgm"]
+        head = rec.split(b"\n", 3)  # write_ppm_header: "P5\n<cols> <rows>\n<maxval>\n" (pnm.cpp)
+        assert head[0] == b"P5" and head[1] == f"{cols_} {rows_}".encode(), head[:3]
+        mv = int(head[2])
+        exp = np.frombuffer(head[3], ">u2" if mv >= 256 else np.uint8).reshape(rows_, cols_)
+        got = Oracle().planes_to_gray(P, cols_)
+        assert np.array_equal(got, exp.astype(np.uint32)), key

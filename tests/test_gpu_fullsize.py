@@ -147,7 +147,8 @@ def test_c1_match_loop_full(ctx, oracle):
 
 def test_c3_full_round_trip(ctx, oracle):
     """§8 f1 at configs[2]'s size: the 8 planes of a 16384^2 gray image -> Golomb and EG streams
-    (packed, with the row index) -> decoded on the device (med inverted there) == the planes"""
+    (packed, with the row index) -> decoded on the device (med inverted there) == the planes ->
+    reassembled on the device (bic_planes_to_gray) == the gray image"""
     rows = cols = 16384
     img = _gray(oracle, 0x5EED0002, rows, cols, "smooth")
     g = ctx.torch.from_numpy(img).to(ctx.dev)
@@ -162,6 +163,10 @@ def test_c3_full_round_trip(ctx, oracle):
     assert ctx.torch.equal(back, planes)
     exp_planes = oracle.bitplanes_par(img, 8)
     assert np.array_equal(as_u64(planes), exp_planes)
+    # ... and the last leg (plane2pgm_tool.cpp:33-52 on the device): the decoded planes -> the gray image
+    gray_back = ctx.planes_to_gray(back, cols)
+    ctx.sync()
+    assert ctx.torch.equal(gray_back, g)
 
 
 @pytest.mark.parametrize("p", [0.5, 0.05])

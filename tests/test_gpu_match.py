@@ -45,17 +45,19 @@ def make_input(oracle, seed, rows, cols, spec):
     return oracle.gen_plane(seed, spec[1], rows, cols)
 
 
-def check(ctx, oracle, I, cols, W, T, R, parts=0):
+def check(ctx, oracle, I, cols, W, T, R, parts=0, invert=False):
     e = oracle.enum_table(W)
-    exp = oracle.match_encode(I, cols, W, T, R, e)
+    exp = oracle.match_encode(I, cols, W, T, R, e, invert=invert)
     ctx.set_match_parts(parts)
     try:
-        got = ctx.match_encode(ctx.to_dev(I), cols, W, T, R, e)
+        got = ctx.match_encode(ctx.to_dev(I), cols, W, T, R, e, invert=invert)
         ctx.sync()
     finally:
         ctx.set_match_parts(0)
     for k in ("besti", "bestj", "bestd", "weights"):
         assert np.array_equal(got[k].cpu().numpy().view(np.uint32), exp[k]), k
+    if invert:
+        assert np.array_equal(got["inverted"].cpu().numpy(), exp["inverted"])
     assert got["modes"].cpu().numpy().tobytes().decode() == exp["modes"]
     assert np.array_equal(as_u64(got["resid"]), exp["residual"])
     st = as_u64(got["stats"])
@@ -73,6 +75,38 @@ def test_match_encode(ctx, oracle, case, sched):
     exp = check(ctx, oracle, I, cols, W, T, R, sched)
     if spec[0] in ("periodic", "text"):
         assert exp["matches"] > 0
+
+
+INV_CASES = [  # W, rows, cols, T, R, input (compress8_test.cpp: patch inversion)
+    (8, 64, 128, 0, 32, ("inverted", 8, 8, 0.5, 0.0, 3)),
+    (8, 64, 96, 2, 24, ("inverted", 8, 24, 0.5, 0.01, 2)),
+    (5, 40, 60, 0, 12, ("inverted", 5, 10, 0.4, 0.0, 4)),
+    (4, 32, 64, 1, 4, ("random", 0.9)),
+    (4, 32, 64, 0, 2, ("random", 0.3)),
+    (16, 64, 128, 3, 40, ("inverted", 16, 32, 0.3, 0.002, 1)),
+    (6, 36, 72, 40, 12, ("random", 0.5)),
+    (16, 256, 256, 2, 128, ("inverted", 16, 48, 0.5, 0.001, 6)),  # compress8's defaults (W 16, R 128)
+    (32, 128, 256, 0, 80, ("inverted", 32, 64, 0.5, 0.003, 2)),
+    (12, 96, 240, 0, 60, ("inverted", 12, 24, 0.2, 0.0, 3)),
+    (16, 48, 6400, 0, 128, ("random", 0.98)),                      # too wide for the row schedule
+    (16, 160, 320, 1, 96, ("text",)),
+]
+
+
+@pytest.mark.parametrize("sched", [AUTO, ROW, TEAM3, TILE])
+@pytest.mark.parametrize("case", range(len(INV_CASES)))
+def test_match_encode_inverted(ctx, oracle, case, sched):
+    """bic_match_encode_inv (compress8_test.cpp's loop) against the oracle's bo_match_encode_v, itself
+    pinned to the driver's loop over the reference objects (test_ref_crosscheck.py), every schedule"""
+    from oracle_lib import inverted_plane
+    W, rows, cols, T, R, spec = INV_CASES[case]
+    if spec[0] == "inverted":
+        I = inverted_plane(6000 + case, rows, cols, *spec[1:])
+    else:
+        I = make_input(oracle, 6000 + case, rows, cols, spec)
+    exp = check(ctx, oracle, I, cols, W, T, R, sched, invert=True)
+    if spec[0] == "inverted":
+        assert exp["inverted"].any() and exp["matches"] > 0
 
 
 @pytest.mark.parametrize("parts", [1, 3, 17])

@@ -85,3 +85,42 @@ def test_p5_file_to_streams(ctx, oracle, tmp_path, rows, cols, maxval, comment):
     for k in range(nplanes):
         eb, est, _ = oracle.encode_plane(exp[k], cols, 1, 0)
         assert int(as_u64(bits)[k]) == eb and stream_bytes(out[k], eb) == est.tobytes(), k
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (3, 70), (17, 1000), (5, 4096), (3, 16384), (2, 4099)])
+@pytest.mark.parametrize("bps,nplanes,plane0", [(1, 8, 0), (1, 3, 2), (2, 16, 0), (2, 10, 0), (2, 5, 9)])
+@pytest.mark.parametrize("off", [0, 3])
+def test_planes_to_gray(ctx, oracle, rows, cols, bps, nplanes, plane0, off):
+    """bic_planes_to_gray (plane2pgm_tool.cpp:33-52) == the oracle's reassembly (bo_planes_to_gray, pinned to
+    the reference tool by test_dropin), as 8-bit samples or big-endian 16-bit ones, at any byte offset"""
+    rng = np.random.default_rng(rows * cols + 7 * nplanes + off)
+    P = np.stack([oracle.gen_plane(int(rng.integers(1 << 30)), (0.5, 0.1, 0.9)[k % 3], rows, cols)
+                  for k in range(nplanes)])
+    exp = oracle.planes_to_gray(P, cols).astype(np.uint64) << np.uint64(plane0)
+    pitch = cols * bps + 5
+    buf = ctx.torch.full((off + rows * pitch,), 0xA5, dtype=ctx.torch.uint8, device=ctx.dev)
+    ctx.planes_to_gray(ctx.to_dev(P), cols, plane0=plane0, sample_bytes=bps, out=buf[off:], pitch=pitch)
+    ctx.sync()
+    got = buf[off:].cpu().numpy().reshape(rows, pitch)
+    samples = got[:, :cols * bps].copy().view(">u2" if bps == 2 else np.uint8).astype(np.uint64)
+    assert np.array_equal(samples, exp)
+    assert (got[:, cols * bps:] == 0xA5).all()  # nothing past a row's samples is written
+    assert (buf[:off].cpu().numpy() == 0xA5).all()
+
+
+def test_planes_to_gray_rejects(ctx):
+    P = ctx.empty_i64(9, 2, 1)
+    with pytest.raises(pybic.BicError):
+        ctx.planes_to_gray(P, 64)  # 9 planes do not fit 8-bit samples
+    with pytest.raises(pybic.BicError):
+        ctx.planes_to_gray(P[:4], 64, plane0=6)
+
+
+def test_gray_round_trip(ctx, oracle):
+    """gray -> bitplanes -> bic_planes_to_gray == gray (8-bit), on the device"""
+    rows, cols = 37, 5000
+    g = oracle.gen_bytes(0x5EED0077, rows * cols).reshape(rows, cols)
+    planes = ctx.bitplanes_u8(ctx.torch.from_numpy(g).to(ctx.dev), nplanes=8)
+    back = ctx.planes_to_gray(planes, cols)
+    ctx.sync()
+    assert np.array_equal(back.cpu().numpy(), g)

@@ -86,6 +86,47 @@ def test_match_encode(oracle, ref, case):
         assert a["matches"] > 0  # the inputs exercise the match branch
 
 
+MATCH8_CASES = [  # W, rows, cols, T, R, input
+    (8, 64, 128, 0, 32, ("inverted", 8, 8, 0.5, 0.0, 3)),
+    (8, 64, 96, 2, 24, ("inverted", 8, 24, 0.5, 0.01, 2)),
+    (5, 40, 60, 0, 12, ("inverted", 5, 10, 0.4, 0.0, 4)),
+    (4, 32, 64, 1, 4, ("random", 0.9)),
+    (4, 32, 64, 0, 2, ("random", 0.3)),   # R < W: empty regions
+    (16, 64, 128, 3, 40, ("inverted", 16, 32, 0.3, 0.002, 1)),
+    (6, 36, 72, 40, 12, ("random", 0.5)),  # T large: initial perfect matches (w <= T or w >= M - T)
+    (8, 48, 64, 0, 128, ("random", 0.02)),
+    (8, 64, 64, 5, 64, ("ones", 0.0)),     # all-1 tiles: bestinv from the tile weight alone
+]
+
+
+def match8_input(oracle, seed, rows, cols, spec):
+    from oracle_lib import inverted_plane, pack_rows
+    if spec[0] == "inverted":
+        return inverted_plane(seed, rows, cols, *spec[1:])
+    if spec[0] == "ones":
+        bits = np.ones((rows, cols), bool)
+        bits[rows // 2:, :] = np.random.default_rng(seed).random((rows - rows // 2, cols)) < 0.5
+        return pack_rows(bits)
+    return oracle.gen_plane(seed, spec[1], rows, cols)
+
+
+@pytest.mark.parametrize("case", range(len(MATCH8_CASES)))
+def test_match_encode_inverted(oracle, ref, case):
+    """compress8_test.cpp (patch inversion): the oracle's bo_match_encode_v == the driver's loop over
+    the reference's own get_submatrix / dist / flip / add / med / set_submatrix / GolombCoder"""
+    W, rows, cols, T, R, spec = MATCH8_CASES[case]
+    I = match8_input(oracle, 5000 + case, rows, cols, spec)
+    e = oracle.enum_table(W)
+    a = oracle.match_encode(I, cols, W, T, R, e, want_stream=False, invert=True)
+    b = ref.match_loop8(I, cols, W, T, R, e)
+    for k in ("besti", "bestj", "bestd", "weights", "residual", "inverted"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in ("modes", "matches", "bits_match", "bits_nomatch", "L"):
+        assert a[k] == b[k], k
+    if spec[0] in ("inverted", "ones"):
+        assert a["inverted"].any()  # the inputs exercise the inversion
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_gf2_algebra(oracle, ref, seed):
     """bo_gf2_mul / bo_gf2_transpose vs the reference's mul() and transpose_to on fresh shapes
