@@ -1,7 +1,7 @@
 """Timing of the §8 rows beside the encoder (measurement for DESIGN.md §3, not a test): at configs[2]'s
 size (8 planes of 16384^2, Bernoulli(0.5) pixels, device-resident) -- the packed encoder with its row
 index, the device decoders (Golomb from the index, EG, both through unmed), the adaptive EG coder
-(encode), bic_row_index from planes, PBM unpack / pack of one plane, P5 raster -> planes. HIP events
+(encode), bic_row_index from planes, PBM unpack / pack of one plane, P5 raster -> planes, planes -> gray. HIP events
 around R launches of each call after a warm-up; every decode is checked against the planes.
 Usage: python tools/time_aux.py [--reps R] > gpurun_out/time_aux.json"""
 import argparse
@@ -99,6 +99,10 @@ def main():
           rows * cols + plane_bytes)
     timed("bitplanes_u8", lambda: ctx.bitplanes_u8(gray[:rows * cols].view(rows, cols), out=pl8),
           rows * cols + plane_bytes)
+    g8 = torch.empty(rows, cols, dtype=torch.uint8, device=ctx.dev)
+    timed("planes_to_gray", lambda: ctx.planes_to_gray(pl8, cols, out=g8), rows * cols + plane_bytes)
+    ctx.sync()
+    out["planes_to_gray_ok"] = bool(torch.equal(g8, gray[:rows * cols].view(rows, cols)))
     ctx.sync()
     print(json.dumps(out))
 
