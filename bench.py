@@ -51,6 +51,9 @@ def parse():
                          "(strong scaling; the gather is in the timed step)")
     ap.add_argument("--separate", action="store_true",
                     help="c3: bic_bitplanes_u8 then bic_encode_planes2 instead of the one-call bic_encode_gray")
+    ap.add_argument("--store-planes", action="store_true",
+                    help="c3: bic_encode_gray also returns the 8 bitplanes (planes != NULL; +256 MiB written per "
+                         "image); default: planes NULL, the count pass keeps the residual planes for the encoder")
     ap.add_argument("--plane-count", type=int, default=8,
                     help="c3 --shard planes: encode planes 0..P-1 of the image (split over the ranks); P = 1 or 2 at "
                          "N = 1 measures the per-rank step of a plane-sharded 8- or 4-GPU run")
@@ -211,7 +214,9 @@ class C3:
         self.gray = [t.randint(0, 256, (self.rows, self.cols), dtype=t.uint8, device=ctx.dev, generator=g)
                      for _ in range(2)]
         self.wpr = (self.cols + 63) // 64
-        self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr)
+        self.separate = args.separate
+        self.store_planes = args.store_planes or args.separate
+        self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr) if self.store_planes else None
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
         self.out_g = ctx.empty_i64(self.nplanes, self.slot_g)
@@ -220,10 +225,10 @@ class C3:
         self.bits_e = ctx.empty_i64(self.nplanes)
         ctx.reserve(self.nplanes, self.rows, self.cols)
         self.k = 0
-        self.separate = args.separate
         self.pixels = self.rows * self.cols * self.nplanes
         self.workload = (f"c3: {self.rows}x{self.cols} 8-bit gray -> 8 bitplanes -> med -> per-row runs "
-                         f"-> Golomb + EG streams per plane")
+                         f"-> Golomb + EG streams per plane" +
+                         ("" if self.store_planes else " (bitplanes formed in registers, not returned: planes NULL)"))
 
     def step(self):
         c = self.ctx
@@ -233,7 +238,8 @@ class C3:
                              outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
         else:  # one call: bitplanes + both streams (bic_encode_gray)
             c.encode_gray(self.gray[self.k & 1], nplanes=8, planes=self.planes, slots=(self.slot_g, self.slot_e),
-                          outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
+                          outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e),
+                          store_planes=self.store_planes)
         self.k += 1
 
     def out_bytes(self):
@@ -250,6 +256,8 @@ class C3:
                 "golomb_emit": plane_b + g, "eg_emit": plane_b + e, "encode_rows_golomb_eg": plane_b + g + e}
 
     def host_planes(self, rows):
+        if self.planes is None:  # the last step's image's planes (device bitplane kernel), for the CPU leg
+            return self.pybic.as_u64(self.ctx.bitplanes_u8(self.gray[(self.k - 1) & 1][:rows], nplanes=self.nplanes))
         return self.pybic.as_u64(self.planes[:, :rows])
 
     def predictor_pass(self, reps):
@@ -260,7 +268,8 @@ class C3:
         alternate, so the 256 MB Infinity Cache cannot hold the input of the next launch
         (SURVEY.md §8 d)."""
         alt = self.ctx.bitplanes_u8(self.gray[self.k & 1], nplanes=8)  # the other image's planes
-        bufs = [self.planes, alt]
+        cur = self.planes if self.planes is not None else self.ctx.bitplanes_u8(self.gray[(self.k - 1) & 1], nplanes=8)
+        bufs = [cur, alt]
         self.ctx.sync()
         self.ctx.prof_enable(True)
         for i in range(reps):
@@ -268,7 +277,7 @@ class C3:
         self.ctx.sync()
         prof = self.ctx.prof_collect()
         self.ctx.prof_enable(False)
-        del alt, bufs
+        del alt, cur, bufs
         n, ms = prof["med_count"]
         avg_s = ms / 1e3 / n
         byts = self.nplanes * self.rows * self.wpr * 8
@@ -278,11 +287,12 @@ class C3:
                 "input": "two plane buffers (2 x 256 MiB) alternated"}
 
     def check(self, oracle):
-        """every plane of the last step: the planes == the oracle's bitplanes of the gray image,
-        and each plane's Golomb and EG streams == the oracle's (host threads)"""
-        P = self.pybic.as_u64(self.planes)
+        """every plane of the last step: the planes (when returned) == the oracle's bitplanes of the
+        gray image, and each plane's Golomb and EG streams == the oracle's streams of those bitplanes
+        (host threads)"""
         gray = self.gray[(self.k - 1) & 1].cpu().numpy()
-        if not np.array_equal(P, oracle.bitplanes_par(gray, self.nplanes)):
+        P = oracle.bitplanes_par(gray, self.nplanes)
+        if self.planes is not None and not np.array_equal(self.pybic.as_u64(self.planes), P):
             return False
         exp = oracle.encode_planes_par(P, self.cols, 1)
         ok = True
@@ -316,7 +326,8 @@ class C3Planes(C3):
         self.gray = [t.randint(0, 256, (self.rows, self.cols), dtype=t.uint8, device=ctx.dev, generator=g)
                      for _ in range(2)]
         self.wpr = (self.cols + 63) // 64
-        self.planes = ctx.empty_i64(max(1, self.nplanes), self.rows, self.wpr)
+        self.store_planes = args.store_planes
+        self.planes = ctx.empty_i64(max(1, self.nplanes), self.rows, self.wpr) if self.store_planes else None
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
         n = max(1, self.nplanes)
@@ -339,7 +350,8 @@ class C3Planes(C3):
         if self.nplanes:  # both streams written packed (word-aligned, plane order): the gather sends them as is
             c.encode_gray_packed(self.gray[self.k & 1], nplanes=self.nplanes, plane0=self.lo, planes=self.planes,
                                  slots=(self.slot_g, self.slot_e), outs=(self.out_g, self.out_e),
-                                 bits=(self.bits_g, self.bits_e), offs=(self.off_g, self.off_e))
+                                 bits=(self.bits_g, self.bits_e), offs=(self.off_g, self.off_e),
+                                 store_planes=self.store_planes)
         got = []
         for packed, off in ((self.out_g, self.off_g), (self.out_e, self.off_e)):
             if self.world > 1:
@@ -373,6 +385,9 @@ class C3Planes(C3):
         return int(b) / 8.0
 
     def host_planes(self, rows):
+        if self.planes is None:
+            return self.pybic.as_u64(self.ctx.bitplanes_u8(self.gray[(self.k - 1) & 1][:rows], nplanes=self.nplanes,
+                                                           plane0=self.lo))
         return self.pybic.as_u64(self.planes[:self.nplanes, :rows])
 
     def check(self, oracle):

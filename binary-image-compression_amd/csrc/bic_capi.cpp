@@ -43,6 +43,8 @@ struct bic_ctx {
   double* enuml_staging = nullptr;  // pinned host staging for it
   size_t enuml_cap = 0;           // entries
   std::vector<double> enuml_host;  // what ctx->enuml holds
+  uint64_t* rbuf = nullptr;       // bic_encode_gray* without planes: the count pass's residual planes
+  size_t rbuf_bytes = 0;
   unsigned match_parts = 0;       // bic_set_match_parts: workgroups per tile (0 = by region size)
   // kernel timing (bic_prof_*): HIP events recorded on the launch stream around each kernel
   bool prof_on = false;
@@ -228,6 +230,7 @@ int bic_ctx_destroy(bic_ctx* ctx) {
   if (ctx->enuml) (void)hipFree(ctx->enuml);
   if (ctx->enuml_staging) (void)hipHostFree(ctx->enuml_staging);
   if (ctx->lut) (void)hipFree(ctx->lut);
+  if (ctx->rbuf) (void)hipFree(ctx->rbuf);
   if (ctx->lentab) (void)hipFree(ctx->lentab);
   if (ctx->staging) (void)hipHostFree(ctx->staging);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
@@ -530,7 +533,23 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   if (!out_golomb && !out_eg) return BIC_EINVAL;
   if (out_golomb && (!bits_golomb || slot_golomb == 0)) return BIC_EINVAL;
   if (out_eg && (!bits_eg || slot_eg == 0)) return BIC_EINVAL;
-  if (rows && (!gray || !planes)) return BIC_EINVAL;
+  if (rows && !gray) return BIC_EINVAL;
+  if (!planes && rows) {
+    // no bitplanes wanted: the count pass stores the med residual planes into the context's buffer
+    // (the same bytes the bitplanes would take) and the encoder reads them with prediction off --
+    // no row above, no med in the emission. Same streams (predict off on R = med on P).
+    const size_t need = (size_t)nplanes * rows * wpr * 8;
+    if (ctx->rbuf_bytes < need) {
+      BIC_HIP(hipStreamSynchronize(ctx->cur));
+      if (ctx->rbuf) (void)hipFree(ctx->rbuf);
+      ctx->rbuf = nullptr;
+      ctx->rbuf_bytes = 0;
+      if (hipMalloc(&ctx->rbuf, need) != hipSuccess) return BIC_ENOMEM;
+      ctx->rbuf_bytes = need;
+    }
+  }
+  const bool store_resid = !planes && predict;
+  if (!planes) planes = ctx->rbuf;
   const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
   const bool fuse = rows && bic::fused_supported(g) && !ctx->force_multipass && !ctx->two_pass && !ctx->single_kernel &&
                     staged_pays(ctx, g) &&
@@ -540,7 +559,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
     return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
                               off_golomb, out_eg, slot_eg, bits_eg, off_eg, row_index);
   }
-  const int pr = predict ? 1 : 0;
+  const int pr = predict && !store_resid ? 1 : 0;  // R stored: the encoder codes it as given
   if ((rc = ensure_scratch(ctx, bic::fused_scratch_bytes(g)))) return rc;
   bic::FusedScratch fs = bic::carve_fused_scratch(ctx->scratch, g);
   fs.counted = true;
@@ -555,14 +574,15 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   };
   stage(bic::kFusedPrep);
   timed(ctx, "bitplanes_count", [&] {
-    bic::launch_gray_rows(ctx->cur, gray, pitch, g, pr, plane0, planes, fs.sones, fs.krec, fs.kpos, fs.counter);
+    bic::launch_gray_rows(ctx->cur, gray, pitch, g, predict ? 1 : 0, plane0, planes, fs.sones, fs.krec, fs.kpos,
+                          fs.counter, store_resid);
   });
   timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
   timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
         [&] { stage(bic::kFusedRows); });
   timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
   BIC_HIP(hipGetLastError());
-  if (row_index && !out_golomb) return bic_row_index(ctx, planes, nplanes, rows, cols, wpr, predict, row_index);
+  if (row_index && !out_golomb) return bic_row_index(ctx, planes, nplanes, rows, cols, wpr, pr, row_index);
   return BIC_OK;
 }
 

@@ -151,8 +151,11 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 // k statistics records per row (one per 64-word strip)
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes);
 uint32_t gray_strips(const Geom& g);
+// store_resid: the words stored are the med residual R (planes = the caller's bitplanes are not
+// wanted; the encoder then reads R with predict off), not the bitplanes P
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
-                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero);
+                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero,
+                      bool store_resid = false);
 
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
                          uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd);

@@ -519,7 +519,7 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
   }
 }
 
-template <bool PREDICT, bool FULL>
+template <bool PREDICT, bool FULL, bool STORE_R>
 __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray, size_t pitch, const Geom& g,
                                                 uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
                                                 uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
@@ -574,7 +574,7 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       if (b >= np) break;
-      if (in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = pw[b];
+      if (!STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = pw[b];
       uint64_t R = pw[b];
       if constexpr (PREDICT) {
         const uint64_t D = pw[b] ^ up[b];
@@ -583,6 +583,7 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
         if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
         up[b] = pw[b];
       }
+      if (STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = R;
       strip_word_put(tw, b, R, (int32_t)(w * 64));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -596,7 +597,7 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
   }
 }
 
-template <bool PREDICT>
+template <bool PREDICT, bool STORE_R>
 __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
                                                         uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
@@ -610,9 +611,9 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
   if (r0 >= g.rows) return;  // whole wave
   // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
   if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
-    gray_strip_rows<PREDICT, true>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+    gray_strip_rows<PREDICT, true, STORE_R>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
   else
-    gray_strip_rows<PREDICT, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+    gray_strip_rows<PREDICT, false, STORE_R>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
 }
 
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes) {
@@ -621,12 +622,14 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
 }
 
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
-                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero) {
+                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero, bool store_resid) {
   const uint32_t ns = gray_strips(g);
   const uint64_t waves = (uint64_t)(g.rows + kGrayRows - 1) / kGrayRows * ns;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
-  if (predict) k_gray_strips<true><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero);
-  else k_gray_strips<false><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero);
+#define BIC_GS(P, R) k_gray_strips<P, R><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero)
+  if (predict) { if (store_resid) BIC_GS(true, true); else BIC_GS(true, false); }
+  else BIC_GS(false, false);  // without prediction R = P
+#undef BIC_GS
 }
 
 void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,

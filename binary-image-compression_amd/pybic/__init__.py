@@ -280,16 +280,17 @@ class Context:
         return (og, bg) if golomb else None, (oe, be) if eg else None
 
     def encode_gray(self, gray, cols=None, nplanes=8, predict=True, planes=None, slots=(None, None),
-                    outs=(None, None), bits=(None, None), golomb=True, eg=True, plane0=0):
+                    outs=(None, None), bits=(None, None), golomb=True, eg=True, plane0=0, store_planes=True):
         """gray uint8 [rows, pitch] -> (planes, (out_g, bits_g) or None, (out_e, bits_e) or None):
         the bitplanes and both streams of every plane in one call (bic_encode_gray; planes plane0 ..
-        plane0 + nplanes - 1 with bic_encode_gray_range)."""
+        plane0 + nplanes - 1 with bic_encode_gray_range). store_planes=False: planes NULL (not
+        returned: None), the count pass keeps the residual planes in the context instead."""
         rows, pitch = gray.shape
         cols = pitch if cols is None else cols
         wpr = (cols + 63) // 64
-        if planes is None:
+        if planes is None and store_planes:
             planes = self.empty_i64(nplanes, rows, wpr)
-        wpr = planes.shape[-1]
+        wpr = planes.shape[-1] if planes is not None else wpr
         res = []
         for on, coder, slot, out, b in ((golomb, CODER_GOLOMB, slots[0], outs[0], bits[0]),
                                         (eg, CODER_EG, slots[1], outs[1], bits[1])):
@@ -327,13 +328,14 @@ class Context:
 
     def encode_gray_packed(self, gray, cols=None, nplanes=8, plane0=0, predict=True, planes=None, golomb=True,
                            eg=True, slots=(None, None), outs=(None, None), bits=(None, None), offs=(None, None),
-                           row_index=None):
-        """bic_encode_gray_packed -> (planes, (out_g, bits_g, off_g) or None, (out_e, bits_e, off_e) or None)"""
+                           row_index=None, store_planes=True):
+        """bic_encode_gray_packed -> (planes, (out_g, bits_g, off_g) or None, (out_e, bits_e, off_e) or None)
+        (store_planes=False: planes NULL, returned as None)"""
         rows, pitch = gray.shape
         cols = pitch if cols is None else cols
-        if planes is None:
+        if planes is None and store_planes:
             planes = self.empty_i64(nplanes, rows, (cols + 63) // 64)
-        wpr = planes.shape[-1]
+        wpr = planes.shape[-1] if planes is not None else (cols + 63) // 64
         (og, sg, bg, fg), (oe, se, be, fe) = self._packed_bufs(nplanes, rows, cols, golomb, eg, slots, outs, bits, offs)
         self._bind_stream()
         self._chk(self.lib.bic_encode_gray_packed(self.h, _p(gray), pitch, rows, cols, plane0, nplanes, _p(planes), wpr,

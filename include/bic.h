@@ -129,7 +129,11 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
  * bic_bitplanes_u8, into `planes`) and both streams of every plane (as bic_encode_planes2). Rows of
  * up to 16384 columns whose gray rows hold ceil(cols/64)*64 readable bytes (pitch >= that, gray and
  * pitch 16-byte aligned) read the image once: the bitplane kernel also produces the encoder's
- * per-row counts. Otherwise the same result through the two separate calls. */
+ * per-row counts. Otherwise the same result through the two separate calls.
+ * planes may be NULL (also in the _range / _packed forms below): the bitplanes are then formed in
+ * registers only and not returned; the count pass stores each plane's med residual instead (in a
+ * buffer the context keeps, nplanes * rows * wpr words), from which the encoder writes the same
+ * streams without recomputing med (no row above, no prediction in the emission). */
 int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,
                     uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
                     uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg);

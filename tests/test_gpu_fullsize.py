@@ -62,6 +62,13 @@ def test_c3_full(ctx, oracle, kind):
     finally:
         ctx.set_one_stream(False)
     _check_streams(ctx, exp, 8, (og, oe))
+    # planes NULL (the bench's default): the count pass keeps the residual, the encoder codes it as is
+    for t in (og[0], og[1], oe[0], oe[1]):
+        t.fill_(-1)
+    none, _, _ = ctx.encode_gray(g, nplanes=8, outs=(og[0], oe[0]), bits=(og[1], oe[1]), store_planes=False)
+    ctx.sync()
+    assert none is None
+    _check_streams(ctx, exp, 8, (og, oe))
 
 
 @pytest.mark.parametrize("p,pred", [(0.5, 0), (0.05, 0), (0.5, 1)])

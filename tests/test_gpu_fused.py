@@ -220,6 +220,49 @@ def test_encode_gray(ctx, oracle, staged, rows, cols, pitch, nplanes, kind):
                 assert stream_bytes(out[k], nb) == est.tobytes(), (pred, k, coder)
 
 
+@pytest.mark.parametrize("rows,cols,pitch,plane0,nplanes,kind", [
+    (1, 64, 64, 0, 8, "uniform"), (17, 100, 128, 0, 8, "uniform"), (33, 4096, 4096, 0, 8, "uniform"),
+    (40, 5000, 5120, 2, 3, "smooth"), (24, 16384, 16384, 0, 8, "uniform"), (70, 16384, 16384, 1, 6, "smooth"),
+    (9, 300, 300, 0, 8, "uniform"),  # pitch < used * 64: the two-call path into the context's buffer
+    (60, 4096, 4096, 0, 8, "blank_top"),  # the planes' first residual 1 far below row 0
+])
+def test_encode_gray_no_planes(ctx, oracle, staged, rows, cols, pitch, plane0, nplanes, kind):
+    """bic_encode_gray(_range / _packed) with planes NULL (the count pass keeps the med residual and
+    the encoder codes it without prediction) == the oracle's streams of bitplane_tool's planes, and
+    the packed form's row index == the oracle's"""
+    t = ctx.torch
+    img = np.zeros((rows, pitch), np.uint8)
+    base = "smooth" if kind == "blank_top" else kind
+    img[:, :cols] = _gray(oracle, rows * 5 + cols + plane0, rows, cols, base)
+    if kind == "blank_top":
+        img[:rows // 2, :cols] = 0x37  # constant rows: residual 0 until row rows / 2 (column 0 aside)
+        img[:rows // 2, 0] = 0x37
+    g = t.from_numpy(img).to(ctx.dev)
+    exp_planes = oracle.bitplanes(np.ascontiguousarray(img[:, :cols]), 8)[plane0:plane0 + nplanes]
+    for pred in (1, 0):
+        planes, (og, bg), (oe, be) = ctx.encode_gray(g, cols=cols, nplanes=nplanes, predict=bool(pred), plane0=plane0,
+                                                      store_planes=False)
+        ctx.sync()
+        assert planes is None
+        for k in range(nplanes):
+            for coder, out, bits in ((0, og, bg), (1, oe, be)):
+                eb, est, _ = oracle.encode_plane(exp_planes[k], cols, pred, coder)
+                nb = int(as_u64(bits)[k])
+                assert nb == eb, (pred, k, coder)
+                assert stream_bytes(out[k], nb) == est.tobytes(), (pred, k, coder)
+    idx = ctx.empty_i64(nplanes * rows * 2)
+    _, (og, bg, fg), (oe, be, fe) = ctx.encode_gray_packed(g, cols=cols, nplanes=nplanes, plane0=plane0,
+                                                           store_planes=False, row_index=idx)
+    ctx.sync()
+    for coder, out, off in ((0, og, fg), (1, oe, fe)):
+        exp, eoff = _packed_expect(oracle, exp_planes, cols, 1, coder)
+        assert list(as_u64(off)) == eoff
+        assert as_u64(out)[:eoff[-1]].tobytes() == exp
+    ri = as_u64(idx).reshape(nplanes, 2 * rows)
+    for k in range(nplanes):
+        assert np.array_equal(ri[k], oracle.row_index(exp_planes[k], cols, 1)), k
+
+
 def test_encode_gray_matches_two_calls(ctx, oracle, staged):
     rows, cols = 300, 16384
     img = _gray(oracle, 5, rows, cols, "uniform")
