@@ -462,6 +462,7 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     fs.off_g = off_golomb;
     fs.off_e = off_eg;
     fs.index = row_index;
+    fs.atom = true;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -567,6 +568,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   fs.off_g = off_golomb;
   fs.off_e = off_eg;
   fs.index = out_golomb ? row_index : nullptr;
+  fs.atom = true;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,

@@ -581,7 +581,8 @@ __device__ __forceinline__ void write_row64(const uint64_t* img, uint64_t L, uin
     const uint64_t v = funnel64(prev, cur, g);
     const bool whole = (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
     if (whole) out[w0 + t] = bswap64(v);
-    else frag[t == 0 ? 0 : 1] = v;
+    else if (frag) frag[t == 0 ? 0 : 1] = v;
+    else atomicOr(reinterpret_cast<unsigned long long*>(out + w0 + t), (unsigned long long)bswap64(v));  // zeroed shared word
   }
 }
 

@@ -556,6 +556,14 @@ __device__ __forceinline__ bool word_complete(uint64_t w, uint64_t G, uint64_t L
   return w * 64 >= G && w * 64 + 64 <= G + L;
 }
 
+// A word the row shares with a neighbouring row: into the fragment table (k_fixup combines them),
+// or -- frag null, the staged encoder -- OR'd straight into the stream word, which the prefix
+// kernels zeroed (k_scan_rows / k_rebase_zero), so no fixup launch is needed.
+__device__ __forceinline__ void put_shared(uint64_t* out, uint64_t wi, uint64_t* frag, int which, uint64_t v) {
+  if (frag) frag[which] = v;
+  else if (v) atomicOr(reinterpret_cast<unsigned long long*>(out + wi), (unsigned long long)bswap64(v));
+}
+
 // Write a row image of L bits to absolute bit G of out (threads tid of nt: a wave's lanes by
 // default): whole words with plain stores, the
 // first/last word (when shared with another row) into frag[0]/frag[1]. Output word t of the row
@@ -570,7 +578,7 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
       const uint64_t wb = (w0 + t) * 64;
       const uint64_t v = img64(img, (int64_t)wb - (int64_t)G, ins);
       if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
-      else frag[t == 0 ? 0 : 1] = v;
+      else put_shared(out, w0 + t, frag, t == 0 ? 0 : 1, v);
     }
     return;
   }
@@ -584,7 +592,7 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
     if (a < 0) v >>= -a;
     if (t != 0 && t != (uint32_t)nw - 1) out[w0 + t] = bswap64(v);
     else if (word_complete(w0 + t, G, L)) out[w0 + t] = bswap64(v);
-    else frag[t == 0 ? 0 : 1] = v;
+    else put_shared(out, w0 + t, frag, t == 0 ? 0 : 1, v);
   }
 }
 
@@ -627,6 +635,7 @@ struct FusedArgs {
   uint64_t* off_g;
   uint64_t* off_e;
   uint64_t* index;  // FusedScratch::index
+  bool atom;        // FusedScratch::atom (staged encoder): shared words OR'd into pre-zeroed stream words
 #ifdef BIC_STAMPS
   int known;
   int dbg;  // diagnostic (BIC_EMIT_DBG): k_emit_known skips 1 = LDS-image Golomb rows, 2 = EG rows, 4 = k = 0 copies
@@ -719,8 +728,8 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
     tl |= shfl_u64(tl, lane ^ d);
   }
   if (lane == 0) {
-    if (hpart) frag[0] = h | (wh == wt ? tl : 0);
-    if (tpart && wt != wh) frag[1] = tl;
+    if (hpart) put_shared(a.out_g, wh, a.atom ? nullptr : frag, 0, h | (wh == wt ? tl : 0));
+    if (tpart && wt != wh) put_shared(a.out_g, wt, a.atom ? nullptr : frag, 1, tl);
   }
 }
 
@@ -1118,7 +1127,7 @@ __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geo
     if (j < nw) {
       const uint64_t wi = w0 + j;
       if ((j != 0 || head_whole) && (j != nw - 1 || tail_whole)) out[wi] = bswap64(v);
-      else frag[j == 0 ? 0 : 1] = v;
+      else put_shared(out, wi, frag, j == 0 ? 0 : 1, v);
     }
   }
 }
@@ -1276,6 +1285,15 @@ __device__ __forceinline__ bool row_class(const FusedArgs& a, uint64_t id, uint3
   return true;
 }
 
+// Zero the stream words a row of L bits at absolute bit G shares with its neighbours (its first
+// word when it starts inside one, its last when it ends inside one); they are OR'd by the emission
+// launches afterwards (FusedScratch::atom). Both rows at a boundary zero the same word: same value.
+__device__ __forceinline__ void zero_shared(uint64_t* out, uint64_t G, uint64_t L) {
+  if (!L) return;
+  if (G & 63) out[G >> 6] = 0;
+  if ((G + L) & 63) out[(G + L - 1) >> 6] = 0;
+}
+
 // Exclusive per-plane scan of per-row values. Each 1024-thread workgroup owns kScanChunk rows of a
 // plane (kScanPer consecutive rows per thread) and sums the plane's earlier rows itself (coalesced,
 // at most rows / 1024 loads per thread), so no workgroup waits on another and a plane spreads over
@@ -1361,6 +1379,12 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       // the row holding the plane's first 1 (EG inserts a '0' after it): listed for REST here unless
       // walked (k_row_walk lists it)
       if (in && pre == 0 && v[i] > 0 && !walk) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)(base + r);
+      if (in && a.atom && a.out_e && !a.ebase) {  // slot mode: the row's shared EG words (offsets in closed form)
+        const uint64_t cap = a.slot_e * 64;
+        const uint64_t Ge = (uint64_t)r * (g.cols + 1) + (pre > 0 ? 1 : 0);
+        const uint64_t Le = (uint64_t)g.cols + 1 + (pre == 0 && v[i] > 0 ? 1 : 0);
+        if (Ge + Le <= cap) zero_shared(a.out_e + (uint64_t)plane * a.slot_e, Ge, Le);
+      }
       pre += v[i];
     }
     if (b == nb - 1 && threadIdx.x == 0) a.pones[plane] = btot + tot;  // the plane's residual 1s
@@ -1374,6 +1398,8 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
         if (pre + v[i] > cap) {
           a.glen[base + r] = 0;  // overflowed: nothing written, fixup skips
           atomicOr(&a.flags[0], 1u);
+        } else if (a.atom && !a.off_g) {
+          zero_shared(a.out_g, (uint64_t)plane * cap + pre, v[i]);  // slot mode (packed: k_rebase_zero)
         }
       }
       pre += v[i];
@@ -1467,6 +1493,10 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
 // tables are staged (XCD-remapped block order: the waves of one XCD hold consecutive rows, the
 // row above is an L2 hit).
 constexpr int kEmitWaves = 4;
+#ifndef BIC_EMIT_PREFETCH
+#define BIC_EMIT_PREFETCH 0  // measured slower (C3 emission 238 -> 248 us): off
+#endif
+constexpr bool kEmitPrefetch = BIC_EMIT_PREFETCH != 0;  // next row loaded during this one (no prediction)
 constexpr bool kRestAux = true;  // k_emit_rest on the context's second stream (beside k_emit_known)
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) {
@@ -1482,14 +1512,45 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
   // persistent waves: rows id, id + stride, ...
   const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
-  for (uint64_t id = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave; id < nrows; id += stride) {
+  const uint64_t id0 = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
+  // Without prediction (the residual planes bic_encode_gray's count pass stores) a row is its WPL
+  // words alone: the next row's words and metadata are loaded while this one is coded (8 VGPRs at
+  // WPL = 4, within the kernel's 4 waves per SIMD), so a wave always has a row in flight.
+  constexpr bool kPre = kEmitPrefetch && !PREDICT;
+  uint64_t pp_[WPL];
+  uint32_t pO = 0;
+  uint64_t pLf = 0, pGb = 0;
+  auto fetch = [&](uint64_t fid) {
+    const uint32_t fplane = (uint32_t)(fid / g.rows), frow = (uint32_t)(fid % g.rows);
+    uint64_t dummy[WPL];
+    row_load<WPL, false>(a.planes, g, fplane, frow, pp_, dummy);
+    pO = a.row_o[fid];
+    pLf = DO_G ? a.glen[fid] : 0;
+    pGb = DO_G ? a.gboff[fid] : 0;
+  };
+  if (kPre && id0 < nrows) fetch(id0);
+  for (uint64_t id = id0; id < nrows; id += stride) {
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     STAMP(0);
     uint64_t cp_[WPL], cu_[WPL];
-    row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
-    const uint32_t O = a.row_o[id];
-    const uint64_t Lf = DO_G ? a.glen[id] : 0;
-    const uint64_t Gb = DO_G ? a.gboff[id] : 0;  // loaded with the row, not after the branch that uses it
+    uint32_t O;
+    uint64_t Lf, Gb;
+    if constexpr (kPre) {
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        cp_[t] = pp_[t];
+        cu_[t] = 0;
+      }
+      O = pO;
+      Lf = pLf;
+      Gb = pGb;
+      if (id + stride < nrows) fetch(id + stride);
+    } else {
+      row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
+      O = a.row_o[id];
+      Lf = DO_G ? a.glen[id] : 0;
+      Gb = DO_G ? a.gboff[id] : 0;  // loaded with the row, not after the branch that uses it
+    }
     const uint64_t L = Lf & kLenMask;
     const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
     bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
@@ -1518,7 +1579,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
       const uint64_t cap = a.slot_e * 64;
       const uint64_t Ge = (a.ebase ? a.ebase[plane] : (uint64_t)plane * cap) + Ge_rel;
       if (Ge_rel + Le <= cap) {
-        if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
+        if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
         if (lane == 0) {
           a.eboff[id] = Ge;
           a.elen[id] = Le;
@@ -1540,7 +1601,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
 #ifdef BIC_STAMPS
         if (!(a.dbg & 4))
 #endif
-        eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.gfrag + 2 * id);
+        eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
       } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
         uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
         int jpc = -1;
@@ -1568,7 +1629,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
         if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        write_row64(img, L, Gb, a.out_g, a.gfrag + 2 * id);
+        write_row64(img, L, Gb, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
       }
       if (lane == 0) {
         // glen keeps its flags: k_emit_rest (on the other stream) reads them too
@@ -1647,7 +1708,7 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
       const uint64_t cap = a.slot_e * 64;
       if (Ge_rel + Le <= cap)
         write_row(eimg, Le, (a.ebase ? a.ebase[plane] : (uint64_t)plane * cap) + Ge_rel, (int64_t)fcol + 1, a.out_e,
-                  a.efrag + 2 * id, threadIdx.x, blockDim.x);
+                  a.atom ? nullptr : a.efrag + 2 * id, threadIdx.x, blockDim.x);
     }
     if (gmix) {
       const uint32_t arow = row * (g.cols + 1);
@@ -1672,7 +1733,7 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
       }
       __syncthreads();
       if (threadIdx.x == 0 && tot != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.gfrag + 2 * id, threadIdx.x, blockDim.x);
+      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id, threadIdx.x, blockDim.x);
     }
     __syncthreads();  // the images and sh are reused by the next row
   }
@@ -1723,11 +1784,24 @@ __global__ __launch_bounds__(256) void k_row_index(FusedArgs a) {
 }
 
 // Packed Golomb output: every row's offset moves from its plane's slot to the plane's packed start.
+// With FusedScratch::atom the rows' shared words of both packed streams are zeroed here too (their
+// offsets are final only now).
 __global__ __launch_bounds__(256) void k_shift_gboff(FusedArgs a) {
   const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (id >= (uint64_t)a.g.rows * a.g.nplanes) return;
-  const uint32_t plane = (uint32_t)(id / a.g.rows);
-  a.gboff[id] = a.gboff[id] - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64;
+  const uint32_t plane = (uint32_t)(id / a.g.rows), row = (uint32_t)(id % a.g.rows);
+  if (a.off_g) {
+    const uint64_t G = a.gboff[id] - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64;
+    a.gboff[id] = G;
+    if (a.atom) zero_shared(a.out_g, G, a.glen[id] & kLenMask);  // (0 when the row overflowed)
+  }
+  if (a.off_e && a.atom) {
+    const uint32_t O = a.row_o[id];
+    const uint32_t onext = row + 1 < a.g.rows ? a.row_o[id + 1] : (uint32_t)a.pones[plane];
+    const uint64_t Ge_rel = (uint64_t)row * (a.g.cols + 1) + (O > 0 ? 1 : 0);
+    const uint64_t Le = (uint64_t)a.g.cols + 1 + (O == 0 && onext > 0 ? 1 : 0);
+    if (Ge_rel + Le <= a.slot_e * 64) zero_shared(a.out_e, a.ebase[plane] * 64 + Ge_rel, Le);
+  }
 }
 
 // Combine the fragments of the words rows share: the row holding a shared word's first bit
@@ -1848,6 +1922,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   a.off_e = out_e ? fs.off_e : nullptr;
   a.ebase = a.off_e ? fs.ebase : nullptr;
   a.index = out_g ? fs.index : nullptr;
+  a.atom = fs.atom && mode == kEncStaged;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
   a.dbg = getenv("BIC_EMIT_DBG") ? atoi(getenv("BIC_EMIT_DBG")) : 0;
@@ -1862,6 +1937,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       if (predict) k_rows_global<true><<<256, 256, 0, s>>>(a);
       else k_rows_global<false><<<256, 256, 0, s>>>(a);
     }
+    if (a.atom) return;  // shared words already OR'd into their zeroed stream words
     k_fixup<<<dg && de ? 2 * fgrid : fgrid, 256, 0, s>>>(dg ? fs.gboff : fs.eboff, dg ? fs.glen : fs.elen,
                                                         dg ? fs.gfrag : fs.efrag, dg ? out_g : out_e,
                                                         fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows,
@@ -1884,7 +1960,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       }
       if (a.off_g || a.off_e) {  // packed output: the planes' start words, then the rows' Golomb offsets
         k_plane_bases<<<1, 1024, 0, s>>>(a);
-        if (a.off_g) k_shift_gboff<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
+        if (a.off_g || a.atom) k_shift_gboff<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
       }
       return;
     }

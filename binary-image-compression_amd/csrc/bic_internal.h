@@ -126,6 +126,9 @@ struct FusedScratch {
   // row index for the decoders (bic_row_index): per row, the bit offset of its first Golomb
   // codeword in its plane's stream and the residual 1s of the plane before it; null: not written
   uint64_t* index = nullptr;
+  // staged encoder with output: the prefix kernels zero the stream words rows share and the
+  // emission launches OR their parts into them (no fragment table, no fixup launch)
+  bool atom = false;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);

@@ -460,7 +460,10 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 // records in one transposed pass, strip_records; row_kstats combines a row's strips). The next row's loads are in flight while a row is used.
 // The gray rows must hold used * 64 readable bytes (pitch >= used * 64, 16-byte aligned;
 // gray_rows_supported).
-constexpr int kGrayRows = 8;
+#ifndef BIC_GRAY_ROWS
+#define BIC_GRAY_ROWS 4
+#endif
+constexpr int kGrayRows = BIC_GRAY_ROWS;
 uint32_t gray_strips(const Geom& g) { return (g.used + 63) / 64; }
 
 // out[b] = bytes b of w0..w3, w0's in the most significant byte (a 4x4 byte transpose)
@@ -519,13 +522,24 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
   }
 }
 
-template <bool PREDICT, bool FULL, bool STORE_R>
+// PIPE: the strip records of row r - 1 are made while row r's plane words are formed (two LDS
+// tables per wave, one wave barrier per row), so the records' serial DPP chain overlaps independent
+// work; NP8: every plane of the image (no plane-count tests in the row loop)
+#ifndef BIC_GRAY_PIPE
+#define BIC_GRAY_PIPE 0
+#endif
+constexpr bool kGrayPipe = BIC_GRAY_PIPE != 0;
+#ifndef BIC_GRAY_PREFETCH
+#define BIC_GRAY_PREFETCH 1
+#endif
+constexpr bool kGrayPrefetch = BIC_GRAY_PREFETCH != 0;  // the next row's pixels loaded during this row
+template <bool PREDICT, bool FULL, bool STORE_R, bool NP8>
 __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray, size_t pitch, const Geom& g,
                                                 uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
                                                 uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
                                                 int4* __restrict__ krec, uint32_t* __restrict__ kpos, uint32_t* tw) {
   const int lane = lane_id();
-  const int np = (int)g.nplanes;
+  const int np = NP8 ? 8 : (int)g.nplanes;
   const uint32_t w = s * 64 + lane;
   const bool in = FULL || w < g.used;
   const uint64_t mask = FULL ? ~0ull : in ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
@@ -560,7 +574,7 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
     const uint32_t row = r0 + r;
     uint4 nxt[4];
     uint32_t nlb = 0;
-    if (r + 1 < nr) load(row + 1, nxt, nlb);
+    if (kGrayPrefetch && r + 1 < nr) load(row + 1, nxt, nlb);
     // D bits (8 planes per byte) of the pixel left of the word: lane l - 1's last, or the strip's
     // preceding pixel for lane 0 (0 at column 0)
     const uint32_t cl = cur[3].w >> 24;
@@ -571,9 +585,10 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
     ulb = clb;
     uint64_t pw[8];
     gray_to_planes<FULL>(cur, pw, mask);
+    uint32_t* tb = kGrayPipe ? tw + (r & 1) * 1024 : tw;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
-      if (b >= np) break;
+      if (!NP8 && b >= np) break;
       if (!STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = pw[b];
       uint64_t R = pw[b];
       if constexpr (PREDICT) {
@@ -584,25 +599,43 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
         up[b] = pw[b];
       }
       if (STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = R;
-      strip_word_put(tw, b, R, (int32_t)(w * 64));
+      strip_word_put(tb, b, R, (int32_t)(w * 64));
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    strip_records(tw, np, krec, kpos, sones, (uint64_t)row * ns + s, (uint64_t)g.rows * ns);
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row rewrites the table
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (kGrayPipe) {
+      // the previous row's records (its table was completed before the last barrier); none at r = 0
+      strip_records(tw + ((r + 1) & 1) * 1024, r ? np : 0, krec, kpos, sones, (uint64_t)(row - (r ? 1 : 0)) * ns + s,
+                    (uint64_t)g.rows * ns);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      strip_records(tw, np, krec, kpos, sones, (uint64_t)row * ns + s, (uint64_t)g.rows * ns);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row rewrites the table
+      __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (kGrayPrefetch) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
-    clb = nlb;
+      for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+      clb = nlb;
+    } else if (r + 1 < nr) {
+      load(row + 1, cur, clb);
+    }
   }
+  if constexpr (kGrayPipe)
+    strip_records(tw + ((nr - 1) & 1) * 1024, np, krec, kpos, sones, (uint64_t)(r0 + nr - 1) * ns + s,
+                  (uint64_t)g.rows * ns);
 }
 
+#ifndef BIC_GRAY_WAVES
+#define BIC_GRAY_WAVES 4
+#endif
 template <bool PREDICT, bool STORE_R>
-__global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
+__global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
                                                         uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
                                                         uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
-  __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][kGrayPipe ? 2048 : 1024];  // strip_word_put tables
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   uint32_t* tw = tab[threadIdx.x >> 6];
   const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
@@ -610,10 +643,12 @@ __global__ __launch_bounds__(kBlock) void k_gray_strips(const uint8_t* __restric
   const uint32_t r0 = (uint32_t)(gw / ns) * kGrayRows;
   if (r0 >= g.rows) return;  // whole wave
   // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
-  if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
-    gray_strip_rows<PREDICT, true, STORE_R>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+  if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
+    gray_strip_rows<PREDICT, true, STORE_R, true>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+  else if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
+    gray_strip_rows<PREDICT, true, STORE_R, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
   else
-    gray_strip_rows<PREDICT, false, STORE_R>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+    gray_strip_rows<PREDICT, false, STORE_R, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
 }
 
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes) {
