@@ -750,10 +750,27 @@ int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
   }
   // per-tile chosen weights feed the sample coder: use the caller's array or scratch
   const size_t wbytes = ((ntiles * sizeof(uint32_t)) + 255) & ~(size_t)255;
-  if ((rc = ensure_scratch(ctx, wbytes + bic::sample_scratch_bytes(ntiles)))) return rc;
+  const uint32_t nsplit = bic::tiles_split_blocks((uint32_t)rows, (uint32_t)cols, W);
+  const size_t lbytes = ((size_t)nsplit * 8 + 255) & ~(size_t)255;
+  if ((rc = ensure_scratch(ctx, wbytes + lbytes + bic::sample_scratch_bytes(ntiles)))) return rc;
   uint32_t* wts = weights ? weights : reinterpret_cast<uint32_t*>(ctx->scratch);
+  uint64_t* lpart = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ctx->scratch) + wbytes);
   const bic::SampleScratch ss =
-      bic::carve_sample_scratch(reinterpret_cast<char*>(ctx->scratch) + wbytes, ntiles);
+      bic::carve_sample_scratch(reinterpret_cast<char*>(ctx->scratch) + wbytes + lbytes, ntiles);
+  if (nsplit) {
+    // three launches: tiles (which zero the coder's scratch and leave per-block length sums), the
+    // coder's scan and emit (stats[0..1] from the scan, stats[2] = the length sums, from the emit)
+    timed(ctx, "tiles", [&] {
+      bic::launch_tiles_split(ctx->cur, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, W, ctx->lentab, wts,
+                              w_nonpred, w_pred, modes, resid, lpart, ss.counter, (uint32_t)(ss.zero_bytes / 4));
+    });
+    timed(ctx, "golomb_samples", [&] {
+      bic::launch_golomb_samples(ctx->cur, wts, ntiles, 0, 0, 0, stream, cap_words, stats, ss, ctx->flags, true, lpart,
+                                 nsplit, stats + 2);
+    });
+    BIC_HIP(hipGetLastError());
+    return BIC_OK;
+  }
   BIC_HIP(hipMemsetAsync(stats, 0, 3 * sizeof(uint64_t), ctx->cur));
   timed(ctx, "tiles", [&] {
     bic::launch_tiles(ctx->cur, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, W, ctx->lentab, wts,

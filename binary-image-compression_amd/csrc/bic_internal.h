@@ -85,9 +85,17 @@ struct SampleScratch {
 };
 size_t sample_scratch_bytes(size_t n);
 SampleScratch carve_sample_scratch(void* base, size_t n);
+// prezeroed: the scratch's counter and records are already 0 (k_tiles_split zeroes them); lpart
+// (nullable): nlpart per-block sums added into *lout by the emit launch
 void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uint64_t n0,
                            uint64_t a0, unsigned bit0, uint64_t* out, size_t cap_words,
-                           uint64_t* bits_out, const SampleScratch& ss, uint32_t* flags);
+                           uint64_t* bits_out, const SampleScratch& ss, uint32_t* flags, bool prezeroed = false,
+                           const uint64_t* lpart = nullptr, uint32_t nlpart = 0, uint64_t* lout = nullptr);
+// the aligned tile path split over 4 waves per strip (W in 8, 16, 32, 64; else 0 blocks)
+uint32_t tiles_split_blocks(uint32_t rows, uint32_t cols, uint32_t W);
+void launch_tiles_split(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t W,
+                        const uint64_t* lentab_dev, uint32_t* weights, uint32_t* w_nonpred, uint32_t* w_pred,
+                        uint8_t* modes, uint64_t* resid, uint64_t* lpart, uint32_t* zero, uint32_t nzero);
 
 // Tiles (compress7 R = 0 path).
 void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols,

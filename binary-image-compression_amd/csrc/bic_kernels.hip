@@ -1165,8 +1165,17 @@ __global__ __launch_bounds__(kBlock) void k_samp_scan(const uint32_t* __restrict
 
 __global__ __launch_bounds__(kBlock) void k_samp_emit(const uint32_t* __restrict__ s, size_t n, uint64_t n0,
                                                       SampleScratch ss, uint64_t* out, const uint64_t* total_bits,
-                                                      unsigned bit0, size_t cap_words) {
+                                                      unsigned bit0, size_t cap_words, const uint64_t* lpart,
+                                                      uint32_t nlpart, uint64_t* lout) {
   __shared__ uint64_t tmp[17];
+  if (lpart && blockIdx.x == 0) {  // the tile kernel's per-block length sums (bic_patch_encode stats[2])
+    uint64_t l = 0;
+    for (uint32_t i = threadIdx.x; i < nlpart; i += kBlock) l += lpart[i];
+    uint64_t tot;
+    block_excl_scan<uint64_t>(l, tmp, tot);
+    if (threadIdx.x == 0) *lout = tot;
+    __syncthreads();  // tmp is reused below
+  }
   if ((bit0 + *total_bits + 63) / 64 > cap_words) return;  // overflow: write nothing (flagged)
   const uint32_t blk = blockIdx.x;
   const uint64_t base = (uint64_t)blk * kSampPerBlk + (uint64_t)threadIdx.x * kItems;
@@ -1225,15 +1234,17 @@ SampleScratch carve_sample_scratch(void* base, size_t n) {
 
 void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uint64_t n0,
                            uint64_t a0, unsigned bit0, uint64_t* out, size_t cap_words,
-                           uint64_t* bits_out, const SampleScratch& ss, uint32_t* flags) {
+                           uint64_t* bits_out, const SampleScratch& ss, uint32_t* flags, bool prezeroed,
+                           const uint64_t* lpart, uint32_t nlpart, uint64_t* lout) {
   const uint32_t nblk = (uint32_t)((n + kSampPerBlk - 1) / kSampPerBlk);
   if (nblk == 0) {
     (void)hipMemsetAsync(bits_out, 0, 2 * sizeof(uint64_t), s);
+    if (lpart) (void)hipMemsetAsync(lout, 0, sizeof(uint64_t), s);
     return;
   }
-  (void)hipMemsetAsync(ss.counter, 0, ss.zero_bytes, s);
+  if (!prezeroed) (void)hipMemsetAsync(ss.counter, 0, ss.zero_bytes, s);
   k_samp_scan<<<nblk, kBlock, 0, s>>>(samples, n, n0, a0, bit0, ss, out, cap_words, bits_out, flags, nblk);
-  if (out) k_samp_emit<<<nblk, kBlock, 0, s>>>(samples, n, n0, ss, out, bits_out, bit0, cap_words);
+  if (out) k_samp_emit<<<nblk, kBlock, 0, s>>>(samples, n, n0, ss, out, bits_out, bit0, cap_words, lpart, nlpart, lout);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1386,6 +1397,116 @@ __global__ __launch_bounds__(kBlock) void k_tiles_aligned(const uint64_t* __rest
   }
   L = wave_sum_u64(L);
   if (lane == 0 && L) atomicAdd(&stats[2], (unsigned long long)L);
+}
+
+// K8c: the aligned tile path with a strip of W rows split over a workgroup's 4 waves (W / 4 rows
+// each, kept in registers), so a launch has 4x the waves of k_tiles_aligned (C5, 8192^2 at W = 32:
+// 2048 waves instead of 512; the strip's serial row loads were its latency): per-wave partial tile
+// counts meet in LDS, every wave takes the totals for its lanes' tiles and writes its rows of the
+// residual image from registers. The tile length sum goes to lpart[block] (no atomics, no zeroed
+// stats: the sample coder adds the parts); the first blocks zero the sample coder's scratch
+// (`zero`, nzero words), so its launch needs no fill before it.
+template <int W>
+__global__ __launch_bounds__(256) void k_tiles_split(const uint64_t* __restrict__ plane, uint32_t rows, uint32_t cols,
+                                                     uint32_t wpr, uint32_t used, uint32_t nx,
+                                                     const uint64_t* __restrict__ lentab, uint32_t* weights,
+                                                     uint32_t* w_nonpred, uint32_t* w_pred, uint8_t* modes,
+                                                     uint64_t* resid, uint64_t* lpart, uint32_t* zero, uint32_t nzero) {
+  constexpr int T = 64 / W, RW = W / 4;
+  __shared__ uint32_t part[4][T][2][64];
+  const int lane = lane_id(), v = threadIdx.x >> 6;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nzero; i += gridDim.x * 256) zero[i] = 0;
+  const uint32_t groups = (used + 63) / 64;
+  const uint32_t ty = blockIdx.x / groups, w = (blockIdx.x % groups) * 64 + lane;
+  const bool act = w < used;
+  uint64_t F = 0;  // first column of every tile in the word
+#pragma unroll
+  for (int j = 0; j < T; ++j) F |= BIC_MSB >> (j * W);
+  const uint32_t r0 = v * RW;  // this wave's first row inside the tile
+  const uint64_t* src = plane + (uint64_t)ty * W * wpr + (act ? w : 0);
+  uint64_t x[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) x[r] = act ? src[(uint64_t)(r0 + r) * wpr] : 0;
+  const uint64_t above = (act && r0) ? src[(uint64_t)(r0 - 1) * wpr] : 0;  // the row above (inside the tile)
+  uint32_t co[T], cO[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) co[j] = cO[j] = 0;
+  uint64_t up = above;
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const uint64_t d = x[r] ^ up;
+    uint64_t R = d ^ ((d >> 1) & ~F);
+    if (r0 + r == 0) R &= ~F;  // compress7's med never writes a tile's R(0,0)
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const uint64_t m = (W == 64) ? ~0ull : (((1ull << W) - 1) << (64 - W * (j + 1)));
+      co[j] += (uint32_t)__popcll(x[r] & m);
+      cO[j] += (uint32_t)__popcll(R & m);
+    }
+    up = x[r];
+  }
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    part[v][j][0][lane] = co[j];
+    part[v][j][1][lane] = cO[j];
+  }
+  __syncthreads();
+  uint64_t L = 0, keepR = 0;  // keepR: word mask of the tiles coded as residuals ('O')
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const uint32_t to = part[0][j][0][lane] + part[1][j][0][lane] + part[2][j][0][lane] + part[3][j][0][lane];
+    const uint32_t tO = part[0][j][1][lane] + part[1][j][1][lane] + part[2][j][1][lane] + part[3][j][1][lane];
+    const uint32_t col0 = w * 64 + j * W;
+    if (!act || col0 >= cols) continue;
+    const bool pred = lentab[to] > lentab[tO];  // compress7_test.cpp:248
+    const uint32_t wc = pred ? tO : to;
+    if (pred) keepR |= (W == 64) ? ~0ull : (((1ull << W) - 1) << (64 - W * (j + 1)));
+    if (v == 0) {
+      const uint64_t tile = (uint64_t)ty * nx + col0 / W;
+      if (weights) weights[tile] = wc;
+      if (w_nonpred) w_nonpred[tile] = to;
+      if (w_pred) w_pred[tile] = tO;
+      if (modes) modes[tile] = pred ? 'O' : 'o';
+      L += lentab[wc];
+    }
+  }
+  if (resid && act) {
+    uint64_t* dst = resid + (uint64_t)ty * W * wpr + w;
+    const uint64_t valid = w == used - 1 && (cols & 63) ? ~(~0ull >> (cols & 63)) : ~0ull;
+    up = above;
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const uint64_t d = x[r] ^ up;
+      uint64_t R = d ^ ((d >> 1) & ~F);
+      if (r0 + r == 0) R &= ~F;
+      dst[(uint64_t)(r0 + r) * wpr] = ((R & keepR) | (x[r] & ~keepR)) & valid;
+      up = x[r];
+    }
+  }
+  if (v == 0) {
+    L = wave_sum_u64(L);
+    if (lane == 0) lpart[blockIdx.x] = L;
+  }
+}
+
+uint32_t tiles_split_blocks(uint32_t rows, uint32_t cols, uint32_t W) {
+  if (W != 8 && W != 16 && W != 32 && W != 64) return 0;
+  return rows / W * (((cols + 63) / 64 + 63) / 64);
+}
+
+void launch_tiles_split(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t W,
+                        const uint64_t* lentab_dev, uint32_t* weights, uint32_t* w_nonpred, uint32_t* w_pred,
+                        uint8_t* modes, uint64_t* resid, uint64_t* lpart, uint32_t* zero, uint32_t nzero) {
+  const uint32_t nx = cols / W, used = (cols + 63) / 64;
+  const uint32_t grid = tiles_split_blocks(rows, cols, W);
+  if (resid && wpr > used) (void)hipMemsetAsync(resid, 0, (size_t)rows * wpr * sizeof(uint64_t), s);
+#define BIC_TS(WW) k_tiles_split<WW><<<grid, 256, 0, s>>>(plane, rows, cols, wpr, used, nx, lentab_dev, weights, \
+                                                       w_nonpred, w_pred, modes, resid, lpart, zero, nzero)
+  if (W == 8) BIC_TS(8);
+  else if (W == 16) BIC_TS(16);
+  else if (W == 32) BIC_TS(32);
+  else BIC_TS(64);
+#undef BIC_TS
 }
 
 void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
