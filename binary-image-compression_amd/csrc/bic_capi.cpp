@@ -393,6 +393,18 @@ size_t bic_encode_slot_words(size_t rows, size_t cols, int coder) {
   return (size_t)((2 * base + 63) / 64 + 64);
 }
 
+// staged encoder: rows' shared stream words OR'd into words the prefix kernels zero, or (default)
+// the fragment table and k_fixup -- measured: the atomics cost the C3 emission 244 -> 455 us and C4's
+// 167 -> 262 us. BIC_COUNT_EG: the EG rows' inner words from bic_encode_gray's count pass -- measured
+// at C3: count pass 153 -> 220 us, emission 245 -> 218 us (step 0.455 -> 0.498 ms): off
+#ifndef BIC_ATOM_WORDS
+#define BIC_ATOM_WORDS 0
+#endif
+#ifndef BIC_COUNT_EG
+#define BIC_COUNT_EG 0
+#endif
+constexpr bool kAtomWords = BIC_ATOM_WORDS != 0, kCountEg = BIC_COUNT_EG != 0;
+
 namespace {
 // Packed output where the encoder cannot write it in place (encoders other than the staged one, the
 // multi-pass path): ONE encode of both coders into slots in stream-ordered temporaries, then
@@ -462,7 +474,7 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     fs.off_g = off_golomb;
     fs.off_e = off_eg;
     fs.index = row_index;
-    fs.atom = true;
+    fs.atom = kAtomWords;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -568,7 +580,12 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   fs.off_g = off_golomb;
   fs.off_e = off_eg;
   fs.index = out_golomb ? row_index : nullptr;
-  fs.atom = true;
+  fs.atom = kAtomWords;
+  // EG rows' inner words from the count pass (plane stride: the slot, or packed, the stream length
+  // of a plane holding a residual 1)
+  const uint64_t eg_words = ((uint64_t)rows * (cols + 1) + 1 + 63) / 64;
+  if (kCountEg && out_eg && bic::gray_eg_supported(g) && eg_words <= slot_eg)
+    fs.eg_cp = off_eg ? eg_words : slot_eg;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
@@ -577,7 +594,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   stage(bic::kFusedPrep);
   timed(ctx, "bitplanes_count", [&] {
     bic::launch_gray_rows(ctx->cur, gray, pitch, g, predict ? 1 : 0, plane0, planes, fs.sones, fs.krec, fs.kpos,
-                          fs.counter, store_resid);
+                          fs.counter, store_resid, fs.eg_cp ? out_eg : nullptr, fs.eg_cp);
   });
   timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
   timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",

@@ -218,6 +218,246 @@ __global__ __launch_bounds__(256) void k_dec_golomb_lanes(DecArgs a) {
   if (bad) atomicOr(&a.flags[1], 2u);                     // malformed stream (bic_sync: BIC_EDATA)
 }
 
+// Golomb, byte machine: still one lane per row, but every lane consumes its stream 8 bits per
+// step, so the stream words are needed on a uniform cadence (one 64-bit view per 8 steps, the next
+// word loaded a chunk ahead) and a step is one table lookup instead of a codeword's serial chain.
+// The state between steps: the phase (S: at a codeword start, U0 / U1: inside the unary part of a
+// k = 0 / k = 1 codeword, and LOW / UK: the binary / unary part of a k >= 2 codeword), the column
+// j of the next residual bit, n (samples so far, Golomb.h's N) and x = A - n (A counted bit by bit:
+// a unary '0' adds 2^k zero columns at once, a k = 1 low bit its value). While 0 < n and x + 16 <= n
+// every codeword start in the next 8 bits has k = golomb_k(n, A) = [x > 0] (A <= 2 n), and x moves
+// by at most +16 over them; the decisions inside 8 bits are the same for every x <= -5 and for every
+// x >= 5 (checked exhaustively), so one table entry per (phase, x clamped to [-5, 5], byte) gives
+// the step: the residual columns it produces (<= 16), dx and the phase after. Other steps (n = 0,
+// k >= 2, the row's last columns) go bit by bit through the general machine. The output words are
+// held in registers and stored at the chunk boundaries, so a wave's only memory waits there are
+// for the stream word loaded a chunk earlier.
+constexpr int kNibXLo = -5, kNibXN = 11;
+constexpr uint32_t kStepBits = 8, kStepVals = 1u << kStepBits;
+constexpr uint32_t kNibTab = 3 * kNibXN * kStepVals;
+enum : uint32_t { kPhS = 0, kPhU0 = 1, kPhU1 = 2, kPhLow = 3, kPhUK = 4 };
+
+// (phase, x, byte) -> ob (the columns, first in bit 15) | len << 16 | (dx + 8) << 21 | phase << 26
+__device__ uint32_t nib_entry(uint32_t idx) {
+  const uint32_t nib = idx % kStepVals, xi = (idx / kStepVals) % kNibXN;
+  uint32_t ph = idx / kStepVals / kNibXN;
+  int x = (int)xi + kNibXLo, dx = 0;
+  uint32_t ob = 0, len = 0;
+  for (int i = 0; i < (int)kStepBits; ++i) {
+    const uint32_t bit = (nib >> (kStepBits - 1 - i)) & 1u;
+    if (ph == kPhS) {
+      if (x > 0) {  // k = 1: the low bit (its value in zero columns)
+        len += bit;
+        x += (int)bit;
+        dx += (int)bit;
+        ph = kPhU1;
+        continue;
+      }
+      ph = kPhU0;
+    }
+    if (bit == 0) {
+      const int z = ph == kPhU1 ? 2 : 1;
+      len += (uint32_t)z;
+      x += z;
+      dx += z;
+    } else {
+      ob |= (1u << (2 * kStepBits - 1)) >> len;
+      ++len;
+      --x;
+      --dx;
+      ph = kPhS;
+    }
+  }
+  return ob | len << 16 | (uint32_t)(dx + 8) << 21 | ph << 26;
+}
+
+__global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
+  __shared__ uint32_t tab[kNibTab];
+  for (uint32_t i = threadIdx.x; i < kNibTab; i += blockDim.x) tab[i] = nib_entry(i);
+  __syncthreads();
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool inrow = id < (uint64_t)a.rows * a.nplanes;
+  const uint32_t plane = inrow ? (uint32_t)(id / a.rows) : 0, row = inrow ? (uint32_t)(id % a.rows) : 0;
+  const uint64_t* st = plane_stream(a, plane);
+  bool over = false;
+  const uint64_t maxw = inrow ? plane_words(a, plane, over) : 0;
+  const uint64_t G = inrow ? a.index[2 * id] : 0, O = inrow ? a.index[2 * id + 1] : 0;
+  const uint64_t E = !inrow ? 0 : row + 1 < a.rows ? a.index[2 * id + 2] : a.plane_bits[plane];
+  uint64_t* dst = a.out + ((uint64_t)plane * a.rows + row) * a.wpr;
+  bool bad = inrow && (over || E < G + 1);  // every row has at least its end-of-row codeword
+  const uint64_t len = bad ? 0 : E - G;
+  bool live = inrow && !bad;
+  const uint32_t cols = a.cols;
+  const bool pred = a.predict != 0;
+  const uint64_t p00 = (pred && row == 0 && a.p00 && a.p00[plane]) ? BIC_MSB : 0ull;
+  // stream: word q holds stream bits [64 q, 64 q + 64) of the plane; the row's chunk c is the 64
+  // bits from G + 64 c
+  const uint64_t q0 = G >> 6;
+  const uint32_t off = (uint32_t)(G & 63);
+  // raw stream words (byte-swapped and cut at the plane's end only when used, so that no wait
+  // for a load sits next to it); lanes without a stream read word 0 of the buffer
+  const uint64_t* sp = live && maxw ? st : a.streams;
+  const uint64_t lastw = live && maxw ? maxw - 1 : 0;
+  auto ld = [&](uint64_t i) -> uint64_t { return sp[min(i, lastw)]; };
+  auto word = [&](uint64_t raw, uint64_t i) -> uint64_t { return i < maxw && live ? bswap64(raw) : 0ull; };
+  uint64_t wa = ld(q0), wb = ld(q0 + 1), wc = ld(q0 + 2);
+  // machine state
+  uint32_t ph = kPhS, j = 0, n = (uint32_t)(O + row), kk = 0, r = 0, low = 0, z = 0;
+  int x = (int)((uint64_t)row * cols - O) - (int)n;
+  uint64_t acc = 0;                // output word j >> 6 being filled (residual bits, MSB-first)
+  uint32_t ow = 0, carry = 0;      // its index; the prefix-XOR parity of the words before it
+  uint64_t d0 = 0, d1 = 0;         // finished words not yet stored: words pw, pw + 1 (nd of them)
+  uint32_t nd = 0, pw = 0;
+  auto store_word = [&](uint64_t v, uint32_t w) {  // word w of the row, in order: as D when predicting
+    if (pred) {
+      if (row == 0 && w == 0) v = (v & ~BIC_MSB) | p00;  // R(0, 0) -> P(0, 0)
+      v ^= v >> 1;
+      v ^= v >> 2;
+      v ^= v >> 4;
+      v ^= v >> 8;
+      v ^= v >> 16;
+      v ^= v >> 32;  // bit j (MSB-first) = XOR of the word's bits 0..j
+      const uint32_t par = (uint32_t)(v & 1ull);
+      if (carry) v = ~v;
+      carry ^= par;
+    }
+    if (w == a.used - 1) v &= a.trail;
+    dst[w] = v;
+  };
+  auto finish_word = [&]() {  // word ow complete -> d0 / d1 (stored at the chunk boundary)
+    if (ow < a.used) {
+      if (nd == 2) {  // (only after long zero runs: k >= 2 codewords)
+        store_word(d0, pw++);
+        d0 = d1;
+        nd = 1;
+      }
+      if (nd == 0) {
+        d0 = acc;
+        pw = ow;
+      } else {
+        d1 = acc;
+      }
+      ++nd;
+    }
+    ++ow;
+    acc = 0;
+  };
+  auto put_one = [&](uint32_t c) {  // residual 1 at column c >= j
+    while ((c >> 6) > ow) finish_word();
+    acc |= BIC_MSB >> (c & 63);
+  };
+  uint64_t bitpos = 0;  // stream bits of the row consumed
+  // the general machine, one stream bit
+  auto slow_bit = [&](uint32_t bit) {
+    ++bitpos;
+    if (ph == kPhS) {
+      const uint32_t k = golomb_k_state(n, (uint32_t)(x + (int)n));
+      if (k == 1) {
+        j += bit;
+        x += (int)bit;
+        ph = kPhU1;
+        return;
+      }
+      if (k == 0) {
+        ph = kPhU0;
+      } else {
+        kk = k;
+        r = k;
+        low = 0;
+        ph = kPhLow;
+      }
+    }
+    if (ph == kPhLow) {
+      low = (low << 1) | bit;
+      if (--r == 0) {
+        ph = kPhUK;
+        z = 0;
+      }
+      return;
+    }
+    if (bit == 0) {
+      if (ph == kPhUK) {
+        if (++z > cols) bad = true;
+      } else {
+        const uint32_t dz = ph == kPhU1 ? 2u : 1u;
+        j += dz;
+        x += (int)dz;
+      }
+      if (j > cols) bad = true;
+      return;
+    }
+    // the codeword's '1': its residual 1 (or the end of the row) at column c
+    uint32_t c = j;
+    if (ph == kPhUK) {
+      const uint64_t s = ((uint64_t)z << kk) | low;
+      if (j + s > cols) {
+        bad = true;
+        return;
+      }
+      c = j + (uint32_t)s;
+      x += (int)s;
+    }
+    ph = kPhS;
+    ++n;
+    --x;
+    if (c == cols) {  // the end-of-row codeword
+      live = false;
+      if (bitpos != len) bad = true;
+      return;
+    }
+    put_one(c);
+    j = c + 1;
+  };
+  for (uint64_t c = 0;; ++c) {
+    if (!__ballot(live && !bad)) break;
+    // this chunk's 64 stream bits; the word after next loaded now, needed a chunk later
+    const uint64_t xa = word(wa, q0 + c), xb = word(wb, q0 + c + 1);
+    const uint64_t v = off ? (xa << off) | (xb >> (64 - off)) : xa;
+    wa = wb;
+    wb = wc;
+    wc = ld(q0 + c + 3);
+#pragma unroll 2
+    for (int i = 0; i < (int)(64 / kStepBits); ++i) {
+      if (live && !bad) {
+        const uint32_t nib = (uint32_t)(v >> (64 - kStepBits * (i + 1))) & (kStepVals - 1);
+        if (ph <= kPhU1 && n > 0 && x + 2 * (int)kStepBits <= (int)n && j + 2 * kStepBits <= cols) {
+          const int xc = min(max(x, kNibXLo), kNibXLo + kNibXN - 1);
+          const uint32_t e = tab[(ph * kNibXN + (uint32_t)(xc - kNibXLo)) * kStepVals + nib];
+          const uint32_t ob = e & 0xffffu, l = (e >> 16) & 31u;
+          const uint32_t pos = j & 63;
+          acc |= ((uint64_t)ob << 48) >> pos;
+          if (pos + l >= 64) {
+            const uint64_t spill = pos ? ((uint64_t)ob << 48) << (64 - pos) : 0ull;
+            finish_word();
+            acc = spill;
+          }
+          j += l;
+          n += (uint32_t)__popc(ob);
+          x += (int)((e >> 21) & 31u) - 8;
+          ph = (e >> 26) & 3u;
+          bitpos += kStepBits;
+        } else {
+#pragma unroll 1
+          for (int b = kStepBits - 1; b >= 0; --b)
+            if (live && !bad) slow_bit((nib >> b) & 1u);
+        }
+      }
+    }
+    if (live && bitpos > len) bad = true;
+    // the chunk's finished words
+    if (nd > 0) store_word(d0, pw);
+    if (nd > 1) store_word(d1, pw + 1);
+    nd = 0;
+  }
+  if (inrow) {
+    while (ow < a.used) finish_word();  // the last (partial) word and any zero words after it
+    if (nd > 0) store_word(d0, pw);
+    if (nd > 1) store_word(d1, pw + 1);
+    for (uint32_t w = a.used; w < a.wpr; ++w) dst[w] = 0;  // pad words
+    if (bad) atomicOr(&a.flags[1], 2u);                     // malformed stream (bic_sync: BIC_EDATA)
+  }
+}
+
 // EG: the row holding each plane's first residual 1 = the first row whose cols + 1 bits at the
 // unshifted offset row * (cols + 1) are not all '1' (rows before it are ~0 and their '1').
 __global__ __launch_bounds__(256) void k_dec_eg_first(DecArgs a) {
@@ -388,7 +628,11 @@ void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t s
   const uint64_t nrows = (uint64_t)rows * nplanes;
   const uint32_t grid = (uint32_t)((nrows + 3) / 4);
   if (coder == 0) {
+#ifdef BIC_DEC_LANES
     k_dec_golomb_lanes<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
+#else
+    k_dec_golomb_nib<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
+#endif
   } else {
     (void)hipMemsetAsync(a.first_row, 0xff, (size_t)nplanes * 4, s);
     k_dec_eg_first<<<grid, 256, 0, s>>>(a);

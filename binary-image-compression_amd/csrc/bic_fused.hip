@@ -636,6 +636,7 @@ struct FusedArgs {
   uint64_t* off_e;
   uint64_t* index;  // FusedScratch::index
   bool atom;        // FusedScratch::atom (staged encoder): shared words OR'd into pre-zeroed stream words
+  uint64_t eg_cp;   // FusedScratch::eg_cp: the count pass wrote the EG rows' inner words (plane stride, words)
 #ifdef BIC_STAMPS
   int known;
   int dbg;  // diagnostic (BIC_EMIT_DBG): k_emit_known skips 1 = LDS-image Golomb rows, 2 = EG rows, 4 = k = 0 copies
@@ -1132,6 +1133,44 @@ __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geo
   }
 }
 
+// The words of an EG row (after the plane's first 1) that the count pass leaves out when it wrote
+// the rest (k_gray_strips, EGW): with g = Ge % 64 != 0, the word across each strip edge (plain store)
+// and the row's first and last words (shared with the neighbouring rows: to the fragment table, or
+// OR'd into the words the prefix kernels zeroed; a last word the row fills, g = 63, is its own);
+// with g = 0 only the end-of-row '1' that opens the next word. Lane 0's work, from the edge lanes'
+// words.
+template <int WPL>
+__device__ __forceinline__ void eg_row_edges(const uint64_t (&rr)[WPL], const Geom& g, uint64_t Ge, uint64_t* out,
+                                             uint64_t* frag) {
+  const uint32_t sh = (uint32_t)(Ge & 63);
+  const uint64_t w0 = Ge >> 6;
+  const uint32_t nt = g.used / 64;  // whole strips (gray_eg_supported)
+  uint64_t last = 0;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    if (t >= (int)nt) break;
+    const uint64_t x = rr[t];
+    const uint64_t e0 = ~(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), 0) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 0));
+    if (sh && lane_id() == 0) {
+      if (t == 0) put_shared(out, w0, frag, 0, e0 >> sh);
+      else out[w0 + 64 * t] = bswap64((last << (64 - sh)) | (e0 >> sh));
+    }
+    last = ~lane63_u64(x);
+  }
+  if (lane_id() == 0) {
+    const uint64_t v = sh ? (last << (64 - sh)) | (BIC_MSB >> sh) : BIC_MSB;
+    if (sh == 63) out[w0 + g.used] = bswap64(v);  // the row ends with the word: not shared, not zeroed
+    else put_shared(out, w0 + g.used, frag, 1, v);
+  }
+}
+
+// whether the count pass's EG words of this plane lie where the row offsets say (every earlier plane
+// of a packed stream held a residual 1; slot mode: always)
+__device__ __forceinline__ bool eg_base_ok(const FusedArgs& a, uint32_t plane) {
+  return !a.ebase || a.ebase[plane] == (uint64_t)plane * a.eg_cp * 64;
+}
+
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * kWin];
@@ -1579,7 +1618,9 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
       const uint64_t cap = a.slot_e * 64;
       const uint64_t Ge = (a.ebase ? a.ebase[plane] : (uint64_t)plane * cap) + Ge_rel;
       if (Ge_rel + Le <= cap) {
-        if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
+        if (a.eg_cp && O > 0 && eg_base_ok(a, plane))
+          eg_row_edges<WPL>(rr, g, Ge, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
+        else if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
         if (lane == 0) {
           a.eboff[id] = Ge;
           a.elen[id] = Le;
@@ -1800,7 +1841,7 @@ __global__ __launch_bounds__(256) void k_shift_gboff(FusedArgs a) {
     const uint32_t onext = row + 1 < a.g.rows ? a.row_o[id + 1] : (uint32_t)a.pones[plane];
     const uint64_t Ge_rel = (uint64_t)row * (a.g.cols + 1) + (O > 0 ? 1 : 0);
     const uint64_t Le = (uint64_t)a.g.cols + 1 + (O == 0 && onext > 0 ? 1 : 0);
-    if (Ge_rel + Le <= a.slot_e * 64) zero_shared(a.out_e, a.ebase[plane] * 64 + Ge_rel, Le);
+    if (Ge_rel + Le <= a.slot_e * 64) zero_shared(a.out_e, a.ebase[plane] + Ge_rel, Le);
   }
 }
 
@@ -1923,6 +1964,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   a.ebase = a.off_e ? fs.ebase : nullptr;
   a.index = out_g ? fs.index : nullptr;
   a.atom = fs.atom && mode == kEncStaged;
+  a.eg_cp = mode == kEncStaged && out_e ? fs.eg_cp : 0;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
   a.dbg = getenv("BIC_EMIT_DBG") ? atoi(getenv("BIC_EMIT_DBG")) : 0;

@@ -137,6 +137,10 @@ struct FusedScratch {
   // staged encoder with output: the prefix kernels zero the stream words rows share and the
   // emission launches OR their parts into them (no fragment table, no fixup launch)
   bool atom = false;
+  // the count pass (launch_gray_rows with out_e) already wrote the EG words inside every row at
+  // plane stride eg_cp words, laid out as if every plane held a residual 1; the emission then writes
+  // only the words at strip edges and row ends of rows after the plane's first 1 (0: off)
+  uint64_t eg_cp = 0;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
@@ -166,7 +170,9 @@ uint32_t gray_strips(const Geom& g);
 // wanted; the encoder then reads R with predict off), not the bitplanes P
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero,
-                      bool store_resid = false);
+                      bool store_resid = false, uint64_t* out_e = nullptr, uint64_t eg_stride = 0);
+// the count pass can write the EG interior words (FusedScratch::eg_cp): rows of whole strips only
+bool gray_eg_supported(const Geom& g);
 
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
                          uint32_t W, uint32_t* besti, uint32_t* bestj, uint32_t* bestd);

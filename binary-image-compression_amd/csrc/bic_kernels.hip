@@ -533,11 +533,17 @@ constexpr bool kGrayPipe = BIC_GRAY_PIPE != 0;
 #define BIC_GRAY_PREFETCH 1
 #endif
 constexpr bool kGrayPrefetch = BIC_GRAY_PREFETCH != 0;  // the next row's pixels loaded during this row
-template <bool PREDICT, bool FULL, bool STORE_R, bool NP8>
+// EGW (FULL strips of a row of whole strips): the EG words inside the row (eg.cpp:20-37: ~R then the
+// row's '1'), at the offsets every row after the plane's first 1 has -- row r at bit r (cols + 1) + 1
+// of plane b's stream at word b * eg_stride (eg_base_ok). A lane forms the stream word that starts
+// inside its own row word from it and lane l + 1's: the words across strip edges and the row's first
+// and last words are the emission's (eg_row_edges), as are whole rows up to the plane's first 1.
+template <bool PREDICT, bool FULL, bool STORE_R, bool NP8, bool EGW>
 __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray, size_t pitch, const Geom& g,
                                                 uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
                                                 uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
-                                                int4* __restrict__ krec, uint32_t* __restrict__ kpos, uint32_t* tw) {
+                                                int4* __restrict__ krec, uint32_t* __restrict__ kpos, uint32_t* tw,
+                                                uint64_t* __restrict__ out_e, uint64_t eg_stride) {
   const int lane = lane_id();
   const int np = NP8 ? 8 : (int)g.nplanes;
   const uint32_t w = s * 64 + lane;
@@ -586,6 +592,10 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
     uint64_t pw[8];
     gray_to_planes<FULL>(cur, pw, mask);
     uint32_t* tb = kGrayPipe ? tw + (r & 1) * 1024 : tw;
+    // EG: the strip's first row bit (wave-uniform shift; lane l's word starts 64 l bits later)
+    const uint64_t ep = (uint64_t)row * (g.cols + 1) + (row ? 1u : 0u) + (uint64_t)s * 4096;
+    const uint32_t esh = (uint32_t)(ep & 63);
+    uint64_t* eo = out_e + (ep >> 6) + lane;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       if (!NP8 && b >= np) break;
@@ -599,6 +609,16 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
         up[b] = pw[b];
       }
       if (STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = R;
+      if constexpr (EGW && FULL) {
+        const uint64_t E = ~R;
+        if (esh == 0) {
+          eo[(uint64_t)b * eg_stride] = bswap64(E);
+        } else {
+          const uint64_t En = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(E >> 32), 0x130, 0xf, 0xf, true) << 32) |
+                              (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)E, 0x130, 0xf, 0xf, true);
+          if (lane != 63) eo[(uint64_t)b * eg_stride + 1] = bswap64((E << (64 - esh)) | (En >> esh));
+        }
+      }
       strip_word_put(tb, b, R, (int32_t)(w * 64));
     }
     if constexpr (kGrayPipe) {
@@ -630,11 +650,12 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
 #ifndef BIC_GRAY_WAVES
 #define BIC_GRAY_WAVES 4
 #endif
-template <bool PREDICT, bool STORE_R>
+template <bool PREDICT, bool STORE_R, bool EGW>
 __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
                                                         uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
-                                                        uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero) {
+                                                        uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero,
+                                                        uint64_t* __restrict__ out_e, uint64_t eg_stride) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][kGrayPipe ? 2048 : 1024];  // strip_word_put tables
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   uint32_t* tw = tab[threadIdx.x >> 6];
@@ -644,12 +665,17 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
   if (r0 >= g.rows) return;  // whole wave
   // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
   if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
-    gray_strip_rows<PREDICT, true, STORE_R, true>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+    gray_strip_rows<PREDICT, true, STORE_R, true, EGW>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw,
+                                                       out_e, eg_stride);
   else if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
-    gray_strip_rows<PREDICT, true, STORE_R, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
-  else
-    gray_strip_rows<PREDICT, false, STORE_R, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw);
+    gray_strip_rows<PREDICT, true, STORE_R, false, EGW>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw,
+                                                        out_e, eg_stride);
+  else if constexpr (!EGW)  // (EGW launches have whole strips only: gray_eg_supported)
+    gray_strip_rows<PREDICT, false, STORE_R, false, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
+                                                           tw, nullptr, 0);
 }
+
+bool gray_eg_supported(const Geom& g) { return g.trail == ~0ull && g.used % 64 == 0; }
 
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes) {
   return g.used <= 256 && pitch % 16 == 0 && pitch >= (size_t)g.used * 64 &&
@@ -657,13 +683,19 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
 }
 
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
-                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero, bool store_resid) {
+                      uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero, bool store_resid,
+                      uint64_t* out_e, uint64_t eg_stride) {
   const uint32_t ns = gray_strips(g);
   const uint64_t waves = (uint64_t)(g.rows + kGrayRows - 1) / kGrayRows * ns;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
-#define BIC_GS(P, R) k_gray_strips<P, R><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero)
-  if (predict) { if (store_resid) BIC_GS(true, true); else BIC_GS(true, false); }
-  else BIC_GS(false, false);  // without prediction R = P
+  const bool egw = out_e && gray_eg_supported(g);
+#define BIC_GS(P, R, E) \
+  k_gray_strips<P, R, E><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero, \
+                                                 out_e, eg_stride)
+#define BIC_GS2(P, R) { if (egw) BIC_GS(P, R, true); else BIC_GS(P, R, false); }
+  if (predict) { if (store_resid) BIC_GS2(true, true) else BIC_GS2(true, false) }
+  else BIC_GS2(false, false)  // without prediction R = P
+#undef BIC_GS2
 #undef BIC_GS
 }
 

@@ -352,6 +352,37 @@ def test_encode_gray_packed(ctx, oracle, staged, plane0, nplanes):
         assert as_u64(out)[:eoff[-1]].tobytes() == exp
 
 
+@pytest.mark.parametrize("rows", [45, 64, 127])
+@pytest.mark.parametrize("cols", [4096, 8192])
+def test_encode_gray_blank_plane(ctx, oracle, staged, rows, cols):
+    """a plane without a residual 1 among planes that have one: its EG stream is one bit shorter, so
+    in the packed buffer the later planes start a word earlier when rows (cols + 1) % 64 == 0 --
+    where the count pass's EG words (written at the offsets of planes that hold a 1) must all be
+    replaced; rows >= 64 also give rows whose EG offset is word-aligned"""
+    img = _gray(oracle, 3 * rows + cols, rows, cols, "uniform")
+    img &= 0xEF  # one blank plane
+    img[: rows // 3] &= 0x7F  # and the top plane's first 1 a third of the way down
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    P = oracle.bitplanes(img, 8)
+    wide = (ctx.slot_words(rows, cols, 0), ctx.slot_words(rows, cols, 1) + 5)  # EG slots longer than a stream
+    for pred in (1, 0):
+        for store, slots in ((False, (None, None)), (True, (None, None)), (False, wide)):
+            _, (og, bg), (oe, be) = ctx.encode_gray(g, predict=bool(pred), store_planes=store, slots=slots)
+            ctx.sync()
+            for k in range(8):
+                for coder, out, bits in ((0, og, bg), (1, oe, be)):
+                    eb, est, _ = oracle.encode_plane(P[k], cols, pred, coder)
+                    assert int(as_u64(bits)[k]) == eb, (pred, store, k, coder)
+                    assert stream_bytes(out[k], eb) == est.tobytes(), (pred, store, k, coder)
+    for store in (False, True):
+        _, (og, bg, fg), (oe, be, fe) = ctx.encode_gray_packed(g, store_planes=store)
+        ctx.sync()
+        for coder, out, off in ((0, og, fg), (1, oe, fe)):
+            exp, eoff = _packed_expect(oracle, P, cols, 1, coder)
+            assert list(as_u64(off)) == eoff, (store, coder)
+            assert as_u64(out)[:eoff[-1]].tobytes() == exp, (store, coder)
+
+
 @pytest.mark.parametrize("rows,cols,wpr", [(37, 4096, 72), (33, 3968, 64), (19, 4000, 63), (50, 256, 4)])
 @pytest.mark.parametrize("p", [0.5, 0.05])
 def test_narrow_rows_pitched(ctx, oracle, rows, cols, wpr, p):
