@@ -24,6 +24,7 @@
 namespace bic {
 
 constexpr uint32_t kDecRowWords = 256;  // cols <= 16384 (the EG row kernel's four words per lane)
+constexpr uint32_t kColChunk = 64;       // unmed's column scan: rows per chunk
 
 struct DecArgs {
   uint32_t rows, cols, wpr, used, nplanes;
@@ -38,6 +39,9 @@ struct DecArgs {
   uint64_t* out;              // [nplanes][rows][wpr]
   uint32_t* flags;
   int predict;
+  // unmed's column chunk totals (k_col_chunks' output), formed by the Golomb row kernel itself when
+  // a wave's 64 rows are one column chunk of one plane (rows % kColChunk == 0); null otherwise
+  uint64_t* ctot;
 };
 
 __device__ __forceinline__ const uint64_t* plane_stream(const DecArgs& a, uint32_t plane) {
@@ -219,8 +223,7 @@ __global__ __launch_bounds__(256) void k_dec_golomb_lanes(DecArgs a) {
 }
 
 // Golomb, byte machine: still one lane per row, but every lane consumes its stream 8 bits per
-// step, so the stream words are needed on a uniform cadence (one 64-bit view per 8 steps, the next
-// word loaded a chunk ahead) and a step is one table lookup instead of a codeword's serial chain.
+// step from one table lookup, instead of a codeword's serial chain per codeword.
 // The state between steps: the phase (S: at a codeword start, U0 / U1: inside the unary part of a
 // k = 0 / k = 1 codeword, and LOW / UK: the binary / unary part of a k >= 2 codeword), the column
 // j of the next residual bit, n (samples so far, Golomb.h's N) and x = A - n (A counted bit by bit:
@@ -229,15 +232,24 @@ __global__ __launch_bounds__(256) void k_dec_golomb_lanes(DecArgs a) {
 // by at most +16 over them; the decisions inside 8 bits are the same for every x <= -5 and for every
 // x >= 5 (checked exhaustively), so one table entry per (phase, x clamped to [-5, 5], byte) gives
 // the step: the residual columns it produces (<= 16), dx and the phase after. Other steps (n = 0,
-// k >= 2, the row's last columns) go bit by bit through the general machine. The output words are
-// held in registers and stored at the chunk boundaries, so a wave's only memory waits there are
-// for the stream word loaded a chunk earlier.
+// k >= 2, the row's last columns) go bit by bit through the general machine.
+// The stream is read in blocks of 4 x 64 bits per lane. When every lane of the wave can take table
+// steps for the whole block (n > 0, x + 512 <= n), the wave runs the block's 32 steps without
+// per-step tests: four steps' columns (<= 64) are gathered in one register and placed once, and
+// the (at most one) word each placement finishes is kept for the next block, whose start stores
+// them -- right after the block's loads were waited for at the previous block's end, so no wait
+// ever covers a young store. A lane stops before the byte holding its row's last stream bit and
+// reads that byte through the general machine, which ends the row exactly at its stream's end.
+// Other blocks (a plane's first row, k >= 2) step with per-step tests and store words as they
+// finish.
 constexpr int kNibXLo = -5, kNibXN = 11;
 constexpr uint32_t kStepBits = 8, kStepVals = 1u << kStepBits;
 constexpr uint32_t kNibTab = 3 * kNibXN * kStepVals;
 enum : uint32_t { kPhS = 0, kPhU0 = 1, kPhU1 = 2, kPhLow = 3, kPhUK = 4 };
+constexpr int kBlkSteps = 32;  // 4 chunks of 8 steps
 
-// (phase, x, byte) -> ob (the columns, first in bit 15) | len << 16 | (dx + 8) << 21 | phase << 26
+// (phase, x, byte) at index (phase * 11 + x + 5) * 256 + byte -> len | (dx + 8) << 6 | (phase' * 11) << 11 |
+// columns << 16 (the step's residual bits, first in bit 31)
 __device__ uint32_t nib_entry(uint32_t idx) {
   const uint32_t nib = idx % kStepVals, xi = (idx / kStepVals) % kNibXN;
   uint32_t ph = idx / kStepVals / kNibXN;
@@ -261,20 +273,28 @@ __device__ uint32_t nib_entry(uint32_t idx) {
       x += z;
       dx += z;
     } else {
-      ob |= (1u << (2 * kStepBits - 1)) >> len;
+      ob |= 0x8000u >> len;
       ++len;
       --x;
       --dx;
       ph = kPhS;
     }
   }
-  return ob | len << 16 | (uint32_t)(dx + 8) << 21 | ph << 26;
+  return len | (uint32_t)(dx + 8) << 6 | (ph * kNibXN) << 11 | ob << 16;
 }
 
+#ifndef BIC_DEC_BLOCKS
+#define BIC_DEC_BLOCKS 1
+#endif
+constexpr bool kDecBlocks = BIC_DEC_BLOCKS != 0;  // the all-lanes block path (else per-step tests always)
 __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
   __shared__ uint32_t tab[kNibTab];
+  __shared__ uint64_t csum[4][kDecRowWords];  // per wave: the XOR of its rows' D words (a.ctot)
   for (uint32_t i = threadIdx.x; i < kNibTab; i += blockDim.x) tab[i] = nib_entry(i);
+  if (a.ctot)
+    for (uint32_t i = threadIdx.x; i < 4 * kDecRowWords; i += blockDim.x) (&csum[0][0])[i] = 0;
   __syncthreads();
+  uint64_t* cs = csum[threadIdx.x >> 6];
   const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const bool inrow = id < (uint64_t)a.rows * a.nplanes;
   const uint32_t plane = inrow ? (uint32_t)(id / a.rows) : 0, row = inrow ? (uint32_t)(id % a.rows) : 0;
@@ -286,28 +306,26 @@ __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
   uint64_t* dst = a.out + ((uint64_t)plane * a.rows + row) * a.wpr;
   bool bad = inrow && (over || E < G + 1);  // every row has at least its end-of-row codeword
   const uint64_t len = bad ? 0 : E - G;
-  bool live = inrow && !bad;
+  bool live = inrow && !bad;  // still decoding (false once the row ended or the stream is malformed)
   const uint32_t cols = a.cols;
   const bool pred = a.predict != 0;
   const uint64_t p00 = (pred && row == 0 && a.p00 && a.p00[plane]) ? BIC_MSB : 0ull;
   // stream: word q holds stream bits [64 q, 64 q + 64) of the plane; the row's chunk c is the 64
-  // bits from G + 64 c
+  // bits from G + 64 c. Raw words (byte-swapped and cut at the plane's end only when used); lanes
+  // without a stream read word 0 of the buffer.
   const uint64_t q0 = G >> 6;
   const uint32_t off = (uint32_t)(G & 63);
-  // raw stream words (byte-swapped and cut at the plane's end only when used, so that no wait
-  // for a load sits next to it); lanes without a stream read word 0 of the buffer
   const uint64_t* sp = live && maxw ? st : a.streams;
   const uint64_t lastw = live && maxw ? maxw - 1 : 0;
   auto ld = [&](uint64_t i) -> uint64_t { return sp[min(i, lastw)]; };
   auto word = [&](uint64_t raw, uint64_t i) -> uint64_t { return i < maxw && live ? bswap64(raw) : 0ull; };
-  uint64_t wa = ld(q0), wb = ld(q0 + 1), wc = ld(q0 + 2);
   // machine state
   uint32_t ph = kPhS, j = 0, n = (uint32_t)(O + row), kk = 0, r = 0, low = 0, z = 0;
   int x = (int)((uint64_t)row * cols - O) - (int)n;
-  uint64_t acc = 0;                // output word j >> 6 being filled (residual bits, MSB-first)
-  uint32_t ow = 0, carry = 0;      // its index; the prefix-XOR parity of the words before it
-  uint64_t d0 = 0, d1 = 0;         // finished words not yet stored: words pw, pw + 1 (nd of them)
-  uint32_t nd = 0, pw = 0;
+  uint64_t acc = 0;            // output word j >> 6 being filled (residual bits, MSB-first)
+  uint32_t ow = 0, carry = 0;  // its index; the prefix-XOR parity of the words before it
+  uint32_t bitpos = 0;         // stream bits of the row consumed
+  bool done = false;           // the end-of-row codeword was read and the row's words stored
   auto store_word = [&](uint64_t v, uint32_t w) {  // word w of the row, in order: as D when predicting
     if (pred) {
       if (row == 0 && w == 0) v = (v & ~BIC_MSB) | p00;  // R(0, 0) -> P(0, 0)
@@ -321,32 +339,20 @@ __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
       if (carry) v = ~v;
       carry ^= par;
     }
+    if (w >= a.used) return;  // (a malformed stream's columns past the row)
     if (w == a.used - 1) v &= a.trail;
     dst[w] = v;
+    if (a.ctot) __hip_atomic_fetch_xor(cs + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   };
-  auto finish_word = [&]() {  // word ow complete -> d0 / d1 (stored at the chunk boundary)
-    if (ow < a.used) {
-      if (nd == 2) {  // (only after long zero runs: k >= 2 codewords)
-        store_word(d0, pw++);
-        d0 = d1;
-        nd = 1;
-      }
-      if (nd == 0) {
-        d0 = acc;
-        pw = ow;
-      } else {
-        d1 = acc;
-      }
-      ++nd;
-    }
+  auto finish_word = [&]() {  // word ow complete: stored now (the stepped path)
+    if (ow < a.used) store_word(acc, ow);
     ++ow;
     acc = 0;
   };
-  auto put_one = [&](uint32_t c) {  // residual 1 at column c >= j
-    while ((c >> 6) > ow) finish_word();
-    acc |= BIC_MSB >> (c & 63);
+  auto fail = [&]() {
+    bad = true;
+    live = false;
   };
-  uint64_t bitpos = 0;  // stream bits of the row consumed
   // the general machine, one stream bit
   auto slow_bit = [&](uint32_t bit) {
     ++bitpos;
@@ -377,13 +383,13 @@ __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
     }
     if (bit == 0) {
       if (ph == kPhUK) {
-        if (++z > cols) bad = true;
+        if (++z > cols) fail();
       } else {
         const uint32_t dz = ph == kPhU1 ? 2u : 1u;
         j += dz;
         x += (int)dz;
       }
-      if (j > cols) bad = true;
+      if (j > cols) fail();
       return;
     }
     // the codeword's '1': its residual 1 (or the end of the row) at column c
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
     if (ph == kPhUK) {
       const uint64_t s = ((uint64_t)z << kk) | low;
       if (j + s > cols) {
-        bad = true;
+        fail();
         return;
       }
       c = j + (uint32_t)s;
@@ -400,61 +406,169 @@ __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
     ph = kPhS;
     ++n;
     --x;
-    if (c == cols) {  // the end-of-row codeword
+    if (c == cols) {  // the end-of-row codeword: the row's last words
       live = false;
-      if (bitpos != len) bad = true;
+      if (bitpos != len) {
+        bad = true;
+        return;
+      }
+      while (ow < a.used) finish_word();
+      done = true;
       return;
     }
-    put_one(c);
+    while ((c >> 6) > ow) finish_word();
+    acc |= BIC_MSB >> (c & 63);
     j = c + 1;
   };
-  for (uint64_t c = 0;; ++c) {
-    if (!__ballot(live && !bad)) break;
-    // this chunk's 64 stream bits; the word after next loaded now, needed a chunk later
-    const uint64_t xa = word(wa, q0 + c), xb = word(wb, q0 + c + 1);
-    const uint64_t v = off ? (xa << off) | (xb >> (64 - off)) : xa;
-    wa = wb;
-    wb = wc;
-    wc = ld(q0 + c + 3);
-#pragma unroll 2
-    for (int i = 0; i < (int)(64 / kStepBits); ++i) {
-      if (live && !bad) {
-        const uint32_t nib = (uint32_t)(v >> (64 - kStepBits * (i + 1))) & (kStepVals - 1);
-        if (ph <= kPhU1 && n > 0 && x + 2 * (int)kStepBits <= (int)n && j + 2 * kStepBits <= cols) {
-          const int xc = min(max(x, kNibXLo), kNibXLo + kNibXN - 1);
-          const uint32_t e = tab[(ph * kNibXN + (uint32_t)(xc - kNibXLo)) * kStepVals + nib];
-          const uint32_t ob = e & 0xffffu, l = (e >> 16) & 31u;
-          const uint32_t pos = j & 63;
-          acc |= ((uint64_t)ob << 48) >> pos;
-          if (pos + l >= 64) {
-            const uint64_t spill = pos ? ((uint64_t)ob << 48) << (64 - pos) : 0ull;
-            finish_word();
-            acc = spill;
-          }
-          j += l;
-          n += (uint32_t)__popc(ob);
-          x += (int)((e >> 21) & 31u) - 8;
-          ph = (e >> 26) & 3u;
-          bitpos += kStepBits;
-        } else {
-#pragma unroll 1
-          for (int b = kStepBits - 1; b >= 0; --b)
-            if (live && !bad) slow_bit((nib >> b) & 1u);
-        }
+  auto tab_at = [&](uint32_t phk, int xv, uint32_t byte) -> uint32_t {  // phk = phase * 11
+    const uint32_t xc = (uint32_t)(min(max(xv, kNibXLo), kNibXLo + kNibXN - 1) - kNibXLo);
+    return tab[(phk + xc) * kStepVals + byte];
+  };
+  // one stepped-path step: a table step when this lane can take one, else 8 general steps
+  auto careful_step = [&](uint32_t byte) {
+    if (ph <= kPhU1 && n > 0 && x + 2 * (int)kStepBits <= (int)n && j + 2 * kStepBits <= cols) {
+      const uint32_t e = tab_at(ph * kNibXN, x, byte);
+      const uint32_t l = e & 31u;
+      const uint64_t obw = (uint64_t)(e & 0xffff0000u) << 32;
+      const uint32_t pos = j & 63;
+      acc |= obw >> pos;
+      if (pos + l >= 64) {
+        const uint64_t spill = pos ? obw << (64 - pos) : 0ull;
+        finish_word();
+        acc = spill;
       }
+      j += l;
+      n += (uint32_t)__popc(e >> 16);
+      x += (int)((e >> 6) & 31u) - 8;
+      ph = (((e >> 11) & 31u) * 3) >> 5;  // (phase * 11) -> phase
+      bitpos += kStepBits;
+    } else {
+#pragma unroll 1
+      for (int b = kStepBits - 1; b >= 0; --b)
+        if (live) slow_bit((byte >> b) & 1u);
     }
-    if (live && bitpos > len) bad = true;
-    // the chunk's finished words
-    if (nd > 0) store_word(d0, pw);
-    if (nd > 1) store_word(d1, pw + 1);
-    nd = 0;
+  };
+  // stream ring: A0..A4 = words q0 + 4 b .. q0 + 4 b + 4 of block b; B0..B3 the next block's words
+  // 5..8, loaded at the block start and moved into A at its end
+  uint64_t A0 = ld(q0), A1 = ld(q0 + 1), A2 = ld(q0 + 2), A3 = ld(q0 + 3), A4 = ld(q0 + 4);
+  uint64_t D0 = 0, D1 = 0, D2 = 0, D3 = 0, D4 = 0, D5 = 0, D6 = 0, D7 = 0;  // words a fast block finished
+  uint32_t dflags = 0, dbase = 0;  // which of D0..D7 hold a word; the first one's index
+  // the byte holding the row's last stream bit (its end-of-row '1'): the block steps stop before it
+  // and the general machine reads it, so the row ends exactly where its stream does
+  const uint32_t last_step = len ? (uint32_t)((len - 1) / kStepBits) : 0u;
+  for (uint64_t blk = 0;; ++blk) {
+    if (!__ballot(live)) break;
+    if (live && dflags) {  // the previous block's finished words, in order
+      uint32_t w = dbase;
+      if (dflags & 1u) store_word(D0, w++);
+      if (dflags & 2u) store_word(D1, w++);
+      if (dflags & 4u) store_word(D2, w++);
+      if (dflags & 8u) store_word(D3, w++);
+      if (dflags & 16u) store_word(D4, w++);
+      if (dflags & 32u) store_word(D5, w++);
+      if (dflags & 64u) store_word(D6, w++);
+      if (dflags & 128u) store_word(D7, w++);
+    }
+    dflags = 0;
+    const uint64_t cb = q0 + 4 * blk;
+    const uint64_t B0 = ld(cb + 5), B1 = ld(cb + 6), B2 = ld(cb + 7), B3 = ld(cb + 8);
+    const uint64_t x0 = word(A0, cb), x1 = word(A1, cb + 1), x2 = word(A2, cb + 2), x3 = word(A3, cb + 3),
+                   x4 = word(A4, cb + 4);
+    auto chunk_bits = [&](uint64_t lo, uint64_t hi) -> uint64_t { return off ? (lo << off) | (hi >> (64 - off)) : lo; };
+    const uint64_t v0 = chunk_bits(x0, x1), v1 = chunk_bits(x1, x2), v2 = chunk_bits(x2, x3), v3 = chunk_bits(x3, x4);
+    // the block's steps before the row's last byte (kBlkSteps: none of it in this block)
+    const uint64_t s0 = (uint64_t)kBlkSteps * blk;
+    const uint32_t stop = !live ? (uint32_t)kBlkSteps
+                                : last_step < s0 ? 0u : (uint32_t)min((uint64_t)kBlkSteps, (uint64_t)last_step - s0);
+    const bool bfast = !live || (ph <= kPhU1 && n > 0 && x + 16 * kBlkSteps <= (int)n);
+    if (kDecBlocks && __all(bfast)) {
+      // every lane: 8 groups of 4 table steps; each group's columns (<= 64) gathered in Q, then
+      // placed after acc (finishing at most one word: kept in D<g>). When a lane's last byte lies
+      // in this block (some lane's stop < 32: a wave-uniform choice), its steps from there on are
+      // void.
+      const bool ends = !__all(stop == (uint32_t)kBlkSteps);
+      uint32_t phk = ph * kNibXN;
+      dbase = ow;
+      auto group = [&](uint32_t half, uint64_t& Dg, uint32_t g) {
+        uint64_t Q = 0;
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t e = tab_at(phk, x, (half >> (24 - 8 * k)) & 255u);
+          const bool act = !ends || 4 * g + k < stop;
+          const uint64_t q = ((uint64_t)(e & 0xffff0000u) << 32) >> m;
+          Q |= act ? q : 0ull;
+          m += act ? e & 31u : 0u;
+          x += act ? (int)((e >> 6) & 31u) - 8 : 0;
+          phk = act ? (e >> 11) & 31u : phk;
+        }
+        const uint32_t pos = j & 63;
+        const uint64_t filled = acc | (Q >> pos);
+        const bool cross = pos + m >= 64;
+        Dg = filled;
+        dflags |= cross ? 1u << g : 0u;
+        acc = cross ? (pos ? Q << (64 - pos) : 0ull) : filled;
+        ow += cross ? 1u : 0u;
+        j += m;
+        n += (uint32_t)__popcll(Q);
+      };
+      group((uint32_t)(v0 >> 32), D0, 0);
+      group((uint32_t)v0, D1, 1);
+      group((uint32_t)(v1 >> 32), D2, 2);
+      group((uint32_t)v1, D3, 3);
+      group((uint32_t)(v2 >> 32), D4, 4);
+      group((uint32_t)v2, D5, 5);
+      group((uint32_t)(v3 >> 32), D6, 6);
+      group((uint32_t)v3, D7, 7);
+      ph = (phk * 3) >> 5;
+      bitpos += kStepBits * stop;
+      if (ends && live && stop < (uint32_t)kBlkSteps) {
+        // the lanes whose row ends here: their words so far, then the last byte bit by bit
+        uint32_t w = dbase;
+        if (dflags & 1u) store_word(D0, w++);
+        if (dflags & 2u) store_word(D1, w++);
+        if (dflags & 4u) store_word(D2, w++);
+        if (dflags & 8u) store_word(D3, w++);
+        if (dflags & 16u) store_word(D4, w++);
+        if (dflags & 32u) store_word(D5, w++);
+        if (dflags & 64u) store_word(D6, w++);
+        if (dflags & 128u) store_word(D7, w++);
+        dflags = 0;
+        const uint64_t vq = stop < 8 ? v0 : stop < 16 ? v1 : stop < 24 ? v2 : v3;
+        const uint32_t byte = (uint32_t)(vq >> (56 - 8 * (stop & 7))) & 255u;
+#pragma unroll 1
+        for (int b = kStepBits - 1; b >= 0; --b)
+          if (live) slow_bit((byte >> b) & 1u);
+        if (live) fail();  // no end-of-row codeword where the stream ends
+      }
+      if (live && bitpos > len) fail();
+    } else {
+      const uint64_t vs[4] = {v0, v1, v2, v3};
+#pragma unroll 1
+      for (int i = 0; i < kBlkSteps; ++i)
+        if (live) careful_step((uint32_t)(vs[i >> 3] >> (56 - 8 * (i & 7))) & 255u);
+      if (live && bitpos > len) fail();
+    }
+    A0 = A4;
+    A1 = B0;
+    A2 = B1;
+    A3 = B2;
+    A4 = B3;
   }
   if (inrow) {
-    while (ow < a.used) finish_word();  // the last (partial) word and any zero words after it
-    if (nd > 0) store_word(d0, pw);
-    if (nd > 1) store_word(d1, pw + 1);
+    if (!done)  // a malformed stream (flagged): the row's words are zeros
+      for (uint32_t w = 0; w < a.used; ++w) dst[w] = 0;
     for (uint32_t w = a.used; w < a.wpr; ++w) dst[w] = 0;  // pad words
     if (bad) atomicOr(&a.flags[1], 2u);                     // malformed stream (bic_sync: BIC_EDATA)
+  }
+  if (a.ctot && __ballot(inrow)) {  // the wave's chunk totals (its rows are chunk row / kColChunk)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t wid = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64 * 64;  // the wave's first row id
+    const uint32_t wplane = (uint32_t)(wid / a.rows), chunk = (uint32_t)(wid % a.rows) / kColChunk;
+    const uint32_t nch = a.rows / kColChunk;
+    for (uint32_t w = lane_id(); w < a.wpr; w += 64)
+      a.ctot[((uint64_t)wplane * nch + chunk) * a.wpr + w] = w < kDecRowWords ? cs[w] : 0ull;
   }
 }
 
@@ -549,7 +663,6 @@ __global__ __launch_bounds__(256) void k_dec_eg_rows(DecArgs a) {
 }
 
 // unmed, column part: P(i) = XOR of D(0..i) per word column, in chunks of kColChunk rows.
-constexpr uint32_t kColChunk = 64;
 __global__ __launch_bounds__(256) void k_col_chunks(const uint64_t* __restrict__ D, uint64_t* __restrict__ ctot,
                                                     uint32_t rows, uint32_t wpr, uint32_t nplanes) {
   const uint32_t nch = (rows + kColChunk - 1) / kColChunk;
@@ -564,20 +677,35 @@ __global__ __launch_bounds__(256) void k_col_chunks(const uint64_t* __restrict__
   for (uint32_t r = 0; r < nr; ++r) acc ^= p[(uint64_t)r * wpr];
   ctot[t] = acc;
 }
-__global__ __launch_bounds__(256) void k_col_scan(uint64_t* __restrict__ ctot, uint32_t rows, uint32_t wpr,
-                                                  uint32_t nplanes) {
+// the exclusive XOR scan over one word column's chunk totals: one workgroup per (plane, word), the
+// chunks 256 at a time (wave scans by shuffles, the waves' totals through LDS)
+__global__ __launch_bounds__(256) void k_col_scan_par(uint64_t* __restrict__ ctot, uint32_t rows, uint32_t wpr) {
+  __shared__ uint64_t wt[4];
   const uint32_t nch = (rows + kColChunk - 1) / kColChunk;
-  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (uint64_t)nplanes * wpr) return;
-  const uint32_t w = (uint32_t)(t % wpr), plane = (uint32_t)(t / wpr);
+  const uint32_t w = blockIdx.x % wpr, plane = blockIdx.x / wpr;
   uint64_t* p = ctot + (uint64_t)plane * nch * wpr + w;
-  uint64_t acc = 0;
-  for (uint32_t c = 0; c < nch; ++c) {  // exclusive
-    const uint64_t v = p[(uint64_t)c * wpr];
-    p[(uint64_t)c * wpr] = acc;
-    acc ^= v;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  uint64_t carry = 0;
+  for (uint32_t c0 = 0; c0 < nch; c0 += 256) {
+    const uint32_t c = c0 + threadIdx.x;
+    const uint64_t v = c < nch ? p[(uint64_t)c * wpr] : 0ull;
+    uint64_t x = v;  // inclusive XOR scan across the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = shfl_up_u64(x, d);
+      if (lane >= d) x ^= y;
+    }
+    if (lane == 63) wt[wv] = x;
+    __syncthreads();
+    uint64_t before = carry;
+    for (int u = 0; u < wv; ++u) before ^= wt[u];
+    const uint64_t all = wt[0] ^ wt[1] ^ wt[2] ^ wt[3];
+    __syncthreads();
+    if (c < nch) p[(uint64_t)c * wpr] = before ^ x ^ v;  // exclusive
+    carry ^= all;
   }
 }
+
 __global__ __launch_bounds__(256) void k_col_apply(uint64_t* __restrict__ D, const uint64_t* __restrict__ ctot,
                                                    uint32_t rows, uint32_t wpr, uint32_t nplanes) {
   const uint32_t nch = (rows + kColChunk - 1) / kColChunk;
@@ -627,7 +755,10 @@ void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t s
   a.first_row = reinterpret_cast<uint32_t*>(ctot + (uint64_t)nplanes * nch * wpr);
   const uint64_t nrows = (uint64_t)rows * nplanes;
   const uint32_t grid = (uint32_t)((nrows + 3) / 4);
+  a.ctot = nullptr;
+  const bool fused_chunks = coder == 0 && predict && rows % kColChunk == 0;
   if (coder == 0) {
+    if (fused_chunks) a.ctot = ctot;
 #ifdef BIC_DEC_LANES
     k_dec_golomb_lanes<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
 #else
@@ -640,8 +771,8 @@ void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t s
   }
   if (predict) {
     const uint64_t nt = (uint64_t)nplanes * nch * wpr;
-    k_col_chunks<<<(uint32_t)((nt + 255) / 256), 256, 0, s>>>(out, ctot, rows, wpr, nplanes);
-    k_col_scan<<<(uint32_t)(((uint64_t)nplanes * wpr + 255) / 256), 256, 0, s>>>(ctot, rows, wpr, nplanes);
+    if (!fused_chunks) k_col_chunks<<<(uint32_t)((nt + 255) / 256), 256, 0, s>>>(out, ctot, rows, wpr, nplanes);
+    k_col_scan_par<<<nplanes * wpr, 256, 0, s>>>(ctot, rows, wpr);
     k_col_apply<<<(uint32_t)((nt + 255) / 256), 256, 0, s>>>(out, ctot, rows, wpr, nplanes);
   }
 }
