@@ -660,7 +660,7 @@ class C5(C3):
 
     def step(self):
         c = self.ctx
-        self.res = c.patch_encode(self.planes[0], self.cols, self.W, self.lt, want_resid=True)
+        self.res = c.patch_encode(self.planes[0], self.cols, self.W, self.lt, want_resid=True, bufs=self.res)
         if self.world > 1:
             from pybic.parallel import sharded_golomb
             wts = self.res["weights"]

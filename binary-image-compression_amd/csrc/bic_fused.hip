@@ -643,6 +643,13 @@ struct FusedArgs {
 #endif
 };
 
+// A row's absolute Golomb bit offset: gboff holds it relative to the plane's slot start (LEN scan);
+// packed output moves the plane to its packed start word gbase[plane]
+__device__ __forceinline__ uint64_t gb_abs(const FusedArgs& a, uint64_t id, uint32_t plane) {
+  const uint64_t G = a.gboff[id];
+  return a.off_g ? G - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G;
+}
+
 // Global-memory emission for a row whose Golomb image does not fit the LDS window: codeword
 // bits landing in the row's first/last output word are kept for the fragment table, the rest
 // is OR'd into words this wave zeroed first.
@@ -694,7 +701,7 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
   const Geom& g = a.g;
   const uint64_t slow = a.gslow[id];
   const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
-  const uint64_t G = a.gboff[id], L = a.glen[id] & kLenMask;
+  const uint64_t G = gb_abs(a, id, plane), L = a.glen[id] & kLenMask;
   uint64_t* frag = a.gfrag + 2 * id;
   const uint64_t wh = G >> 6, wt = (G + L - 1) >> 6;
   const bool hpart = !word_complete(wh, G, L);
@@ -1333,6 +1340,38 @@ __device__ __forceinline__ void zero_shared(uint64_t* out, uint64_t G, uint64_t 
   if ((G + L) & 63) out[(G + L - 1) >> 6] = 0;
 }
 
+// Packed output: the planes' start words in each coder's buffer (streams word-aligned, plane order:
+// bic_pack_streams' layout) from the Golomb totals (LEN scan) and the EG lengths (rows (cols + 1), + 1
+// when the plane holds a residual 1: eg.cpp's first-run bit), each capped at the slot size so that an
+// overflowing plane (BIC_ENOSPC) cannot push a later one past the buffer. One workgroup.
+__device__ __forceinline__ void plane_bases(const FusedArgs& a, uint64_t* tmp) {
+  const Geom& g = a.g;
+  uint64_t cg = 0, ce = 0;  // running bases (words)
+  for (uint32_t q0 = 0; q0 < g.nplanes; q0 += 1024) {
+    const uint32_t q = q0 + threadIdx.x;
+    const bool in = q < g.nplanes;
+    uint64_t gw = 0, ew = 0;
+    if (in && a.off_g) gw = min((a.bits_g[q] + 63) / 64, a.slot_g);
+    if (in && a.off_e) ew = min(((uint64_t)g.rows * (g.cols + 1) + (a.pones[q] ? 1 : 0) + 63) / 64, a.slot_e);
+    uint64_t tg, te;
+    const uint64_t pg = block_excl_scan<uint64_t>(gw, tmp, tg) + cg;
+    const uint64_t pe = block_excl_scan<uint64_t>(ew, tmp, te) + ce;
+    if (in && a.off_g) {
+      a.off_g[q] = pg;
+      a.gbase[q] = pg;
+    }
+    if (in && a.off_e) {
+      a.off_e[q] = pe;
+      a.ebase[q] = pe * 64;
+    }
+    cg += tg;
+    ce += te;
+  }
+  if (threadIdx.x == 0) {
+    if (a.off_g) a.off_g[g.nplanes] = cg;
+    if (a.off_e) a.off_e[g.nplanes] = ce;
+  }
+}
 // Exclusive per-plane scan of per-row values. Each 1024-thread workgroup owns kScanChunk rows of a
 // plane (kScanPer consecutive rows per thread) and sums the plane's earlier rows itself (coalesced,
 // at most rows / 1024 loads per thread), so no workgroup waits on another and a plane spreads over
@@ -1434,6 +1473,10 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       const uint32_t r = r0 + i;
       if (r < g.rows) {
         a.gboff[base + r] = (uint64_t)plane * cap + pre;
+        if (a.index) {  // the decoders' row index (bic_row_index): slot-relative offset, 1s before the row
+          a.index[2 * (base + r)] = pre;
+          a.index[2 * (base + r) + 1] = a.row_o[base + r];
+        }
         if (pre + v[i] > cap) {
           a.glen[base + r] = 0;  // overflowed: nothing written, fixup skips
           atomicOr(&a.flags[0], 1u);
@@ -1536,7 +1579,10 @@ constexpr int kEmitWaves = 4;
 #define BIC_EMIT_PREFETCH 0  // measured slower (C3 emission 238 -> 248 us): off
 #endif
 constexpr bool kEmitPrefetch = BIC_EMIT_PREFETCH != 0;  // next row loaded during this one (no prediction)
-constexpr bool kRestAux = true;  // k_emit_rest on the context's second stream (beside k_emit_known)
+#ifndef BIC_REST_AUX
+#define BIC_REST_AUX 1
+#endif
+constexpr bool kRestAux = BIC_REST_AUX != 0;  // k_emit_rest on the context's second stream (beside k_emit_known)
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * kGImg];
@@ -1565,7 +1611,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
     row_load<WPL, false>(a.planes, g, fplane, frow, pp_, dummy);
     pO = a.row_o[fid];
     pLf = DO_G ? a.glen[fid] : 0;
-    pGb = DO_G ? a.gboff[fid] : 0;
+    pGb = DO_G ? gb_abs(a, fid, fplane) : 0;
   };
   if (kPre && id0 < nrows) fetch(id0);
   for (uint64_t id = id0; id < nrows; id += stride) {
@@ -1588,7 +1634,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
       row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
       O = a.row_o[id];
       Lf = DO_G ? a.glen[id] : 0;
-      Gb = DO_G ? a.gboff[id] : 0;  // loaded with the row, not after the branch that uses it
+      Gb = DO_G ? gb_abs(a, id, plane) : 0;  // loaded with the row, not after the branch that uses it
     }
     const uint64_t L = Lf & kLenMask;
     const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
@@ -1774,68 +1820,25 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
       }
       __syncthreads();
       if (threadIdx.x == 0 && tot != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-      write_row(gimg, L, a.gboff[id], -1, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id, threadIdx.x, blockDim.x);
+      write_row(gimg, L, gb_abs(a, id, plane), -1, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id, threadIdx.x,
+                blockDim.x);
     }
     __syncthreads();  // the images and sh are reused by the next row
   }
 }
 
-// Packed output: the planes' start words in each coder's buffer (streams word-aligned, plane order:
-// bic_pack_streams' layout) from the Golomb totals (LEN scan) and the EG lengths (rows (cols + 1), + 1
-// when the plane holds a residual 1: eg.cpp's first-run bit), each capped at the slot size so that an
-// overflowing plane (BIC_ENOSPC) cannot push a later one past the buffer. One workgroup.
 __global__ __launch_bounds__(1024) void k_plane_bases(FusedArgs a) {
   __shared__ uint64_t tmp[17];
-  const Geom& g = a.g;
-  uint64_t cg = 0, ce = 0;  // running bases (words)
-  for (uint32_t q0 = 0; q0 < g.nplanes; q0 += 1024) {
-    const uint32_t q = q0 + threadIdx.x;
-    const bool in = q < g.nplanes;
-    uint64_t gw = 0, ew = 0;
-    if (in && a.off_g) gw = min((a.bits_g[q] + 63) / 64, a.slot_g);
-    if (in && a.off_e) ew = min(((uint64_t)g.rows * (g.cols + 1) + (a.pones[q] ? 1 : 0) + 63) / 64, a.slot_e);
-    uint64_t tg, te;
-    const uint64_t pg = block_excl_scan<uint64_t>(gw, tmp, tg) + cg;
-    const uint64_t pe = block_excl_scan<uint64_t>(ew, tmp, te) + ce;
-    if (in && a.off_g) {
-      a.off_g[q] = pg;
-      a.gbase[q] = pg;
-    }
-    if (in && a.off_e) {
-      a.off_e[q] = pe;
-      a.ebase[q] = pe * 64;
-    }
-    cg += tg;
-    ce += te;
-  }
-  if (threadIdx.x == 0) {
-    if (a.off_g) a.off_g[g.nplanes] = cg;
-    if (a.off_e) a.off_e[g.nplanes] = ce;
-  }
+  plane_bases(a, tmp);
 }
 
-// The decoders' row index (bic_row_index): [2 id] = the row's Golomb bit offset in its plane's stream
-// (before the packed-output shift), [2 id + 1] = the plane's residual 1s before the row.
-__global__ __launch_bounds__(256) void k_row_index(FusedArgs a) {
-  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (id >= (uint64_t)a.g.rows * a.g.nplanes) return;
-  const uint32_t plane = (uint32_t)(id / a.g.rows);
-  a.index[2 * id] = a.gboff[id] - (uint64_t)plane * a.slot_g * 64;
-  a.index[2 * id + 1] = a.row_o[id];
-}
-
-// Packed Golomb output: every row's offset moves from its plane's slot to the plane's packed start.
-// With FusedScratch::atom the rows' shared words of both packed streams are zeroed here too (their
-// offsets are final only now).
+// Packed output with FusedScratch::atom: the rows' shared words of both packed streams are zeroed
+// here (their offsets are final only now).
 __global__ __launch_bounds__(256) void k_shift_gboff(FusedArgs a) {
   const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (id >= (uint64_t)a.g.rows * a.g.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.g.rows), row = (uint32_t)(id % a.g.rows);
-  if (a.off_g) {
-    const uint64_t G = a.gboff[id] - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64;
-    a.gboff[id] = G;
-    if (a.atom) zero_shared(a.out_g, G, a.glen[id] & kLenMask);  // (0 when the row overflowed)
-  }
+  if (a.off_g) zero_shared(a.out_g, gb_abs(a, id, plane), a.glen[id] & kLenMask);  // (0 when the row overflowed)
   if (a.off_e && a.atom) {
     const uint32_t O = a.row_o[id];
     const uint32_t onext = row + 1 < a.g.rows ? a.row_o[id + 1] : (uint32_t)a.pones[plane];
@@ -1851,23 +1854,27 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
                                                const uint64_t* __restrict__ frag, uint64_t* __restrict__ out,
                                                const uint64_t* __restrict__ boff2, const uint64_t* __restrict__ len2,
                                                const uint64_t* __restrict__ frag2, uint64_t* __restrict__ out2,
-                                               uint32_t rows, uint64_t nrows, uint32_t second) {
+                                               uint32_t rows, uint64_t nrows, uint32_t second,
+                                               const uint64_t* __restrict__ gbase = nullptr, uint64_t slot_bits = 0) {
   // blocks [second, ...) serve the second stream (EG) when both streams are written
   if (blockIdx.x >= second) {
     boff = boff2;
     len = len2;
     frag = frag2;
     out = out2;
+    gbase = nullptr;
   }
   const uint64_t id = (uint64_t)(blockIdx.x >= second ? blockIdx.x - second : blockIdx.x) * 256 + threadIdx.x;
   if (id >= nrows) return;
   const uint64_t pend = (id / rows + 1) * (uint64_t)rows;
+  // gbase: the first stream's offsets are slot-relative, its planes packed from word gbase[plane]
+  const uint64_t sft = gbase ? gbase[id / rows] * 64 - (id / rows) * slot_bits : 0;
   // every load this row usually needs is issued at once (the row, its two fragments, the next row's
   // offset, length and head fragment): one memory round trip instead of three dependent ones
   const bool nx = id + 1 < pend;
-  const uint64_t G = boff[id], L = len[id] & kLenMask;  // (the staged encoder's glen carries row flags)
+  const uint64_t G = boff[id] + sft, L = len[id] & kLenMask;  // (the staged encoder's glen carries row flags)
   const uint64_t f0 = frag[2 * id], f1 = frag[2 * id + 1];
-  const uint64_t G1 = nx ? boff[id + 1] : 0, L1 = nx ? len[id + 1] & kLenMask : 0, h1 = nx ? frag[2 * id + 2] : 0;
+  const uint64_t G1 = nx ? boff[id + 1] + sft : 0, L1 = nx ? len[id + 1] & kLenMask : 0, h1 = nx ? frag[2 * id + 2] : 0;
   if (L == 0) return;
   const uint64_t wt = (G + L - 1) >> 6, wh = G >> 6;
   const uint64_t wb = wt * 64;
@@ -1880,7 +1887,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
   }
   v |= h1;
   for (uint64_t r2 = id + 2; r2 < pend; ++r2) {
-    if ((len[r2] & kLenMask) == 0 || boff[r2] >= wb + 64) break;
+    if ((len[r2] & kLenMask) == 0 || boff[r2] + sft >= wb + 64) break;
     v |= frag[2 * r2];
   }
   out[wt] = bswap64(v);
@@ -1983,7 +1990,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     k_fixup<<<dg && de ? 2 * fgrid : fgrid, 256, 0, s>>>(dg ? fs.gboff : fs.eboff, dg ? fs.glen : fs.elen,
                                                         dg ? fs.gfrag : fs.efrag, dg ? out_g : out_e,
                                                         fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows,
-                                                        dg && de ? fgrid : 0xffffffffu);
+                                                        dg && de ? fgrid : 0xffffffffu,
+                                                        dg && mode == kEncStaged ? a.off_g ? fs.gbase : nullptr : nullptr,
+                                                        slot_g * 64);
     return;
   }
   const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
@@ -1997,13 +2006,13 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
         const uint32_t nwv = (g.used + 63) / 64;  // one workgroup per row, one word per lane
         if (predict) k_row_walk<true><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
         else k_row_walk<false><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
-        k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);
-        if (a.index) k_row_index<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
+        k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);  // (+ the row index)
       }
-      if (a.off_g || a.off_e) {  // packed output: the planes' start words, then the rows' Golomb offsets
-        k_plane_bases<<<1, 1024, 0, s>>>(a);
-        if (a.off_g || a.atom) k_shift_gboff<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
-      }
+      // packed output: the planes' start words (the rows' Golomb offsets stay slot-relative: gb_abs)
+      // -- as the LEN scan's last workgroup instead, its device-scope release fences (an L2 write-back
+      // per workgroup) made C4's prefix 99 -> 153 us
+      if (a.off_g || a.off_e) k_plane_bases<<<1, 1024, 0, s>>>(a);
+      if ((a.off_g || a.off_e) && a.atom) k_shift_gboff<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
       return;
     }
     // persistent grids (more rows per wave when the image is larger)

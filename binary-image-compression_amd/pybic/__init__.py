@@ -421,21 +421,29 @@ class Context:
                                                      cap_words, _p(bits)), "bic_golomb_encode_samples")
         return out, bits
 
-    def patch_encode(self, plane, cols, W, lentab, cap_words=None, want_resid=True):
-        """plane: int64 [rows, wpr]; lentab: numpy uint64 [W*W+1] (host)."""
+    def patch_encode(self, plane, cols, W, lentab, cap_words=None, want_resid=True, bufs=None):
+        """plane: int64 [rows, wpr]; lentab: numpy uint64 [W*W+1] (host). bufs: the dict an earlier
+        call returned, whose device buffers are written again (same shapes; no allocation)."""
         rows, wpr = plane.shape
         nt = (rows // W) * (cols // W)
         t = self.torch
-        weights = t.empty(nt, dtype=t.int32, device=self.dev)
-        wo = t.empty(nt, dtype=t.int32, device=self.dev)
-        wO = t.empty(nt, dtype=t.int32, device=self.dev)
-        modes = t.empty(nt, dtype=t.uint8, device=self.dev)
-        resid = self.empty_i64(rows, wpr) if want_resid else None
         # sum of tile weights <= rows*cols, and k + 1 <= 32 per tile: always enough
         cap_words = cap_words or max(1, (rows * cols + 32 * nt + 63) // 64 + 1)
-        stream = self.empty_i64(cap_words)
-        stats = self.empty_i64(3)
-        lt = np.ascontiguousarray(lentab, np.uint64)
+        if bufs is not None and bufs["weights"].numel() == nt and bufs["stream"].numel() >= cap_words and \
+                (bufs["resid"] is not None) == bool(want_resid):
+            weights, wo, wO, modes = bufs["weights"], bufs["w_nonpred"], bufs["w_pred"], bufs["modes"]
+            resid, stream, stats = bufs["resid"], bufs["stream"], bufs["stats"]
+            cap_words = stream.numel()
+        else:
+            weights = t.empty(nt, dtype=t.int32, device=self.dev)
+            wo = t.empty(nt, dtype=t.int32, device=self.dev)
+            wO = t.empty(nt, dtype=t.int32, device=self.dev)
+            modes = t.empty(nt, dtype=t.uint8, device=self.dev)
+            resid = self.empty_i64(rows, wpr) if want_resid else None
+            stream = self.empty_i64(cap_words)
+            stats = self.empty_i64(3)
+        lt = lentab if isinstance(lentab, np.ndarray) and lentab.dtype == np.uint64 and lentab.flags.c_contiguous \
+            else np.ascontiguousarray(lentab, np.uint64)
         self._bind_stream()
         self._chk(self.lib.bic_patch_encode(self.h, _p(plane), rows, cols, wpr, W, lt.ctypes.data_as(C.c_void_p),
                                             _p(weights), _p(wo), _p(wO), _p(modes), _p(resid), _p(stream),

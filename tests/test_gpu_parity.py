@@ -275,6 +275,23 @@ def test_tiles_stream(ctx, oracle, W, rows, cols, p, wpr):
         assert bytes(res["modes"].cpu().numpy()).decode() == exp["modes"], "modes"
 
 
+def test_tiles_stream_reused_buffers(ctx, oracle):
+    """patch_encode(bufs=...) writes the same buffers again: a second plane through the first call's
+    buffers (stream words of the first, longer stream left behind) == the oracle's"""
+    W, rows, cols = 32, 512, 1024
+    lt = oracle.lentab(W)
+    I1 = oracle.gen_plane(7, 0.5, rows, cols)
+    I2 = oracle.gen_plane(8, 0.05, rows, cols)
+    res = ctx.patch_encode(ctx.to_dev(I1), cols, W, lt)
+    res2 = ctx.patch_encode(ctx.to_dev(I2), cols, W, lt, bufs=res)
+    ctx.sync()
+    assert res2["stream"].data_ptr() == res["stream"].data_ptr()
+    exp = oracle.patch_encode(I2, cols, W, lt)
+    assert int(as_u64(res2["stats"])[0]) == exp["bits"]
+    assert stream_bytes(res2["stream"], exp["bits"]) == exp["stream"].tobytes()
+    assert np.array_equal(as_u64(res2["resid"]), mask_pixels(exp["residual"], cols))
+
+
 def test_pack_streams(ctx, oracle):
     rows, cols = 50, 700
     P = planes_of(oracle, 4, rows, cols, 0.2, 600)
