@@ -65,6 +65,10 @@ namespace {
   do {                                              \
     if ((x) != hipSuccess) return BIC_EDEVICE;      \
   } while (0)
+#ifndef BIC_PROF_EVENT_FLAGS
+#define BIC_PROF_EVENT_FLAGS hipEventDisableSystemFence
+#endif
+constexpr unsigned kProfEventFlags = BIC_PROF_EVENT_FLAGS;
 
 hipEvent_t take_event(bic_ctx* ctx) {
   if (!ctx->pool.empty()) {
@@ -73,7 +77,9 @@ hipEvent_t take_event(bic_ctx* ctx) {
     return e;
   }
   hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
+  // device-scope timing events: a system-scope release at every record would write back L2 between
+  // the launches it brackets
+  if (hipEventCreateWithFlags(&e, kProfEventFlags) != hipSuccess) (void)hipEventCreate(&e);
   return e;
 }
 

@@ -254,10 +254,14 @@ def test_tiles_golden(ctx, golden):
 @pytest.mark.parametrize("W,rows,cols,p,wpr", [(32, 1024, 1024, 0.5, None), (32, 512, 2048, 0.02, None),
                                                (8, 256, 512, 0.1, None), (5, 100, 200, 0.3, None),
                                                (64, 256, 320, 0.01, None), (16, 96, 208, 0.4, None),
-                                               (8, 64, 72, 0.5, None), (32, 64, 96, 0.3, 4), (16, 48, 4160, 0.2, None)])
+                                               (8, 64, 72, 0.5, None), (32, 64, 96, 0.3, 4), (16, 48, 4160, 0.2, None),
+                                               (32, 512, 4096, 0.5, None), (8, 64, 4096, 0.3, None),
+                                               (16, 96, 8192, 0.05, None), (64, 128, 4096, 0.5, None),
+                                               (32, 2048, 8192, 0.02, None)])
 def test_tiles_stream(ctx, oracle, W, rows, cols, p, wpr):
     """aligned tiles (W in 8..64, one word holds 64/W tiles) and the generic path (W = 5); partial
-    last words, rows with words past the pixels (wpr > ceil(cols/64))"""
+    last words, rows with words past the pixels (wpr > ceil(cols/64)); rows of whole 64-word groups
+    (cols % 4096 == 0) take the tile kernel that also scans the sample coder"""
     I = oracle.gen_plane(31 + W, p, rows, cols, wpr=wpr)
     lt = oracle.lentab(W)
     exp = oracle.patch_encode(I, cols, W, lt)
