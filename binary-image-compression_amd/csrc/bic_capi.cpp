@@ -148,11 +148,13 @@ void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
 }
 
 // The staged encoder's ~8 dependent launches cost more than the single kernel's look-back waits
-// on small batches (C2, one 4096^2 plane: 92 vs 25 us); from kStagedMinRows rows (all planes) on
-// it is the faster one (C3: 131,072 rows). BIC_OPT_STAGED forces it.
-constexpr uint64_t kStagedMinRows = 32768;
+// on small batches (C2, one 4096^2 plane: 81 vs 45 us); from kStagedMinRows rows or kStagedMinWords
+// plane words (all planes) on it is the faster one (C3: 131,072 rows; one 16384^2 plane, 16,384 rows
+// of 256 words: 0.181 vs 0.252 ms). BIC_OPT_STAGED forces it.
+constexpr uint64_t kStagedMinRows = 32768, kStagedMinWords = 1ull << 20;
 bool staged_pays(const bic_ctx* ctx, const bic::Geom& g) {
-  return ctx->force_staged || (uint64_t)g.rows * g.nplanes >= kStagedMinRows;
+  const uint64_t rows = (uint64_t)g.rows * g.nplanes;
+  return ctx->force_staged || rows >= kStagedMinRows || rows * g.used >= kStagedMinWords;
 }
 
 bool geom_ok(size_t rows, size_t cols, size_t wpr) {

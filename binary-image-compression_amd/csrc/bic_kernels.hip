@@ -1117,7 +1117,10 @@ void launch_eg_emit(hipStream_t s, const Geom& g, const uint64_t* planes, int pr
 // before it (the coder's accumulated error A) and, once its lengths are known, its bit offset
 // -- and zeroes the block's output words; a second kernel writes the codewords.
 // ------------------------------------------------------------------------------------
-constexpr int kItems = 8;
+#ifndef BIC_SAMP_ITEMS
+#define BIC_SAMP_ITEMS 4  // C5 (65,536 samples): 4 per thread 13 us for both launches, 8: 15.5, 16: 20.5
+#endif
+constexpr int kItems = BIC_SAMP_ITEMS;
 constexpr uint32_t kSampPerBlk = kBlock * kItems;
 
 __global__ __launch_bounds__(kBlock) void k_samp_scan(const uint32_t* __restrict__ s, size_t n, uint64_t n0,
