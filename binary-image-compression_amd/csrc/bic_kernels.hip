@@ -452,7 +452,7 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 }
 
 // From the gray image (bic_encode_gray: bitplane_tool.cpp:24-30 and the count pass in one read):
-// one wave per strip of 64 plane words (4096 columns) and kGrayRows rows; lane l owns word
+// one wave per strip of 64 plane words (4096 columns) and gray_rows_per_wave() rows; lane l owns word
 // 64 s + l of strip s: four 16-byte loads give its 64 pixels, K1's 8x8 transposes one word per
 // plane; the plane words are stored and the med residual is formed from the row above (plane
 // words kept in registers) and the pixel left of the word (lane l - 1's last; lane 0 of strip s > 0
@@ -463,7 +463,13 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 #ifndef BIC_GRAY_ROWS
 #define BIC_GRAY_ROWS 4
 #endif
-constexpr int kGrayRows = BIC_GRAY_ROWS;
+// rows per wave: the plane-word form carries the row above's plane words from row to row (four rows,
+// one transpose of the row above per wave); the byte-domain med (BYTEMED below) needs only the row
+// above's bytes, so one row per wave (53 VGPRs, up to 8 waves per SIMD: C3 count pass 150 -> 135 us)
+#ifndef BIC_GRAY_ROWS_BM
+#define BIC_GRAY_ROWS_BM 1
+#endif
+constexpr int kGrayRowsP = BIC_GRAY_ROWS, kGrayRowsBM = BIC_GRAY_ROWS_BM;
 uint32_t gray_strips(const Geom& g) { return (g.used + 63) / 64; }
 
 // out[b] = bytes b of w0..w3, w0's in the most significant byte (a 4x4 byte transpose)
@@ -533,11 +539,21 @@ constexpr bool kGrayPipe = BIC_GRAY_PIPE != 0;
 #define BIC_GRAY_PREFETCH 1
 #endif
 constexpr bool kGrayPrefetch = BIC_GRAY_PREFETCH != 0;  // the next row's pixels loaded during this row
+// BYTEMED (residual planes stored, planes = NULL in bic_encode_gray): bitplane extraction is linear over
+// XOR, so the med residual is formed on the gray bytes -- G = row ^ row above, H = G ^ (G one pixel to
+// the left) -- and ONE transpose of H gives every plane's R (pred.cpp:3-15: R = P ^ up ^ left ^ up-left).
+// The row above is kept as bytes (no transpose of it, also none for the row above the wave's first row).
+#ifndef BIC_GRAY_BYTEMED
+#define BIC_GRAY_BYTEMED 1
+#endif
+constexpr bool kGrayByteMed = BIC_GRAY_BYTEMED != 0;
 // EGW (FULL strips of a row of whole strips): the EG words inside the row (eg.cpp:20-37: ~R then the
 // row's '1'), at the offsets every row after the plane's first 1 has -- row r at bit r (cols + 1) + 1
 // of plane b's stream at word b * eg_stride (eg_base_ok). A lane forms the stream word that starts
 // inside its own row word from it and lane l + 1's: the words across strip edges and the row's first
 // and last words are the emission's (eg_row_edges), as are whole rows up to the plane's first 1.
+template <bool PREDICT, bool STORE_R>
+constexpr int gray_rows_per_wave() { return kGrayByteMed && PREDICT && STORE_R ? kGrayRowsBM : kGrayRowsP; }
 template <bool PREDICT, bool FULL, bool STORE_R, bool NP8, bool EGW>
 __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray, size_t pitch, const Geom& g,
                                                 uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
@@ -563,19 +579,27 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
       lb >>= plane0;
     }
   };
+  constexpr bool BM = kGrayByteMed && PREDICT && STORE_R;
   uint64_t up[8];
 #pragma unroll
   for (int b = 0; b < 8; ++b) up[b] = 0;
   uint32_t ulast = 0, ulb = 0;  // the row above's last pixel of the word / pixel before the strip
-  uint4 cur[4];
+  uint4 cur[4], upb[4];         // (BM: the row above's bytes)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) upb[q] = make_uint4(0, 0, 0, 0);
   uint32_t clb;
   if (PREDICT && r0) {
     load(r0 - 1, cur, ulb);
-    gray_to_planes<FULL>(cur, up, mask);
-    ulast = cur[3].w >> 24;
+    if constexpr (BM) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) upb[q] = cur[q];
+    } else {
+      gray_to_planes<FULL>(cur, up, mask);
+      ulast = cur[3].w >> 24;
+    }
   }
   load(r0, cur, clb);
-  const uint32_t nr = min((uint32_t)kGrayRows, g.rows - r0);
+  const uint32_t nr = min((uint32_t)gray_rows_per_wave<PREDICT, STORE_R>(), g.rows - r0);
   for (uint32_t r = 0; r < nr; ++r) {
     const uint32_t row = r0 + r;
     uint4 nxt[4];
@@ -583,14 +607,41 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
     if (kGrayPrefetch && r + 1 < nr) load(row + 1, nxt, nlb);
     // D bits (8 planes per byte) of the pixel left of the word: lane l - 1's last, or the strip's
     // preceding pixel for lane 0 (0 at column 0)
-    const uint32_t cl = cur[3].w >> 24;
-    const uint32_t dl = (PREDICT && row) ? cl ^ ulast : cl;
-    uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x138, 0xf, 0xf, true);
-    if (lane == 0) left = (PREDICT && row) ? clb ^ ulb : clb;
-    ulast = cl;
-    ulb = clb;
     uint64_t pw[8];
-    gray_to_planes<FULL>(cur, pw, mask);
+    uint32_t left = 0;
+    if constexpr (BM) {
+      // G = D bytes (8 planes per byte), H = G ^ G one pixel left: H's planes are R
+      uint32_t gd[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        gd[4 * q] = cur[q].x ^ upb[q].x;
+        gd[4 * q + 1] = cur[q].y ^ upb[q].y;
+        gd[4 * q + 2] = cur[q].z ^ upb[q].z;
+        gd[4 * q + 3] = cur[q].w ^ upb[q].w;
+      }
+      uint32_t gl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(gd[15] >> 24), 0x138, 0xf, 0xf, true);
+      if (lane == 0) gl = clb ^ ulb;  // the D byte before the strip (0 at column 0)
+      uint32_t hd[16];
+      hd[0] = gd[0] ^ __builtin_amdgcn_alignbyte(gd[0], gl << 24, 3);
+#pragma unroll
+      for (int d = 1; d < 16; ++d) hd[d] = gd[d] ^ __builtin_amdgcn_alignbyte(gd[d], gd[d - 1], 3);
+      if (row == 0 && w == 0) hd[0] &= ~0xffu;  // pred.cpp never writes pP(0,0)
+      uint4 hv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hv[q] = make_uint4(hd[4 * q], hd[4 * q + 1], hd[4 * q + 2], hd[4 * q + 3]);
+      gray_to_planes<FULL>(hv, pw, mask);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) upb[q] = cur[q];
+      ulb = clb;
+    } else {
+      const uint32_t cl = cur[3].w >> 24;
+      const uint32_t dl = (PREDICT && row) ? cl ^ ulast : cl;
+      left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x138, 0xf, 0xf, true);
+      if (lane == 0) left = (PREDICT && row) ? clb ^ ulb : clb;
+      ulast = cl;
+      ulb = clb;
+      gray_to_planes<FULL>(cur, pw, mask);
+    }
     uint32_t* tb = kGrayPipe ? tw + (r & 1) * 1024 : tw;
     // EG: the strip's first row bit (wave-uniform shift; lane l's word starts 64 l bits later)
     const uint64_t ep = (uint64_t)row * (g.cols + 1) + (row ? 1u : 0u) + (uint64_t)s * 4096;
@@ -601,7 +652,7 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
       if (!NP8 && b >= np) break;
       if (!STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = pw[b];
       uint64_t R = pw[b];
-      if constexpr (PREDICT) {
+      if constexpr (PREDICT && !BM) {
         const uint64_t D = pw[b] ^ up[b];
         R = D ^ ((D >> 1) | ((uint64_t)((left >> b) & 1u) << 63));
         if constexpr (!FULL) R &= mask;
@@ -661,7 +712,7 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
   uint32_t* tw = tab[threadIdx.x >> 6];
   const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
   const uint32_t s = (uint32_t)(gw % ns);  // the strips of one row block are neighbouring waves
-  const uint32_t r0 = (uint32_t)(gw / ns) * kGrayRows;
+  const uint32_t r0 = (uint32_t)(gw / ns) * gray_rows_per_wave<PREDICT, STORE_R>();
   if (r0 >= g.rows) return;  // whole wave
   // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
   if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
@@ -686,7 +737,8 @@ void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Ge
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero, bool store_resid,
                       uint64_t* out_e, uint64_t eg_stride) {
   const uint32_t ns = gray_strips(g);
-  const uint64_t waves = (uint64_t)(g.rows + kGrayRows - 1) / kGrayRows * ns;
+  const uint32_t rpw = predict && store_resid ? gray_rows_per_wave<true, true>() : gray_rows_per_wave<true, false>();
+  const uint64_t waves = (uint64_t)(g.rows + rpw - 1) / rpw * ns;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
   const bool egw = out_e && gray_eg_supported(g);
 #define BIC_GS(P, R, E) \
