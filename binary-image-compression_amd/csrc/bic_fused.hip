@@ -1583,18 +1583,116 @@ constexpr bool kEmitPrefetch = BIC_EMIT_PREFETCH != 0;  // next row loaded durin
 #define BIC_REST_AUX 1
 #endif
 constexpr bool kRestAux = BIC_REST_AUX != 0;  // k_emit_rest on the context's second stream (beside k_emit_known)
+// One row of k_emit_known (rr: its residual words; O, Lf, Gb: its ones before, Golomb length + flags,
+// absolute Golomb bit offset; Eb: its plane's EG start bit), by one wave with its LDS image gimg.
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+__device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, uint32_t plane, uint32_t row,
+                                               const uint64_t (&rr)[WPL], uint32_t O, uint64_t Lf, uint64_t Gb,
+                                               uint64_t Eb, uint32_t* gimg, const uint32_t* s_lut) {
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+  const uint64_t L = Lf & kLenMask;
+  const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
+  bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
+#ifdef BIC_STAMPS
+  if (a.dbg & 1) gk1 = false;
+#endif
+  if (gk1) {  // zero the Golomb image
+    uint4* z = reinterpret_cast<uint4*>(gimg);
+    for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  bool f_here = false;  // the plane's first 1 is in this row (k_emit_rest writes its EG row)
+  if (DO_E && O == 0) {
+    uint32_t ones = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) ones += (uint32_t)__popcll(rr[t]);
+    f_here = wave_sum_u32(ones) > 0;
+  }
+#ifdef BIC_STAMPS
+  if (!(a.dbg & 2))
+#endif
+  if constexpr (DO_E) {  // EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1
+    const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
+    const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
+    const uint64_t cap = a.slot_e * 64;
+    const uint64_t Ge = Eb + Ge_rel;
+    if (Ge_rel + Le <= cap) {
+      if (a.eg_cp && O > 0 && eg_base_ok(a, plane))
+        eg_row_edges<WPL>(rr, g, Ge, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
+      else if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
+      if (lane == 0) {
+        a.eboff[id] = Ge;
+        a.elen[id] = Le;
+      }
+    } else if (lane == 0) {
+      a.eboff[id] = Ge;
+      a.elen[id] = 0;
+      atomicOr(&a.flags[0], 1u);
+    }
+    if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
+  }
+  STAMP(1);
+#ifdef BIC_STAMPS
+  if (lane == 0) g_stamps[id * 8 + 3] = (k0 ? 1u : 0u) | (gk1 ? 2u : 0u) | ((uint64_t)blockIdx.x << 8) |
+                                        ((uint64_t)(threadIdx.x >> 6) << 40);
+#endif
+  if constexpr (DO_G) {
+    if (k0 && L) {
+#ifdef BIC_STAMPS
+      if (!(a.dbg & 4))
+#endif
+      eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
+    } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
+      uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
+      int jpc = -1;
+      uint32_t loc = 0;
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        if (t * 64 >= (int)g.used) break;
+        const uint32_t w = t * 64 + lane;
+        const uint64_t x = rr[t];
+        const int jp = step_jp(x, w, jpc);
+        const bool eol = w == g.used - 1;
+        const LaneEnc e = encode_word_k1b(x, w, jp, eol, g.cols, s_lut);
+        const uint32_t inc = wave_incl_sum_u32(e.len);
+        const uint32_t off = loc + inc - e.len;
+        loc += lane63_u32(inc);
+        if (!e.lng) {
+          if (e.head) lds_or64(img, off >> 6, BIC_MSB >> (off & 63));
+          place128_64(img, off + 1 + e.z, e.t0, e.t1, e.tlen);
+        } else {
+          LdsSink64 ls{img, 0, 0};
+          emit_word_k1(ls, off, x, w, jp, eol, g.cols);
+          ls.flush();
+        }
+      }
+      if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      write_row64(img, L, Gb, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
+    }
+    if (lane == 0) {
+      // glen keeps its flags: k_emit_rest (on the other stream) reads them too
+      const bool slow = L && !k0 && !fits;
+      a.gslow[id] = slow ? O + row + 1 : 0;  // k_rows_global writes the row
+      if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
+    }
+  }
+}
+
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * kGImg];
   __shared__ uint32_t s_lut[512];
   const Geom& g = a.g;
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  [[maybe_unused]] const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
   uint32_t* gimg = lds + wave * kGImg;
   if (DO_G)
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
   __syncthreads();  // the only workgroup barrier
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
   // persistent waves: rows id, id + stride, ...
   const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
   const uint64_t id0 = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
@@ -1636,100 +1734,16 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
       Lf = DO_G ? a.glen[id] : 0;
       Gb = DO_G ? gb_abs(a, id, plane) : 0;  // loaded with the row, not after the branch that uses it
     }
-    const uint64_t L = Lf & kLenMask;
-    const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
-    bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
-#ifdef BIC_STAMPS
-    if (a.dbg & 1) gk1 = false;
-#endif
-    if (gk1) {  // zero the Golomb image
-      uint4* z = reinterpret_cast<uint4*>(gimg);
-      for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
-    }
     uint64_t rr[WPL];
     row_resid<WPL, PREDICT>(g, row, cp_, cu_, rr);
-    bool f_here = false;  // the plane's first 1 is in this row (k_emit_rest writes its EG row)
-    if (DO_E && O == 0) {
-      uint32_t ones = 0;
-#pragma unroll
-      for (int t = 0; t < WPL; ++t) ones += (uint32_t)__popcll(rr[t]);
-      f_here = wave_sum_u32(ones) > 0;
-    }
-#ifdef BIC_STAMPS
-    if (!(a.dbg & 2))
-#endif
-    if constexpr (DO_E) {  // EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1
-      const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
-      const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
-      const uint64_t cap = a.slot_e * 64;
-      const uint64_t Ge = (a.ebase ? a.ebase[plane] : (uint64_t)plane * cap) + Ge_rel;
-      if (Ge_rel + Le <= cap) {
-        if (a.eg_cp && O > 0 && eg_base_ok(a, plane))
-          eg_row_edges<WPL>(rr, g, Ge, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
-        else if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
-        if (lane == 0) {
-          a.eboff[id] = Ge;
-          a.elen[id] = Le;
-        }
-      } else if (lane == 0) {
-        a.eboff[id] = Ge;
-        a.elen[id] = 0;
-        atomicOr(&a.flags[0], 1u);
-      }
-      if (lane == 0 && row == g.rows - 1) a.bits_e[plane] = Ge_rel + Le;
-    }
-    STAMP(1);
-#ifdef BIC_STAMPS
-    if (lane == 0) g_stamps[id * 8 + 3] = (k0 ? 1u : 0u) | (gk1 ? 2u : 0u) | ((uint64_t)blockIdx.x << 8) |
-                                          ((uint64_t)(threadIdx.x >> 6) << 40);
-#endif
-    if constexpr (DO_G) {
-      if (k0 && L) {
-#ifdef BIC_STAMPS
-        if (!(a.dbg & 4))
-#endif
-        eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
-      } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
-        uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
-        int jpc = -1;
-        uint32_t loc = 0;
-#pragma unroll
-        for (int t = 0; t < WPL; ++t) {
-          if (t * 64 >= (int)g.used) break;
-          const uint32_t w = t * 64 + lane;
-          const uint64_t x = rr[t];
-          const int jp = step_jp(x, w, jpc);
-          const bool eol = w == g.used - 1;
-          const LaneEnc e = encode_word_k1b(x, w, jp, eol, g.cols, s_lut);
-          const uint32_t inc = wave_incl_sum_u32(e.len);
-          const uint32_t off = loc + inc - e.len;
-          loc += lane63_u32(inc);
-          if (!e.lng) {
-            if (e.head) lds_or64(img, off >> 6, BIC_MSB >> (off & 63));
-            place128_64(img, off + 1 + e.z, e.t0, e.t1, e.tlen);
-          } else {
-            LdsSink64 ls{img, 0, 0};
-            emit_word_k1(ls, off, x, w, jp, eol, g.cols);
-            ls.flush();
-          }
-        }
-        if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        write_row64(img, L, Gb, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
-      }
-      if (lane == 0) {
-        // glen keeps its flags: k_emit_rest (on the other stream) reads them too
-        const bool slow = L && !k0 && !fits;
-        a.gslow[id] = slow ? O + row + 1 : 0;  // k_rows_global writes the row
-        if (slow) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
-      }
-    }
+    const uint64_t Eb = DO_E ? (a.ebase ? a.ebase[plane] : (uint64_t)plane * a.slot_e * 64) : 0;
+    emit_known_row<WPL, PREDICT, DO_G, DO_E>(a, id, plane, row, rr, O, Lf, Gb, Eb, gimg, s_lut);
     STAMP(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
     __builtin_amdgcn_wave_barrier();
   }
 }
+
 
 // The rows the prefix kernels leave to this launch: Golomb rows with mixed k (per-codeword k,
 // encode_word; among the walked rows, counter[2]) and the EG row holding the plane's first 1 (with

@@ -738,8 +738,8 @@ void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Ge
                       uint64_t* out_e, uint64_t eg_stride) {
   const uint32_t ns = gray_strips(g);
   const uint32_t rpw = predict && store_resid ? gray_rows_per_wave<true, true>() : gray_rows_per_wave<true, false>();
-  const uint64_t waves = (uint64_t)(g.rows + rpw - 1) / rpw * ns;
-  const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
+  const uint64_t units = (uint64_t)(g.rows + rpw - 1) / rpw;  // row groups per strip
+  const uint32_t grid = (uint32_t)((units * ns + kWaves - 1) / kWaves);
   const bool egw = out_e && gray_eg_supported(g);
 #define BIC_GS(P, R, E) \
   k_gray_strips<P, R, E><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero, \
