@@ -425,8 +425,9 @@ class C3Planes(C3):
 class C3File(C3):
     """C3 from a P5 file's bytes: the whole file -- header + 16384^2 raster -- is
     resident in HBM as read; a step parses the header on the host (bic_pnm_parse_header, from the
-    file's first bytes), extracts the planes from the raster where it lies (19 bytes into the file:
-    bic_pgm_bitplanes, unaligned loads) and encodes them (bic_encode_planes2, Golomb + EG)."""
+    file's first bytes) and encodes the raster where it lies (19 bytes into the file) in one call:
+    bic_encode_gray, whose count pass reads misaligned rows through aligned 16-byte chunks (planes
+    NULL, as the default C3 step). --separate: bic_pgm_bitplanes then bic_encode_planes2."""
 
     def __init__(self, ctx, args, rank):
         import pybic
@@ -447,7 +448,9 @@ class C3File(C3):
             self.files.append(f)
         self.gray = [f[len(hdr):].view(self.rows, self.cols) for f in self.files]
         self.wpr = (self.cols + 63) // 64
-        self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr)
+        self.separate = args.separate
+        self.store_planes = args.separate or args.store_planes
+        self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr) if self.store_planes else None
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
         self.out_g = ctx.empty_i64(self.nplanes, self.slot_g)
@@ -456,18 +459,25 @@ class C3File(C3):
         self.bits_e = ctx.empty_i64(self.nplanes)
         ctx.reserve(self.nplanes, self.rows, self.cols)
         self.k = 0
-        self.separate = True
         self.pixels = self.rows * self.cols * self.nplanes
         self.workload = (f"c3f: a {self.rows}x{self.cols} P5 file's bytes in HBM -> header (host) -> 8 bitplanes "
-                         f"from the raster in place -> med -> Golomb + EG streams per plane")
+                         f"from the raster in place (offset {len(hdr)}) -> med -> Golomb + EG streams per plane" +
+                         (" (bic_pgm_bitplanes + bic_encode_planes2)" if self.separate else
+                          " (one bic_encode_gray call on the misaligned raster)"))
 
     def step(self):
         c = self.ctx
         h = self.pybic.pnm_header(self.head)
         f = self.files[self.k & 1]
-        c.pgm_bitplanes(f[h.data_offset:], h.rows, h.cols, h.maxval, self.nplanes, out=self.planes)
-        c.encode_planes2(self.planes, self.cols, True, slots=(self.slot_g, self.slot_e), outs=(self.out_g, self.out_e),
-                         bits=(self.bits_g, self.bits_e))
+        if self.separate or h.maxval > 255:
+            c.pgm_bitplanes(f[h.data_offset:], h.rows, h.cols, h.maxval, self.nplanes, out=self.planes)
+            c.encode_planes2(self.planes, self.cols, True, slots=(self.slot_g, self.slot_e),
+                             outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
+        else:  # 8-bit samples: the raster is a gray image with pitch = cols, wherever it starts
+            raster = f[h.data_offset:h.data_offset + h.rows * h.cols].view(h.rows, h.cols)
+            c.encode_gray(raster, cols=h.cols, nplanes=8, planes=self.planes, slots=(self.slot_g, self.slot_e),
+                          outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e),
+                          store_planes=self.store_planes)
         self.k += 1
 
     def kernel_bytes(self):

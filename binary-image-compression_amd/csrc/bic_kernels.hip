@@ -554,7 +554,46 @@ constexpr bool kGrayByteMed = BIC_GRAY_BYTEMED != 0;
 // and last words are the emission's (eg_row_edges), as are whole rows up to the plane's first 1.
 template <bool PREDICT, bool STORE_R>
 constexpr int gray_rows_per_wave() { return kGrayByteMed && PREDICT && STORE_R ? kGrayRowsBM : kGrayRowsP; }
-template <bool PREDICT, bool FULL, bool STORE_R, bool NP8, bool EGW>
+// 64 bytes from src at any alignment (MIS: src not 16-byte aligned): the aligned 16-byte chunks that
+// hold them (never a chunk without one of them: no read past the buffer's last page), realigned by
+// the offset (the same for every lane of a wave: w * 64 is a multiple of 16)
+__device__ __forceinline__ void load64_mis(const uint8_t* src, uint4 (&v)[4]) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+  const uint32_t mis = (uint32_t)(a & 15), bs = mis & 3, dq = mis >> 2;
+  const uint4* b = reinterpret_cast<const uint4*>(src - mis);  // (pointer arithmetic: stays a global load)
+  uint32_t in[20];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4 x = b[q];
+    in[4 * q] = x.x;
+    in[4 * q + 1] = x.y;
+    in[4 * q + 2] = x.z;
+    in[4 * q + 3] = x.w;
+  }
+  const uint4 x4 = mis ? b[4] : make_uint4(0, 0, 0, 0);
+  in[16] = x4.x;
+  in[17] = x4.y;
+  in[18] = x4.z;
+  in[19] = x4.w;
+  // out dword d = bytes 4 (d + dq) + bs ..: one wave-uniform case per dword offset (static indices)
+#define BIC_MIS_CASE(DQ)                                                                                    \
+  case DQ:                                                                                                  \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) v[q] =                                                    \
+        make_uint4(__builtin_amdgcn_alignbyte(in[4 * q + DQ + 1], in[4 * q + DQ], bs),                     \
+                   __builtin_amdgcn_alignbyte(in[4 * q + DQ + 2], in[4 * q + DQ + 1], bs),                 \
+                   __builtin_amdgcn_alignbyte(in[4 * q + DQ + 3], in[4 * q + DQ + 2], bs),                 \
+                   __builtin_amdgcn_alignbyte(in[4 * q + DQ + 4], in[4 * q + DQ + 3], bs));                \
+    break;
+  switch (dq) {
+    BIC_MIS_CASE(0)
+    BIC_MIS_CASE(1)
+    BIC_MIS_CASE(2)
+    default: BIC_MIS_CASE(3)
+  }
+#undef BIC_MIS_CASE
+}
+
+template <bool PREDICT, bool FULL, bool STORE_R, bool NP8, bool EGW, bool MIS = false>
 __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray, size_t pitch, const Geom& g,
                                                 uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
                                                 uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
@@ -568,8 +607,15 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
   // the word's 64 pixels, and (lane 0 of strips s > 0) the pixel before the strip
   auto load = [&](uint32_t row, uint4 (&v)[4], uint32_t& lb) {
     const uint8_t* src = gray + (uint64_t)row * pitch + (uint64_t)w * 64;
+    if constexpr (MIS) {
+      if (in) load64_mis(src, v);
+      else
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = in ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) v[q] = make_uint4(0, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = in ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
+    }
     lb = (lane == 0 && s > 0) ? (uint32_t)src[-1] : 0u;
     if (plane0) {  // planes plane0.. of the range: every pixel's bits shifted down (a wave-uniform branch)
       const uint32_t m = 0x01010101u * (0xffu >> plane0);
@@ -701,7 +747,7 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
 #ifndef BIC_GRAY_WAVES
 #define BIC_GRAY_WAVES 4
 #endif
-template <bool PREDICT, bool STORE_R, bool EGW>
+template <bool PREDICT, bool STORE_R, bool EGW, bool MIS = false>
 __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
                                                         uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
@@ -716,21 +762,23 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
   if (r0 >= g.rows) return;  // whole wave
   // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
   if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
-    gray_strip_rows<PREDICT, true, STORE_R, true, EGW>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw,
-                                                       out_e, eg_stride);
+    gray_strip_rows<PREDICT, true, STORE_R, true, EGW, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
+                                                            tw, out_e, eg_stride);
   else if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
-    gray_strip_rows<PREDICT, true, STORE_R, false, EGW>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos, tw,
-                                                        out_e, eg_stride);
+    gray_strip_rows<PREDICT, true, STORE_R, false, EGW, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
+                                                             tw, out_e, eg_stride);
   else if constexpr (!EGW)  // (EGW launches have whole strips only: gray_eg_supported)
-    gray_strip_rows<PREDICT, false, STORE_R, false, false>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
-                                                           tw, nullptr, 0);
+    gray_strip_rows<PREDICT, false, STORE_R, false, false, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec,
+                                                                kpos, tw, nullptr, 0);
 }
 
 bool gray_eg_supported(const Geom& g) { return g.trail == ~0ull && g.used % 64 == 0; }
 
+// any gray alignment and pitch (rows not 16-byte aligned: load64_mis); every row must hold used * 64
+// readable bytes
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes) {
-  return g.used <= 256 && pitch % 16 == 0 && pitch >= (size_t)g.used * 64 &&
-         reinterpret_cast<uintptr_t>(gray) % 16 == 0 && reinterpret_cast<uintptr_t>(planes) % 8 == 0;
+  (void)gray;
+  return g.used <= 256 && pitch >= (size_t)g.used * 64 && reinterpret_cast<uintptr_t>(planes) % 8 == 0;
 }
 
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
@@ -740,11 +788,12 @@ void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Ge
   const uint32_t rpw = predict && store_resid ? gray_rows_per_wave<true, true>() : gray_rows_per_wave<true, false>();
   const uint64_t units = (uint64_t)(g.rows + rpw - 1) / rpw;  // row groups per strip
   const uint32_t grid = (uint32_t)((units * ns + kWaves - 1) / kWaves);
-  const bool egw = out_e && gray_eg_supported(g);
-#define BIC_GS(P, R, E) \
-  k_gray_strips<P, R, E><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, zero, \
-                                                 out_e, eg_stride)
-#define BIC_GS2(P, R) { if (egw) BIC_GS(P, R, true); else BIC_GS(P, R, false); }
+  const bool mis = pitch % 16 != 0 || reinterpret_cast<uintptr_t>(gray) % 16 != 0;  // e.g. a P5 raster in its file
+  const bool egw = out_e && gray_eg_supported(g) && !mis;
+#define BIC_GS(P, R, E, M) \
+  k_gray_strips<P, R, E, M><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, \
+                                                    zero, out_e, eg_stride)
+#define BIC_GS2(P, R) { if (mis) BIC_GS(P, R, false, true); else if (egw) BIC_GS(P, R, true, false); else BIC_GS(P, R, false, false); }
   if (predict) { if (store_resid) BIC_GS2(true, true) else BIC_GS2(true, false) }
   else BIC_GS2(false, false)  // without prediction R = P
 #undef BIC_GS2

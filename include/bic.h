@@ -127,9 +127,10 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
                        uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg);
 /* a2 + a5-a10 in one call: bitplane_tool.cpp:24-30's planes of a gray image (as
  * bic_bitplanes_u8, into `planes`) and both streams of every plane (as bic_encode_planes2). Rows of
- * up to 16384 columns whose gray rows hold ceil(cols/64)*64 readable bytes (pitch >= that, gray and
- * pitch 16-byte aligned) read the image once: the bitplane kernel also produces the encoder's
- * per-row counts. Otherwise the same result through the two separate calls.
+ * up to 16384 columns whose gray rows hold ceil(cols/64)*64 readable bytes (pitch >= that; any
+ * alignment of gray and pitch, e.g. a P5 raster where it lies in its file's bytes) read the image
+ * once: the bitplane kernel also produces the encoder's per-row counts. Otherwise the same result
+ * through the two separate calls.
  * planes may be NULL (also in the _range / _packed forms below): the bitplanes are then formed in
  * registers only and not returned; the count pass stores each plane's med residual instead (in a
  * buffer the context keeps, nplanes * rows * wpr words), from which the encoder writes the same

@@ -220,6 +220,39 @@ def test_encode_gray(ctx, oracle, staged, rows, cols, pitch, nplanes, kind):
                 assert stream_bytes(out[k], nb) == est.tobytes(), (pred, k, coder)
 
 
+@pytest.mark.parametrize("off,rows,cols,pitch,kind", [
+    (19, 40, 4096, 4096, "uniform"),  # a P5 raster 19 bytes into its file (c3f's layout)
+    (3, 33, 16384, 16384, "smooth"), (1, 17, 100, 131, "uniform"), (7, 24, 5000, 5125, "smooth"),
+    (8, 9, 64, 72, "uniform"), (13, 70, 16384, 16387, "uniform"),  # pitch % 16 != 0: every row its own offset
+])
+def test_encode_gray_misaligned(ctx, oracle, staged, off, rows, cols, pitch, kind):
+    """bic_encode_gray on gray rows at any byte alignment (the count pass reads the aligned 16-byte
+    chunks that hold a lane's 64 pixels and realigns them) == the oracle's planes and streams, with
+    and without the planes returned, with and without prediction"""
+    t = ctx.torch
+    buf = np.full(off + rows * pitch + 64, 0x5A, np.uint8)
+    img = np.zeros((rows, pitch), np.uint8)
+    img[:, :cols] = _gray(oracle, off * 131 + rows + cols, rows, cols, kind)
+    img[:, cols:] = 0xC3  # bytes past cols never reach a plane
+    buf[off:off + rows * pitch] = img.reshape(-1)
+    d = t.from_numpy(buf).to(ctx.dev)
+    g = d[off:off + rows * pitch].view(rows, pitch)
+    assert g.data_ptr() % 16 == (d.data_ptr() + off) % 16
+    exp_planes = oracle.bitplanes(np.ascontiguousarray(img[:, :cols]), 8)
+    for pred in (1, 0):
+        for store in (True, False):
+            planes, (og, bg), (oe, be) = ctx.encode_gray(g, cols=cols, nplanes=8, predict=bool(pred), store_planes=store)
+            ctx.sync()
+            if store:
+                assert np.array_equal(as_u64(planes), exp_planes)
+            for k in range(8):
+                for coder, out, bits in ((0, og, bg), (1, oe, be)):
+                    eb, est, _ = oracle.encode_plane(exp_planes[k], cols, pred, coder)
+                    nb = int(as_u64(bits)[k])
+                    assert nb == eb, (pred, store, k, coder)
+                    assert stream_bytes(out[k], nb) == est.tobytes(), (pred, store, k, coder)
+
+
 @pytest.mark.parametrize("rows,cols,pitch,plane0,nplanes,kind", [
     (1, 64, 64, 0, 8, "uniform"), (17, 100, 128, 0, 8, "uniform"), (33, 4096, 4096, 0, 8, "uniform"),
     (40, 5000, 5120, 2, 3, "smooth"), (24, 16384, 16384, 0, 8, "uniform"), (70, 16384, 16384, 1, 6, "smooth"),
