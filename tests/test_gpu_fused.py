@@ -239,18 +239,18 @@ def test_encode_gray_misaligned(ctx, oracle, staged, off, rows, cols, pitch, kin
     g = d[off:off + rows * pitch].view(rows, pitch)
     assert g.data_ptr() % 16 == (d.data_ptr() + off) % 16
     exp_planes = oracle.bitplanes(np.ascontiguousarray(img[:, :cols]), 8)
-    for pred in (1, 0):
-        for store in (True, False):
-            planes, (og, bg), (oe, be) = ctx.encode_gray(g, cols=cols, nplanes=8, predict=bool(pred), store_planes=store)
-            ctx.sync()
-            if store:
-                assert np.array_equal(as_u64(planes), exp_planes)
-            for k in range(8):
-                for coder, out, bits in ((0, og, bg), (1, oe, be)):
-                    eb, est, _ = oracle.encode_plane(exp_planes[k], cols, pred, coder)
-                    nb = int(as_u64(bits)[k])
-                    assert nb == eb, (pred, store, k, coder)
-                    assert stream_bytes(out[k], nb) == est.tobytes(), (pred, store, k, coder)
+    for pred, store, p0, n in ((1, True, 0, 8), (1, False, 0, 8), (0, True, 0, 8), (0, False, 0, 8), (1, False, 2, 3)):
+        planes, (og, bg), (oe, be) = ctx.encode_gray(g, cols=cols, plane0=p0, nplanes=n, predict=bool(pred),
+                                                     store_planes=store)
+        ctx.sync()
+        if store:
+            assert np.array_equal(as_u64(planes), exp_planes[p0:p0 + n])
+        for k in range(n):
+            for coder, out, bits in ((0, og, bg), (1, oe, be)):
+                eb, est, _ = oracle.encode_plane(exp_planes[p0 + k], cols, pred, coder)
+                nb = int(as_u64(bits)[k])
+                assert nb == eb, (pred, store, p0, k, coder)
+                assert stream_bytes(out[k], nb) == est.tobytes(), (pred, store, p0, k, coder)
 
 
 @pytest.mark.parametrize("rows,cols,pitch,plane0,nplanes,kind", [
