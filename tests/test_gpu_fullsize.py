@@ -203,4 +203,11 @@ def test_c3_p5_file_full(ctx, oracle):
     ctx.sync()
     exp_planes = oracle.bitplanes_par(img, 8)
     assert np.array_equal(as_u64(planes), exp_planes)
-    _check_streams(ctx, oracle.encode_planes_par(exp_planes, cols, 1), 8, ((og, bg), (oe, be)))
+    exp = oracle.encode_planes_par(exp_planes, cols, 1)
+    _check_streams(ctx, exp, 8, ((og, bg), (oe, be)))
+    # the bench's c3f step: ONE bic_encode_gray call on the raster where it lies (misaligned count pass)
+    raster = dev[h.data_offset:h.data_offset + rows * cols].view(rows, cols)
+    assert raster.data_ptr() % 16 == 3
+    _, (og2, bg2), (oe2, be2) = ctx.encode_gray(raster, cols=cols, nplanes=8, store_planes=False)
+    ctx.sync()
+    _check_streams(ctx, exp, 8, ((og2, bg2), (oe2, be2)))
