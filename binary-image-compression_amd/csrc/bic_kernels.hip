@@ -453,13 +453,15 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 
 // From the gray image (bic_encode_gray: bitplane_tool.cpp:24-30 and the count pass in one read):
 // one wave per strip of 64 plane words (4096 columns) and gray_rows_per_wave() rows; lane l owns word
-// 64 s + l of strip s: four 16-byte loads give its 64 pixels, K1's 8x8 transposes one word per
-// plane; the plane words are stored and the med residual is formed from the row above (plane
-// words kept in registers) and the pixel left of the word (lane l - 1's last; lane 0 of strip s > 0
-// loads the byte before the strip). One k statistics record per (plane, row, strip) (all planes'
-// records in one transposed pass, strip_records; row_kstats combines a row's strips). The next row's loads are in flight while a row is used.
-// The gray rows must hold used * 64 readable bytes (pitch >= used * 64, 16-byte aligned;
-// gray_rows_supported).
+// 64 s + l of strip s: four 16-byte loads give its 64 pixels (load64_mis when the rows are not
+// 16-byte aligned), K1's 8x8 transposes one word per plane. The med residual (pred.cpp:3-15) needs
+// the row above and the pixel left of the word (lane l - 1's last; lane 0 of strip s > 0 loads the
+// byte before the strip): with prediction and planes = NULL it is formed on the bytes (BYTEMED, one
+// row per wave, the residual planes stored); with the planes returned, from the plane words (four
+// rows per wave, the row above's words carried, the next row's loads in flight); without prediction
+// R = P. One k statistics record per (plane, row,
+// strip) (all planes' records in one transposed pass, strip_records; row_kstats combines a row's
+// strips). The gray rows must hold used * 64 readable bytes (pitch >= used * 64; gray_rows_supported).
 #ifndef BIC_GRAY_ROWS
 #define BIC_GRAY_ROWS 4
 #endif
