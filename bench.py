@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--store-planes", action="store_true",
                     help="c3: bic_encode_gray also returns the 8 bitplanes (planes != NULL; +256 MiB written per "
                          "image); default: planes NULL, the count pass keeps the residual planes for the encoder")
+    ap.add_argument("--no-eg-source", action="store_true",
+                    help="c3 (planes NULL): the round-3 path -- the count pass stores the med residual planes for "
+                         "the encoder -- instead of writing the EG stream and reading the residual rows back from it")
     ap.add_argument("--plane-count", type=int, default=8,
                     help="c3 --shard planes: encode planes 0..P-1 of the image (split over the ranks); P = 1 or 2 at "
                          "N = 1 measures the per-rank step of a plane-sharded 8- or 4-GPU run")
@@ -216,6 +219,10 @@ class C3:
         self.wpr = (self.cols + 63) // 64
         self.separate = args.separate
         self.store_planes = args.store_planes or args.separate
+        # planes NULL: the count pass writes the EG stream and the Golomb emission reads the residual rows
+        # from it (BIC_OPT_EG_SOURCE; off: the residual planes stored in a context buffer)
+        self.eg_src = not self.store_planes and not args.no_eg_source
+        ctx.set_eg_source(self.eg_src)
         self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr) if self.store_planes else None
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
@@ -228,7 +235,9 @@ class C3:
         self.pixels = self.rows * self.cols * self.nplanes
         self.workload = (f"c3: {self.rows}x{self.cols} 8-bit gray -> 8 bitplanes -> med -> per-row runs "
                          f"-> Golomb + EG streams per plane" +
-                         ("" if self.store_planes else " (bitplanes formed in registers, not returned: planes NULL)"))
+                         ("" if self.store_planes else " (bitplanes formed in registers, not returned: planes NULL)") +
+                         (" -- the count pass writes the EG stream, the Golomb emission reads the residual rows "
+                          "from it" if self.eg_src else ""))
 
     def step(self):
         c = self.ctx
@@ -251,9 +260,12 @@ class C3:
         plane_b = self.nplanes * self.rows * self.wpr * 8
         g = int(self.pybic.as_u64(self.bits_g).astype(np.int64).sum()) // 8
         e = int(self.pybic.as_u64(self.bits_e).astype(np.int64).sum()) // 8
-        return {"bitplanes_u8": self.rows * self.cols + plane_b, "bitplanes_count": self.rows * self.cols + plane_b,
+        # EG source: the count pass writes the EG stream (not R) and the emission reads it and writes Golomb
+        return {"bitplanes_u8": self.rows * self.cols + plane_b,
+                "bitplanes_count": self.rows * self.cols + (e if self.eg_src else plane_b),
                 "med_count": plane_b, "golomb_bits": plane_b,
-                "golomb_emit": plane_b + g, "eg_emit": plane_b + e, "encode_rows_golomb_eg": plane_b + g + e}
+                "golomb_emit": plane_b + g, "eg_emit": plane_b + e, "encode_rows_golomb_eg": plane_b + g + e,
+                "encode_rows_golomb_egsrc": e + g}
 
     def host_planes(self, rows):
         if self.planes is None:  # the last step's image's planes (device bitplane kernel), for the CPU leg
@@ -450,6 +462,8 @@ class C3File(C3):
         self.wpr = (self.cols + 63) // 64
         self.separate = args.separate
         self.store_planes = args.separate or args.store_planes
+        self.eg_src = not self.store_planes and not args.no_eg_source
+        ctx.set_eg_source(self.eg_src)
         self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr) if self.store_planes else None
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
@@ -772,11 +786,11 @@ class C1(C3):
         return all((g.cpu().numpy().view(np.uint32)[:nt] == e[:nt]).all() for g, e in zip(self.res, exp))
 
     def cpu_time(self, rows):
-        """the reference's own search loop (oracle/_ref) on the first `rows` rows, extrapolated to
-        the whole image by the exact count of visited windows"""
-        from oracle_lib import Oracle, Ref, have_ref
+        """the oracle's restatement of the reference's search loop on the first `rows` rows,
+        extrapolated to the whole image by the exact count of visited windows"""
+        from oracle_lib import Oracle
         P = np.ascontiguousarray(self.pybic.as_u64(self.planes[0])[:rows])
-        impl, kind = (Ref(), "reference") if have_ref() else (Oracle(), "port")
+        impl, kind = Oracle(), "port"
         t0 = time.perf_counter()
         impl.patch_search(P, self.cols, self.W)
         dt = time.perf_counter() - t0
@@ -824,9 +838,9 @@ class C1M(C1):
                 bool((self.pybic.as_u64(self.resid) == exp["residual"]).all()))
 
     def cpu_time(self, rows):
-        """the driver's loop over the reference's own objects (oracle/_ref), whole image"""
-        from oracle_lib import Oracle, Ref, have_ref
-        impl, kind = (Ref(), "reference") if have_ref() else (Oracle(), "port")
+        """the oracle's restatement of the driver's loop, whole image"""
+        from oracle_lib import Oracle
+        impl, kind = Oracle(), "port"
         t0 = time.perf_counter()
         if kind == "reference":
             impl.match_loop(self.host, self.cols, self.W, self.T, self.R, self.enuml)
@@ -838,10 +852,10 @@ class C1M(C1):
 
 # ------------------------------------------------------------------------------------------
 def cpu_baseline(wl, args):
-    """The reference's own bit-serial med + GolombCoder + EGCoder (oracle/_ref, kind
-    "reference") -- or the oracle restatement ("port") where _ref was not built -- on a bounded
-    sample of the same workload, OpenMP over independent planes, on this host's cores."""
-    from oracle_lib import Oracle, Ref, have_ref
+    """The oracle's restatement of the reference's bit-serial med + GolombCoder + EGCoder (kind
+    "port", the streams written) on a bounded sample of the same workload, OpenMP over independent
+    planes, on this host's cores; plus the word-parallel CPU encoder as `strong`."""
+    from oracle_lib import Oracle
     if isinstance(wl, C1M):
         est, dt, kind = wl.cpu_time(wl.rows)
         return {"value": wl.pixels / est / 1e6, "unit": "MPix/s", "cores": 1, "kind": kind,
@@ -863,18 +877,17 @@ def cpu_baseline(wl, args):
     do_eg = 1 if type(wl) in (C3, C3Planes, C3File) else 0
     predict = 0 if isinstance(wl, C2) else 1
     reps, dt, used = 0, 0.0, 0
+    # the restatement (BASELINE.md's plan): bit-serial med, serial GolombCoder / EGCoder, the streams
+    # written; OpenMP over planes. (The reference's own objects stay an in-container cross-check:
+    # oracle/_ref does not travel to the GPU box.)
+    import ctypes as C
+    o = Oracle()
     while reps == 0 or (dt < args.cpu_seconds and reps < 32):
-        if have_ref():
-            t, _, _, used = Ref().baseline(planes, rows, wl.cols, predict=predict, do_eg=do_eg, threads=threads)
-            kind = "reference"
-        else:
-            import ctypes as C
-            o = Oracle()
-            used_c = C.c_int(0)
-            t0 = time.perf_counter()
-            o.lib.bo_baseline_planes(planes.ctypes.data_as(C.POINTER(C.c_uint64)), nplanes, rows, wl.cols,
-                                     planes.shape[-1], predict, do_eg, C.byref(used_c))
-            t, used, kind = time.perf_counter() - t0, used_c.value, "port"
+        used_c = C.c_int(0)
+        t0 = time.perf_counter()
+        o.lib.bo_baseline_planes(planes.ctypes.data_as(C.POINTER(C.c_uint64)), nplanes, rows, wl.cols,
+                                 planes.shape[-1], predict, do_eg, C.byref(used_c))
+        t, used, kind = time.perf_counter() - t0, used_c.value, "port"
         dt += t
         reps += 1
     px = reps * nplanes * rows * wl.cols
@@ -883,7 +896,8 @@ def cpu_baseline(wl, args):
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
     out = {"value": px / dt / 1e6, "unit": "MPix/s", "cores": int(min(used, nplanes)), "kind": kind,
            "sample": f"{nplanes} planes x {rows} rows x {wl.cols} cols (first {rows} rows of the bench input), "
-                     f"{what}, bit counts as the reference's coders keep them (their writers are commented out), "
+                     f"{what}, the streams written bit by bit (bo_encode_plane, the oracle's restatement of "
+                     f"pred.cpp / GolombCoder.cpp / eg.cpp), "
                      f"OpenMP over planes (one coder per plane: at most {nplanes} threads), {reps} repetitions, "
                      f"{dt:.2f} s",
            "host": host}

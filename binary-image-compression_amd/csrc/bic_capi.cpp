@@ -54,6 +54,7 @@ struct bic_ctx {
   bool single_kernel = false;  // BIC_OPT_SINGLE_KERNEL: the single kernel with decoupled look-backs
   bool force_staged = false;   // BIC_OPT_STAGED: the staged encoder whatever the batch size
   bool one_stream = false;     // BIC_OPT_ONE_STREAM: no second stream for the staged encoder's emission
+  bool eg_src_off = false;     // BIC_OPT_EG_SOURCE = 0: bic_encode_gray* stores R instead of writing EG
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -350,6 +351,10 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
     ctx->one_stream = value != 0;
     return BIC_OK;
   }
+  if (option == BIC_OPT_EG_SOURCE) {
+    ctx->eg_src_off = value == 0;
+    return BIC_OK;
+  }
   return BIC_EINVAL;
 }
 
@@ -400,18 +405,6 @@ size_t bic_encode_slot_words(size_t rows, size_t cols, int coder) {
   if (coder == BIC_CODER_EG) return (size_t)((base + 1 + 63) / 64);
   return (size_t)((2 * base + 63) / 64 + 64);
 }
-
-// staged encoder: rows' shared stream words OR'd into words the prefix kernels zero, or (default)
-// the fragment table and k_fixup -- measured: the atomics cost the C3 emission 244 -> 455 us and C4's
-// 167 -> 262 us. BIC_COUNT_EG: the EG rows' inner words from bic_encode_gray's count pass -- measured
-// at C3: count pass 153 -> 220 us, emission 245 -> 218 us (step 0.455 -> 0.498 ms): off
-#ifndef BIC_ATOM_WORDS
-#define BIC_ATOM_WORDS 0
-#endif
-#ifndef BIC_COUNT_EG
-#define BIC_COUNT_EG 0
-#endif
-constexpr bool kAtomWords = BIC_ATOM_WORDS != 0, kCountEg = BIC_COUNT_EG != 0;
 
 namespace {
 // Packed output where the encoder cannot write it in place (encoders other than the staged one, the
@@ -482,7 +475,6 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     fs.off_g = off_golomb;
     fs.off_e = off_eg;
     fs.index = row_index;
-    fs.atom = kAtomWords;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -555,7 +547,17 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   if (out_golomb && (!bits_golomb || slot_golomb == 0)) return BIC_EINVAL;
   if (out_eg && (!bits_eg || slot_eg == 0)) return BIC_EINVAL;
   if (rows && !gray) return BIC_EINVAL;
-  if (!planes && rows) {
+  const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
+  // EG source: no bitplanes wanted and the EG stream into slots -- the count pass writes the EG
+  // stream (its uniform layout) instead of the residual planes, and the Golomb kernels read the
+  // residual rows back from it (bic_internal.h FusedScratch::eg_src): no residual buffer at all
+  const uint64_t eg_words = ((uint64_t)rows * (cols + 1) + 1 + 63) / 64;
+  const bool fuse = rows && bic::fused_supported(g) && !ctx->force_multipass && !ctx->two_pass && !ctx->single_kernel &&
+                    staged_pays(ctx, g) && bic::med_rows_supported(g, planes, nullptr) &&
+                    bic::gray_rows_supported(g, gray, pitch, planes);
+  const bool eg_src = fuse && !planes && predict && out_eg && !off_eg && bic::gray_eg_supported(g) &&
+                      eg_words <= slot_eg && (out_golomb || !row_index) && !ctx->eg_src_off;
+  if (!planes && rows && !eg_src) {
     // no bitplanes wanted: the count pass stores the med residual planes into the context's buffer
     // (the same bytes the bitplanes would take) and the encoder reads them with prediction off --
     // no row above, no med in the emission. Same streams (predict off on R = med on P).
@@ -570,11 +572,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
     }
   }
   const bool store_resid = !planes && predict;
-  if (!planes) planes = ctx->rbuf;
-  const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
-  const bool fuse = rows && bic::fused_supported(g) && !ctx->force_multipass && !ctx->two_pass && !ctx->single_kernel &&
-                    staged_pays(ctx, g) &&
-                    bic::med_rows_supported(g, planes, nullptr) && bic::gray_rows_supported(g, gray, pitch, planes);
+  if (!planes && !eg_src) planes = ctx->rbuf;
   if (!fuse) {  // the same result through the two separate calls
     if ((rc = bic_bitplanes_u8_range(ctx, gray, pitch, rows, cols, plane0, nplanes, planes, wpr))) return rc;
     return encode_planes_impl(ctx, planes, nplanes, rows, cols, wpr, predict, out_golomb, slot_golomb, bits_golomb,
@@ -588,12 +586,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   fs.off_g = off_golomb;
   fs.off_e = off_eg;
   fs.index = out_golomb ? row_index : nullptr;
-  fs.atom = kAtomWords;
-  // EG rows' inner words from the count pass (plane stride: the slot, or packed, the stream length
-  // of a plane holding a residual 1)
-  const uint64_t eg_words = ((uint64_t)rows * (cols + 1) + 1 + 63) / 64;
-  if (kCountEg && out_eg && bic::gray_eg_supported(g) && eg_words <= slot_eg)
-    fs.eg_cp = off_eg ? eg_words : slot_eg;
+  fs.eg_src = eg_src;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
@@ -602,10 +595,12 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   stage(bic::kFusedPrep);
   timed(ctx, "bitplanes_count", [&] {
     bic::launch_gray_rows(ctx->cur, gray, pitch, g, predict ? 1 : 0, plane0, planes, fs.sones, fs.krec, fs.kpos,
-                          fs.counter, store_resid, fs.eg_cp ? out_eg : nullptr, fs.eg_cp);
+                          fs.counter, store_resid, eg_src ? out_eg : nullptr, slot_eg, eg_src ? fs.jfrag : nullptr);
   });
   timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
-  timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
+  // (EG source: the emission is Golomb's alone, reading the residual rows from the EG stream)
+  timed(ctx, eg_src ? "encode_rows_golomb_egsrc"
+                    : out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
         [&] { stage(bic::kFusedRows); });
   timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
   BIC_HIP(hipGetLastError());
@@ -838,7 +833,7 @@ static int match_encode_impl(bic_ctx* ctx, const uint64_t* plane, size_t rows, s
                              unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
                              uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid,
                              uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats,
-                             int invert, uint8_t* inverted) {
+                             int invert, uint8_t* inverted, int var = 0) {
   int rc = bind(ctx);
   if (rc) return rc;
   if (!plane || !resid || !enuml || !stream_match || !stream_nomatch || !stats || cap_words == 0)
@@ -871,7 +866,8 @@ static int match_encode_impl(bic_ctx* ctx, const uint64_t* plane, size_t rows, s
     BIC_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(uint64_t), ctx->cur));
     return BIC_OK;
   }
-  const bic::MatchSched sched = bic::match_schedule(W, R, (uint32_t)cols, ctx->match_parts);
+  const bic::MatchSched sched = bic::match_schedule(W, R, (uint32_t)cols, ctx->match_parts, (uint32_t)var,
+                                                    (uint32_t)rows);
   if ((rc = ensure_scratch(ctx, bic::match_scratch_bytes(ntiles, sched)))) return rc;
   if (resid != plane)
     BIC_HIP(hipMemcpyAsync(resid, plane, rows * wpr * sizeof(uint64_t), hipMemcpyDeviceToDevice, ctx->cur));
@@ -895,6 +891,7 @@ static int match_encode_impl(bic_ctx* ctx, const uint64_t* plane, size_t rows, s
   a.flags = ctx->flags;
   a.inv = invert ? 1u : 0u;
   a.inverted = inverted;
+  a.var = (uint32_t)var;
   timed(ctx, "match_tiles", [&] { bic::launch_match_tiles(ctx->cur, a, sched, ctx->scratch); });
   timed(ctx, "match_code", [&] {
     bic::launch_match_code(ctx->cur, a, reinterpret_cast<unsigned long long*>(stream_match),
@@ -918,6 +915,18 @@ int bic_match_encode_inv(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_
                          uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats) {
   return match_encode_impl(ctx, plane, rows, cols, wpr, W, T, R, enuml, besti, bestj, bestd, weights, modes, resid,
                            stream_match, stream_nomatch, cap_words, stats, 1, inverted);
+}
+
+int bic_match_encode_var(bic_ctx* ctx, int variant, const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
+                         unsigned W, unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                         uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid, uint64_t* stream_match,
+                         uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats) {
+  if (variant == 7 || variant == 8)
+    return match_encode_impl(ctx, plane, rows, cols, wpr, W, T, R, enuml, besti, bestj, bestd, weights, modes, resid,
+                             stream_match, stream_nomatch, cap_words, stats, variant == 8, nullptr);
+  if (variant < 4 || variant > 6) return BIC_EINVAL;
+  return match_encode_impl(ctx, plane, rows, cols, wpr, W, T, R, enuml, besti, bestj, bestd, weights, modes, resid,
+                           stream_match, stream_nomatch, cap_words, stats, 0, nullptr, variant);
 }
 
 int bic_set_match_parts(bic_ctx* ctx, unsigned parts) {

@@ -556,12 +556,11 @@ __device__ __forceinline__ bool word_complete(uint64_t w, uint64_t G, uint64_t L
   return w * 64 >= G && w * 64 + 64 <= G + L;
 }
 
-// A word the row shares with a neighbouring row: into the fragment table (k_fixup combines them),
-// or -- frag null, the staged encoder -- OR'd straight into the stream word, which the prefix
-// kernels zeroed (k_scan_rows / k_rebase_zero), so no fixup launch is needed.
+// A word the row shares with a neighbouring row: into the fragment table (k_fixup combines them).
 __device__ __forceinline__ void put_shared(uint64_t* out, uint64_t wi, uint64_t* frag, int which, uint64_t v) {
-  if (frag) frag[which] = v;
-  else if (v) atomicOr(reinterpret_cast<unsigned long long*>(out + wi), (unsigned long long)bswap64(v));
+  (void)out;
+  (void)wi;
+  frag[which] = v;
 }
 
 // Write a row image of L bits to absolute bit G of out (threads tid of nt: a wave's lanes by
@@ -635,11 +634,13 @@ struct FusedArgs {
   uint64_t* off_g;
   uint64_t* off_e;
   uint64_t* index;  // FusedScratch::index
-  bool atom;        // FusedScratch::atom (staged encoder): shared words OR'd into pre-zeroed stream words
-  uint64_t eg_cp;   // FusedScratch::eg_cp: the count pass wrote the EG rows' inner words (plane stride, words)
+  // bic_encode_gray without planes (FusedScratch::eg_src): the count pass wrote the EG stream in its
+  // uniform layout and the residual rows are read back from it (null: residual from planes)
+  const uint64_t* esrc;
+  uint64_t* jfrag;  // the count pass's strip-edge fragments (2 per plane, row, strip)
+  uint64_t* efix;   // per plane: the EG bit to clear after the emission (eg_fix_bit)
 #ifdef BIC_STAMPS
   int known;
-  int dbg;  // diagnostic (BIC_EMIT_DBG): k_emit_known skips 1 = LDS-image Golomb rows, 2 = EG rows, 4 = k = 0 copies
 #endif
 };
 
@@ -648,6 +649,59 @@ struct FusedArgs {
 __device__ __forceinline__ uint64_t gb_abs(const FusedArgs& a, uint64_t id, uint32_t plane) {
   const uint64_t G = a.gboff[id];
   return a.off_g ? G - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G;
+}
+
+// ---- residual rows read back from the EG stream (FusedArgs::esrc) ------------------------------
+// bic_encode_gray without planes: the count pass (k_gray_strips, EGS) writes each plane's EG stream
+// (eg.cpp:20-37 with the block size fixed at 1: per row ~R, then the end-of-row '1') in its uniform
+// layout -- bit 0 a '1', row r at bit r (cols + 1) + 1 -- instead of storing R: that layout is the
+// stream itself but for ONE bit, cleared after the emission (eg_fix_bit). Every reader of R takes
+// the row from there: ~(64 stream bits at the row's offset + 64 w), a wave-uniform funnel shift.
+__device__ __forceinline__ uint64_t eg_src_bit0(const Geom& g, uint32_t row) {
+  return (uint64_t)row * (g.cols + 1) + 1;
+}
+// residual word w of a row (any lane pattern; two loads, the second one usually a cache hit)
+__device__ __forceinline__ uint64_t eg_src_word(const uint64_t* eplane, const Geom& g, uint32_t row, uint32_t w) {
+  if (w >= g.used) return 0;
+  const uint64_t b = eg_src_bit0(g, row) + (uint64_t)w * 64;
+  const uint64_t* p = eplane + (b >> 6);
+  const uint32_t sh = (uint32_t)(b & 63);
+  const uint64_t hi = bswap64(p[0]);
+  const uint64_t x = sh ? funnel64(hi, bswap64(p[1]), 64 - sh) : hi;
+  return ~x & (w == g.used - 1 ? g.trail : ~0ull);
+}
+// the row's words t * 64 + lane (t < WPL) as resid_row gives them: one load per word, lane l + 1's word
+// through DPP (wave_shl:1), lane 63's from lane 0 of the next word group (the last: one uniform load)
+template <int WPL>
+__device__ __forceinline__ void eg_src_row(const uint64_t* eplane, const Geom& g, uint32_t row, uint64_t (&r)[WPL]) {
+  const int lane = lane_id();
+  const uint64_t b = eg_src_bit0(g, row);
+  const uint64_t* p = eplane + (b >> 6);
+  const uint32_t sh = (uint32_t)(b & 63);
+  const uint32_t nw = g.used;  // stream words used: nw (+ 1 when sh != 0)
+  uint64_t v[WPL];
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t j = t * 64 + lane;
+    v[t] = j < nw ? p[j] : 0;
+  }
+  const uint64_t last = sh ? p[nw] : 0;  // (uniform address)
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t j = t * 64 + lane;
+    const uint64_t hi = bswap64(v[t]);
+    uint64_t nx = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v[t] >> 32), 0x130, 0xf, 0xf, true) << 32) |
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v[t], 0x130, 0xf, 0xf, true);
+    if (lane == 63) {
+      if (t + 1 < WPL && (t + 1) * 64 < (int)nw)
+        nx = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v[t + 1 < WPL ? t + 1 : t] >> 32), 0) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v[t + 1 < WPL ? t + 1 : t], 0);
+      else
+        nx = last;
+    }
+    const uint64_t x = sh ? funnel64(hi, bswap64(nx), 64 - sh) : hi;
+    r[t] = j < nw ? ~x & (j == nw - 1 ? g.trail : ~0ull) : 0;
+  }
 }
 
 // Global-memory emission for a row whose Golomb image does not fit the LDS window: codeword
@@ -716,7 +770,8 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
   uint64_t carry = G;
   for (uint32_t w0 = 0; w0 < g.used; w0 += 64) {
     const uint32_t w = w0 + lane;
-    const uint64_t x = resid_word<PREDICT>(rc, g, row, w);
+    const uint64_t x = (!PREDICT && a.esrc) ? eg_src_word(a.esrc + (uint64_t)plane * a.slot_e, g, row, w)
+                                            : resid_word<PREDICT>(rc, g, row, w);
     uint32_t n;
     int jp;
     step_prefix(x, w, st, n, jp);
@@ -736,14 +791,25 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
     tl |= shfl_u64(tl, lane ^ d);
   }
   if (lane == 0) {
-    if (hpart) put_shared(a.out_g, wh, a.atom ? nullptr : frag, 0, h | (wh == wt ? tl : 0));
-    if (tpart && wt != wh) put_shared(a.out_g, wt, a.atom ? nullptr : frag, 1, tl);
+    if (hpart) put_shared(a.out_g, wh, frag, 0, h | (wh == wt ? tl : 0));
+    if (tpart && wt != wh) put_shared(a.out_g, wt, frag, 1, tl);
   }
+}
+
+// EG source: after every reader of the residual rows, the one bit per plane in which the uniform
+// layout differs from the EG stream (eg_src_junctions' ONES scan found it: the first 1's bit, or the
+// layout's bit past the end of a plane without 1s) is cleared.
+__device__ __forceinline__ void eg_fix_bit(const FusedArgs& a) {
+  if (!a.esrc || blockIdx.x != 0 || threadIdx.x >= a.g.nplanes) return;
+  const uint64_t P = a.efix[threadIdx.x];
+  uint64_t* w = a.out_e + (uint64_t)threadIdx.x * a.slot_e + (P >> 6);
+  *w &= ~bswap64(BIC_MSB >> (P & 63));
 }
 
 template <bool PREDICT>
 __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
   const int lane = lane_id();
+  eg_fix_bit(a);
   const uint32_t nslow = *a.slow_n;
   for (uint32_t li = blockIdx.x * 4 + (threadIdx.x >> 6); li < nslow; li += gridDim.x * 4)
     row_global<PREDICT>(a, a.slow_ids[li], lane);
@@ -1140,44 +1206,6 @@ __device__ __forceinline__ void eg_row_regs(const uint64_t (&rr)[WPL], const Geo
   }
 }
 
-// The words of an EG row (after the plane's first 1) that the count pass leaves out when it wrote
-// the rest (k_gray_strips, EGW): with g = Ge % 64 != 0, the word across each strip edge (plain store)
-// and the row's first and last words (shared with the neighbouring rows: to the fragment table, or
-// OR'd into the words the prefix kernels zeroed; a last word the row fills, g = 63, is its own);
-// with g = 0 only the end-of-row '1' that opens the next word. Lane 0's work, from the edge lanes'
-// words.
-template <int WPL>
-__device__ __forceinline__ void eg_row_edges(const uint64_t (&rr)[WPL], const Geom& g, uint64_t Ge, uint64_t* out,
-                                             uint64_t* frag) {
-  const uint32_t sh = (uint32_t)(Ge & 63);
-  const uint64_t w0 = Ge >> 6;
-  const uint32_t nt = g.used / 64;  // whole strips (gray_eg_supported)
-  uint64_t last = 0;
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) {
-    if (t >= (int)nt) break;
-    const uint64_t x = rr[t];
-    const uint64_t e0 = ~(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), 0) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 0));
-    if (sh && lane_id() == 0) {
-      if (t == 0) put_shared(out, w0, frag, 0, e0 >> sh);
-      else out[w0 + 64 * t] = bswap64((last << (64 - sh)) | (e0 >> sh));
-    }
-    last = ~lane63_u64(x);
-  }
-  if (lane_id() == 0) {
-    const uint64_t v = sh ? (last << (64 - sh)) | (BIC_MSB >> sh) : BIC_MSB;
-    if (sh == 63) out[w0 + g.used] = bswap64(v);  // the row ends with the word: not shared, not zeroed
-    else put_shared(out, w0 + g.used, frag, 1, v);
-  }
-}
-
-// whether the count pass's EG words of this plane lie where the row offsets say (every earlier plane
-// of a packed stream held a residual 1; slot mode: always)
-__device__ __forceinline__ bool eg_base_ok(const FusedArgs& a, uint32_t plane) {
-  return !a.ebase || a.ebase[plane] == (uint64_t)plane * a.eg_cp * 64;
-}
-
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * kWin];
@@ -1331,13 +1359,35 @@ __device__ __forceinline__ bool row_class(const FusedArgs& a, uint64_t id, uint3
   return true;
 }
 
-// Zero the stream words a row of L bits at absolute bit G shares with its neighbours (its first
-// word when it starts inside one, its last when it ends inside one); they are OR'd by the emission
-// launches afterwards (FusedScratch::atom). Both rows at a boundary zero the same word: same value.
-__device__ __forceinline__ void zero_shared(uint64_t* out, uint64_t G, uint64_t L) {
-  if (!L) return;
-  if (G & 63) out[G >> 6] = 0;
-  if ((G + L) & 63) out[(G + L - 1) >> 6] = 0;
+// EG source (FusedArgs::esrc): the stream words the count pass left as fragments -- one where each
+// strip of row r starts (the previous strip's or row's tail, this strip's head; row 0's strip 0 after
+// the stream's first bit, a '1') and the word holding the last row's end-of-row '1' -- assembled by
+// the thread of row r in the ONES scan (k_gray_strips writes jfrag[2 s] = head, jfrag[2 s + 1] = tail,
+// the last strip's tail with the end-of-row '1'). A strip starting on a word boundary has no head;
+// its predecessor's tail is then a whole word (the row ended at bit 63), stored here.
+__device__ __forceinline__ void eg_src_junctions(const FusedArgs& a, uint32_t plane, uint32_t r) {
+  const Geom& g = a.g;
+  const uint32_t ns = a.ns;
+  uint64_t* eo = a.out_e + (uint64_t)plane * a.slot_e;
+  const uint64_t* jf = a.jfrag + 2 * ((uint64_t)plane * g.rows + r) * ns;
+  uint64_t hd[kMaxStrips], tl[kMaxStrips];
+#pragma unroll
+  for (uint32_t s = 0; s < kMaxStrips; ++s) {
+    hd[s] = s < ns ? jf[2 * s] : 0;
+    tl[s] = s < ns ? jf[2 * s + 1] : 0;
+  }
+  uint64_t prev = r ? jf[-1] : BIC_MSB;  // (row r - 1's last tail)
+  const uint64_t B = eg_src_bit0(g, r);
+#pragma unroll
+  for (uint32_t s = 0; s <= kMaxStrips; ++s) {
+    const bool end = s == ns;  // the word after the row: only for the last row
+    if (s > ns || (end && r + 1 != g.rows)) break;
+    const uint64_t bb = end ? B + g.cols + 1 : B + (uint64_t)s * 4096;
+    const uint64_t v = prev | (end ? 0 : hd[s]);
+    if (bb & 63) eo[bb >> 6] = bswap64(v);
+    else if (s == 0 || end) eo[(bb >> 6) - 1] = bswap64(prev);
+    if (!end) prev = tl[s];
+  }
 }
 
 // Packed output: the planes' start words in each coder's buffer (streams word-aligned, plane order:
@@ -1454,18 +1504,36 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
           if (walk) a.walk_ids[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)(base + r);
         }
       }
-      // the row holding the plane's first 1 (EG inserts a '0' after it): listed for REST here unless
-      // walked (k_row_walk lists it)
-      if (in && pre == 0 && v[i] > 0 && !walk) a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)(base + r);
-      if (in && a.atom && a.out_e && !a.ebase) {  // slot mode: the row's shared EG words (offsets in closed form)
-        const uint64_t cap = a.slot_e * 64;
-        const uint64_t Ge = (uint64_t)r * (g.cols + 1) + (pre > 0 ? 1 : 0);
-        const uint64_t Le = (uint64_t)g.cols + 1 + (pre == 0 && v[i] > 0 ? 1 : 0);
-        if (Ge + Le <= cap) zero_shared(a.out_e + (uint64_t)plane * a.slot_e, Ge, Le);
+      const bool first1 = in && pre == 0 && v[i] > 0;  // the row holding the plane's first 1
+      if (a.esrc) {
+        if (in) eg_src_junctions(a, plane, r);
+        // EG source: the stream bit eg.cpp's first-run '0' makes differ from the uniform layout: the
+        // first 1's own bit (the layout has a '1' there, the shifted ~R of the pixel before it)
+        if (first1) {
+          const uint32_t* so = a.sones + (base + r) * a.ns;
+          const uint32_t* kp = a.kpos + (base + r) * a.ns;
+          uint32_t j1 = 0;
+          for (uint32_t q = 0; q < a.ns; ++q)
+            if (so[q]) {
+              j1 = kp[q] & 0xffffu;
+              break;
+            }
+          a.efix[plane] = (uint64_t)r * (g.cols + 1) + j1;
+        }
+      } else if (first1 && !walk && a.out_e) {
+        // (EG inserts a '0' after it): listed for REST here unless walked (k_row_walk's list)
+        a.rest_ids[atomicAdd(a.counter + 3, 1u)] = (uint32_t)(base + r);
       }
       pre += v[i];
     }
-    if (b == nb - 1 && threadIdx.x == 0) a.pones[plane] = btot + tot;  // the plane's residual 1s
+    if (b == nb - 1 && threadIdx.x == 0) {
+      const uint64_t po = btot + tot;
+      a.pones[plane] = po;  // the plane's residual 1s
+      if (a.esrc) {  // the EG length (eg.cpp: rows (cols + 1), + 1 for the first run's g = 1 bit)
+        a.bits_e[plane] = (uint64_t)g.rows * (g.cols + 1) + (po ? 1 : 0);
+        if (!po) a.efix[plane] = (uint64_t)g.rows * (g.cols + 1);  // no 1: the layout's last bit is past the end
+      }
+    }
   } else {
     const uint64_t cap = a.slot_g * 64;
 #pragma unroll
@@ -1480,8 +1548,6 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
         if (pre + v[i] > cap) {
           a.glen[base + r] = 0;  // overflowed: nothing written, fixup skips
           atomicOr(&a.flags[0], 1u);
-        } else if (a.atom && !a.off_g) {
-          zero_shared(a.out_g, (uint64_t)plane * cap + pre, v[i]);  // slot mode (packed: k_rebase_zero)
         }
       }
       pre += v[i];
@@ -1539,7 +1605,8 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     const uint32_t O = a.row_o[id];
     uint64_t rr[1];
-    resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
+    if (!PREDICT && a.esrc) rr[0] = eg_src_word(a.esrc + (uint64_t)plane * a.slot_e, g, row, w);
+    else resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
     const WideRow p = wide_prefix(rr[0], w, O + row, sh);
     uint32_t kor = 0;
     uint32_t ll = word_len(rr[0], w, p.n, p.jp, row * (g.cols + 1), w == g.used - 1, g.cols, kor);
@@ -1575,10 +1642,6 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
 // tables are staged (XCD-remapped block order: the waves of one XCD hold consecutive rows, the
 // row above is an L2 hit).
 constexpr int kEmitWaves = 4;
-#ifndef BIC_EMIT_PREFETCH
-#define BIC_EMIT_PREFETCH 0  // measured slower (C3 emission 238 -> 248 us): off
-#endif
-constexpr bool kEmitPrefetch = BIC_EMIT_PREFETCH != 0;  // next row loaded during this one (no prediction)
 #ifndef BIC_REST_AUX
 #define BIC_REST_AUX 1
 #endif
@@ -1594,10 +1657,7 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
   const uint64_t L = Lf & kLenMask;
   const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
-  bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
-#ifdef BIC_STAMPS
-  if (a.dbg & 1) gk1 = false;
-#endif
+  const bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
   if (gk1) {  // zero the Golomb image
     uint4* z = reinterpret_cast<uint4*>(gimg);
     for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
@@ -1609,18 +1669,13 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
     for (int t = 0; t < WPL; ++t) ones += (uint32_t)__popcll(rr[t]);
     f_here = wave_sum_u32(ones) > 0;
   }
-#ifdef BIC_STAMPS
-  if (!(a.dbg & 2))
-#endif
   if constexpr (DO_E) {  // EG as written (eg.cpp:20-37): per row ~R then '1'; a '0' after the plane's first 1
     const uint64_t Le = (uint64_t)g.cols + 1 + (f_here ? 1 : 0);
     const uint64_t Ge_rel = (uint64_t)row * (g.cols + 1) + (O > 0 ? 1 : 0);
     const uint64_t cap = a.slot_e * 64;
     const uint64_t Ge = Eb + Ge_rel;
     if (Ge_rel + Le <= cap) {
-      if (a.eg_cp && O > 0 && eg_base_ok(a, plane))
-        eg_row_edges<WPL>(rr, g, Ge, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
-      else if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.atom ? nullptr : a.efrag + 2 * id);
+      if (!f_here) eg_row_regs<WPL>(rr, g, Ge, Le, a.out_e, a.efrag + 2 * id);
       if (lane == 0) {
         a.eboff[id] = Ge;
         a.elen[id] = Le;
@@ -1639,10 +1694,7 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
 #endif
   if constexpr (DO_G) {
     if (k0 && L) {
-#ifdef BIC_STAMPS
-      if (!(a.dbg & 4))
-#endif
-      eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
+      eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.gfrag + 2 * id);
     } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
       uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
       int jpc = -1;
@@ -1670,7 +1722,7 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
       if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      write_row64(img, L, Gb, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id);
+      write_row64(img, L, Gb, a.out_g, a.gfrag + 2 * id);
     }
     if (lane == 0) {
       // glen keeps its flags: k_emit_rest (on the other stream) reads them too
@@ -1681,7 +1733,8 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
   }
 }
 
-template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
+// ES: the residual rows from the EG stream the count pass wrote (FusedArgs::esrc; PREDICT false)
+template <int WPL, bool PREDICT, bool DO_G, bool DO_E, bool ES = false>
 __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * kGImg];
   __shared__ uint32_t s_lut[512];
@@ -1696,46 +1749,25 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   // persistent waves: rows id, id + stride, ...
   const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
   const uint64_t id0 = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
-  // Without prediction (the residual planes bic_encode_gray's count pass stores) a row is its WPL
-  // words alone: the next row's words and metadata are loaded while this one is coded (8 VGPRs at
-  // WPL = 4, within the kernel's 4 waves per SIMD), so a wave always has a row in flight.
-  constexpr bool kPre = kEmitPrefetch && !PREDICT;
-  uint64_t pp_[WPL];
-  uint32_t pO = 0;
-  uint64_t pLf = 0, pGb = 0;
-  auto fetch = [&](uint64_t fid) {
-    const uint32_t fplane = (uint32_t)(fid / g.rows), frow = (uint32_t)(fid % g.rows);
-    uint64_t dummy[WPL];
-    row_load<WPL, false>(a.planes, g, fplane, frow, pp_, dummy);
-    pO = a.row_o[fid];
-    pLf = DO_G ? a.glen[fid] : 0;
-    pGb = DO_G ? gb_abs(a, fid, fplane) : 0;
-  };
-  if (kPre && id0 < nrows) fetch(id0);
   for (uint64_t id = id0; id < nrows; id += stride) {
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     STAMP(0);
-    uint64_t cp_[WPL], cu_[WPL];
+    uint64_t rr[WPL];
     uint32_t O;
     uint64_t Lf, Gb;
-    if constexpr (kPre) {
-#pragma unroll
-      for (int t = 0; t < WPL; ++t) {
-        cp_[t] = pp_[t];
-        cu_[t] = 0;
-      }
-      O = pO;
-      Lf = pLf;
-      Gb = pGb;
-      if (id + stride < nrows) fetch(id + stride);
+    if constexpr (ES) {
+      eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
+      O = a.row_o[id];
+      Lf = DO_G ? a.glen[id] : 0;
+      Gb = DO_G ? gb_abs(a, id, plane) : 0;
     } else {
+      uint64_t cp_[WPL], cu_[WPL];
       row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_, cu_);
       O = a.row_o[id];
       Lf = DO_G ? a.glen[id] : 0;
       Gb = DO_G ? gb_abs(a, id, plane) : 0;  // loaded with the row, not after the branch that uses it
+      row_resid<WPL, PREDICT>(g, row, cp_, cu_, rr);
     }
-    uint64_t rr[WPL];
-    row_resid<WPL, PREDICT>(g, row, cp_, cu_, rr);
     const uint64_t Eb = DO_E ? (a.ebase ? a.ebase[plane] : (uint64_t)plane * a.slot_e * 64) : 0;
     emit_known_row<WPL, PREDICT, DO_G, DO_E>(a, id, plane, row, rr, O, Lf, Gb, Eb, gimg, s_lut);
     STAMP(2);
@@ -1743,7 +1775,6 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
     __builtin_amdgcn_wave_barrier();
   }
 }
-
 
 // The rows the prefix kernels leave to this launch: Golomb rows with mixed k (per-codeword k,
 // encode_word; among the walked rows, counter[2]) and the EG row holding the plane's first 1 (with
@@ -1776,11 +1807,12 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
     const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0;
     if (i >= nrest) {  // a walked row: skip it unless mixed or the first-1 row (uniform over the workgroup)
       const uint64_t onext = row + 1 < g.rows ? a.row_o[id + 1] : a.pones[plane];
-      if (!(L && !k0 && !k1) && !(O == 0 && onext > 0)) continue;
+      if (!(L && !k0 && !k1) && !(DO_E && O == 0 && onext > 0)) continue;
     }
     const bool gmix = DO_G && L && !k0 && !k1 && L <= kCapBits;
     uint64_t rr[1];
-    resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
+    if (!PREDICT && a.esrc) rr[0] = eg_src_word(a.esrc + (uint64_t)plane * a.slot_e, g, row, w);
+    else resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
     const uint64_t x = rr[0];
     const WideRow p = wide_prefix(x, w, O + row, sh);
     const bool f_here = DO_E && O == 0 && p.ones > 0;
@@ -1809,7 +1841,7 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
       const uint64_t cap = a.slot_e * 64;
       if (Ge_rel + Le <= cap)
         write_row(eimg, Le, (a.ebase ? a.ebase[plane] : (uint64_t)plane * cap) + Ge_rel, (int64_t)fcol + 1, a.out_e,
-                  a.atom ? nullptr : a.efrag + 2 * id, threadIdx.x, blockDim.x);
+                  a.efrag + 2 * id, threadIdx.x, blockDim.x);
     }
     if (gmix) {
       const uint32_t arow = row * (g.cols + 1);
@@ -1834,7 +1866,7 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
       }
       __syncthreads();
       if (threadIdx.x == 0 && tot != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-      write_row(gimg, L, gb_abs(a, id, plane), -1, a.out_g, a.atom ? nullptr : a.gfrag + 2 * id, threadIdx.x,
+      write_row(gimg, L, gb_abs(a, id, plane), -1, a.out_g, a.gfrag + 2 * id, threadIdx.x,
                 blockDim.x);
     }
     __syncthreads();  // the images and sh are reused by the next row
@@ -1844,22 +1876,6 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
 __global__ __launch_bounds__(1024) void k_plane_bases(FusedArgs a) {
   __shared__ uint64_t tmp[17];
   plane_bases(a, tmp);
-}
-
-// Packed output with FusedScratch::atom: the rows' shared words of both packed streams are zeroed
-// here (their offsets are final only now).
-__global__ __launch_bounds__(256) void k_shift_gboff(FusedArgs a) {
-  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (id >= (uint64_t)a.g.rows * a.g.nplanes) return;
-  const uint32_t plane = (uint32_t)(id / a.g.rows), row = (uint32_t)(id % a.g.rows);
-  if (a.off_g) zero_shared(a.out_g, gb_abs(a, id, plane), a.glen[id] & kLenMask);  // (0 when the row overflowed)
-  if (a.off_e && a.atom) {
-    const uint32_t O = a.row_o[id];
-    const uint32_t onext = row + 1 < a.g.rows ? a.row_o[id + 1] : (uint32_t)a.pones[plane];
-    const uint64_t Ge_rel = (uint64_t)row * (a.g.cols + 1) + (O > 0 ? 1 : 0);
-    const uint64_t Le = (uint64_t)a.g.cols + 1 + (O == 0 && onext > 0 ? 1 : 0);
-    if (Ge_rel + Le <= a.slot_e * 64) zero_shared(a.out_e, a.ebase[plane] + Ge_rel, Le);
-  }
 }
 
 // Combine the fragments of the words rows share: the row holding a shared word's first bit
@@ -1917,7 +1933,8 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024 + (size_t)g.nplanes * 8 * 3 + 64;
+  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024 + (size_t)g.nplanes * 8 * 4 + 64 +
+         n * kMaxStrips * 16;  // (jfrag: the EG source's strip-edge fragments)
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -1949,6 +1966,8 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
     fs.pones = reinterpret_cast<uint64_t*>(e);
     fs.gbase = fs.pones + g.nplanes;
     fs.ebase = fs.gbase + g.nplanes;
+    fs.efix = fs.ebase + g.nplanes;
+    fs.jfrag = fs.efix + g.nplanes;
   }
   fs.ns = 1;
   fs.counted = false;
@@ -1984,23 +2003,28 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   a.off_e = out_e ? fs.off_e : nullptr;
   a.ebase = a.off_e ? fs.ebase : nullptr;
   a.index = out_g ? fs.index : nullptr;
-  a.atom = fs.atom && mode == kEncStaged;
-  a.eg_cp = mode == kEncStaged && out_e ? fs.eg_cp : 0;
+  // EG source (bic_encode_gray without planes): the count pass wrote the EG stream, the emission is
+  // Golomb's alone and reads the residual rows from it
+  const bool es = mode == kEncStaged && fs.eg_src && out_e && !a.off_e && !predict;
+  a.esrc = es ? out_e : nullptr;
+  a.jfrag = es ? fs.jfrag : nullptr;
+  a.efix = es ? fs.efix : nullptr;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
-  a.dbg = getenv("BIC_EMIT_DBG") ? atoi(getenv("BIC_EMIT_DBG")) : 0;
 #endif
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t grid = (uint32_t)((g.rows + kTileRows - 1) / kTileRows * (uint64_t)g.nplanes);  // one per tile
   const uint32_t egrid = (uint32_t)((nrows + kTileRows - 1) / kTileRows);                       // one per 8 rows
-  const bool dg = out_g != nullptr, de = out_e != nullptr;
+  const bool dg = out_g != nullptr, de = out_e != nullptr && !es;  // de: the emission writes EG
   const uint32_t fgrid = (uint32_t)((nrows + 255) / 256);
   if (stage == kFusedFinish) {
-    if (dg) {  // a fixed small grid walks the list of LDS-overflow rows (usually empty)
-      if (predict) k_rows_global<true><<<256, 256, 0, s>>>(a);
-      else k_rows_global<false><<<256, 256, 0, s>>>(a);
+    // a fixed small grid walks the list of LDS-overflow rows (usually empty); block 0 also clears
+    // the EG source's one bit per plane (eg_fix_bit)
+    if (dg || es) {
+      if (predict) k_rows_global<true><<<dg ? 256 : 1, 256, 0, s>>>(a);
+      else k_rows_global<false><<<dg ? 256 : 1, 256, 0, s>>>(a);
     }
-    if (a.atom) return;  // shared words already OR'd into their zeroed stream words
+    if (!dg && !de) return;
     k_fixup<<<dg && de ? 2 * fgrid : fgrid, 256, 0, s>>>(dg ? fs.gboff : fs.eboff, dg ? fs.glen : fs.elen,
                                                         dg ? fs.gfrag : fs.efrag, dg ? out_g : out_e,
                                                         fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows,
@@ -2026,9 +2050,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       // -- as the LEN scan's last workgroup instead, its device-scope release fences (an L2 write-back
       // per workgroup) made C4's prefix 99 -> 153 us
       if (a.off_g || a.off_e) k_plane_bases<<<1, 1024, 0, s>>>(a);
-      if ((a.off_g || a.off_e) && a.atom) k_shift_gboff<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
       return;
     }
+    if (!dg && !de) return;  // EG source without Golomb: the count pass and the ONES scan wrote it all
     // persistent grids (more rows per wave when the image is larger)
     static thread_local int cus = 0;
     if (!cus) {
@@ -2055,16 +2079,19 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     if (kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
         hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
       rs = fs.aux;
-#define BIC_EMIT1(W, P, DG, DE)                                                                        \
+#define BIC_EMIT1(W, P, DG, DE, ES)                                                                    \
   {                                                                                                  \
     k_emit_rest<P, DG, DE><<<rgrid, 64 * nwv, 0, rs>>>(a);                                           \
-    static const int occ_ = occ_of(reinterpret_cast<const void*>(&k_emit_known<W, P, DG, DE>));   \
-    k_emit_known<W, P, DG, DE><<<egrid_of(occ_), 64 * kEmitWaves, 0, s>>>(a);                        \
+    static const int occ_ = occ_of(reinterpret_cast<const void*>(&k_emit_known<W, P, DG, DE, ES>));  \
+    k_emit_known<W, P, DG, DE, ES><<<egrid_of(occ_), 64 * kEmitWaves, 0, s>>>(a);                    \
   }
 #define BIC_EMIT(W, P)                                                                                \
-  if (dg && de) BIC_EMIT1(W, P, true, true) else if (dg) BIC_EMIT1(W, P, true, false) else BIC_EMIT1(W, P, false, true)
+  if (dg && de) BIC_EMIT1(W, P, true, true, false) else if (dg) BIC_EMIT1(W, P, true, false, false) else BIC_EMIT1(W, P, false, true, false)
     if (predict) {
       if (wpl == 1) { BIC_EMIT(1, true); } else if (wpl == 2) { BIC_EMIT(2, true); } else { BIC_EMIT(4, true); }
+    } else if (es) {  // Golomb alone, the residual rows from the EG stream
+      if (wpl == 1) { BIC_EMIT1(1, false, true, false, true); } else if (wpl == 2) { BIC_EMIT1(2, false, true, false, true); }
+      else { BIC_EMIT1(4, false, true, false, true); }
     } else {
       if (wpl == 1) { BIC_EMIT(1, false); } else if (wpl == 2) { BIC_EMIT(2, false); } else { BIC_EMIT(4, false); }
     }

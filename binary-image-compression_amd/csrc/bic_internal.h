@@ -134,13 +134,14 @@ struct FusedScratch {
   // row index for the decoders (bic_row_index): per row, the bit offset of its first Golomb
   // codeword in its plane's stream and the residual 1s of the plane before it; null: not written
   uint64_t* index = nullptr;
-  // staged encoder with output: the prefix kernels zero the stream words rows share and the
-  // emission launches OR their parts into them (no fragment table, no fixup launch)
-  bool atom = false;
-  // the count pass (launch_gray_rows with out_e) already wrote the EG words inside every row at
-  // plane stride eg_cp words, laid out as if every plane held a residual 1; the emission then writes
-  // only the words at strip edges and row ends of rows after the plane's first 1 (0: off)
-  uint64_t eg_cp = 0;
+  // EG source (bic_encode_gray without planes, slot output): the count pass (launch_gray_rows with
+  // out_e) wrote the EG stream in its uniform layout (row r at bit r (cols + 1) + 1) instead of the
+  // residual planes, leaving the words across strip edges as fragments in jfrag (2 per plane, row,
+  // strip); the ONES scan assembles those, the Golomb kernels read the residual rows back from the
+  // stream, and one bit per plane (efix) is cleared after them (bic_fused.hip eg_src_junctions)
+  bool eg_src = false;
+  uint64_t* jfrag = nullptr;
+  uint64_t* efix = nullptr;
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
@@ -167,11 +168,14 @@ void launch_row_ones(hipStream_t s, const Geom& g, const uint64_t* planes, int p
 bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const void* planes);
 uint32_t gray_strips(const Geom& g);
 // store_resid: the words stored are the med residual R (planes = the caller's bitplanes are not
-// wanted; the encoder then reads R with predict off), not the bitplanes P
+// wanted; the encoder then reads R with predict off), not the bitplanes P. out_e (with predict, the
+// bitplanes not wanted): the EG stream instead of R (FusedScratch::eg_src; slot eg_stride words,
+// strip-edge fragments to jfrag); planes is then unused
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero,
-                      bool store_resid = false, uint64_t* out_e = nullptr, uint64_t eg_stride = 0);
-// the count pass can write the EG interior words (FusedScratch::eg_cp): rows of whole strips only
+                      bool store_resid = false, uint64_t* out_e = nullptr, uint64_t eg_stride = 0,
+                      uint64_t* jfrag = nullptr);
+// the count pass can write the EG stream (FusedScratch::eg_src): rows of whole 64-word strips only
 bool gray_eg_supported(const Geom& g);
 
 void launch_patch_search(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t cols, uint32_t wpr,
@@ -196,6 +200,10 @@ struct MatchArgs {
   uint32_t* flags;
   uint32_t inv;                     // compress8_test.cpp's patch inversion (0: compress7_test.cpp)
   uint8_t* inverted;                // per tile: the patch was flipped (nullable)
+  // the loop of compress4_test.cpp (4), compress5_test.cpp (5), compress6_test.cpp (6); 0: compress7/8
+  // (per-tile schedule only)
+  uint32_t var;
+  unsigned long long* key2;         // scratch, variant 5: per tile the first window with d < W*W/2
 };
 constexpr uint32_t kSchedTiles = 0, kSchedRows = 1, kSchedTeam = 2;
 struct MatchSched {
@@ -203,7 +211,8 @@ struct MatchSched {
 };
 // code: 0 auto; 1..256 workgroups per tile; 0x10000 | H a team of 1 + H workgroups per tile row;
 // anything else: per-tile workgroups, count from W and R
-MatchSched match_schedule(uint32_t W, uint32_t R, uint32_t cols, uint32_t code);
+// var (MatchArgs::var) != 0: per-tile workgroups only; rows bounds the region for the automatic count
+MatchSched match_schedule(uint32_t W, uint32_t R, uint32_t cols, uint32_t code, uint32_t var = 0, uint32_t rows = 0);
 size_t match_scratch_bytes(size_t ntiles, const MatchSched& m);
 void launch_match_tiles(hipStream_t s, MatchArgs& a, const MatchSched& m, void* scratch);
 void launch_match_code(hipStream_t s, const MatchArgs& a, unsigned long long* out_m, unsigned long long* out_n,

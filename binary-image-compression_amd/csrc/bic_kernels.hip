@@ -530,13 +530,7 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
   }
 }
 
-// PIPE: the strip records of row r - 1 are made while row r's plane words are formed (two LDS
-// tables per wave, one wave barrier per row), so the records' serial DPP chain overlaps independent
-// work; NP8: every plane of the image (no plane-count tests in the row loop)
-#ifndef BIC_GRAY_PIPE
-#define BIC_GRAY_PIPE 0
-#endif
-constexpr bool kGrayPipe = BIC_GRAY_PIPE != 0;
+// NP8: every plane of the image (no plane-count tests in the row loop)
 #ifndef BIC_GRAY_PREFETCH
 #define BIC_GRAY_PREFETCH 1
 #endif
@@ -549,11 +543,13 @@ constexpr bool kGrayPrefetch = BIC_GRAY_PREFETCH != 0;  // the next row's pixels
 #define BIC_GRAY_BYTEMED 1
 #endif
 constexpr bool kGrayByteMed = BIC_GRAY_BYTEMED != 0;
-// EGW (FULL strips of a row of whole strips): the EG words inside the row (eg.cpp:20-37: ~R then the
-// row's '1'), at the offsets every row after the plane's first 1 has -- row r at bit r (cols + 1) + 1
-// of plane b's stream at word b * eg_stride (eg_base_ok). A lane forms the stream word that starts
-// inside its own row word from it and lane l + 1's: the words across strip edges and the row's first
-// and last words are the emission's (eg_row_edges), as are whole rows up to the plane's first 1.
+// EGS (FULL strips of rows of whole strips, BM): the EG stream instead of R (eg.cpp:20-37 with the
+// block size fixed at 1: per row ~R then the end-of-row '1'), in the uniform layout -- bit 0 a '1', row
+// r at bit r (cols + 1) + 1 of plane b's slot (word b * eg_stride) -- which is the stream but for one
+// bit (bic_fused.hip eg_src_junctions / eg_fix_bit). With the strip's first bit at offset e of a word,
+// lane l < 63 stores the word that starts inside its own row word (its bits and lane l + 1's); the
+// two words across the strip's edges are left as fragments: head (lane 0's bits in the first word),
+// tail (lane 63's bits, and on a row's last strip its '1', in the word after) -> jfrag.
 template <bool PREDICT, bool STORE_R>
 constexpr int gray_rows_per_wave() { return kGrayByteMed && PREDICT && STORE_R ? kGrayRowsBM : kGrayRowsP; }
 // 64 bytes from src at any alignment (MIS: src not 16-byte aligned): the aligned 16-byte chunks that
@@ -595,12 +591,13 @@ __device__ __forceinline__ void load64_mis(const uint8_t* src, uint4 (&v)[4]) {
 #undef BIC_MIS_CASE
 }
 
-template <bool PREDICT, bool FULL, bool STORE_R, bool NP8, bool EGW, bool MIS = false>
+template <bool PREDICT, bool FULL, bool STORE_R, bool NP8, bool EGS, bool MIS = false>
 __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray, size_t pitch, const Geom& g,
                                                 uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
                                                 uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
                                                 int4* __restrict__ krec, uint32_t* __restrict__ kpos, uint32_t* tw,
-                                                uint64_t* __restrict__ out_e, uint64_t eg_stride) {
+                                                uint64_t* __restrict__ out_e, uint64_t eg_stride,
+                                                uint64_t* __restrict__ jfrag) {
   const int lane = lane_id();
   const int np = NP8 ? 8 : (int)g.nplanes;
   const uint32_t w = s * 64 + lane;
@@ -690,11 +687,15 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
       ulb = clb;
       gray_to_planes<FULL>(cur, pw, mask);
     }
-    uint32_t* tb = kGrayPipe ? tw + (r & 1) * 1024 : tw;
+    uint32_t* tb = tw;
     // EG: the strip's first row bit (wave-uniform shift; lane l's word starts 64 l bits later)
-    const uint64_t ep = (uint64_t)row * (g.cols + 1) + (row ? 1u : 0u) + (uint64_t)s * 4096;
+    const uint64_t ep = (uint64_t)row * (g.cols + 1) + 1 + (uint64_t)s * 4096;
     const uint32_t esh = (uint32_t)(ep & 63);
     uint64_t* eo = out_e + (ep >> 6) + lane;
+    // fragments: lane 0 the head, lane 63 the tail (one store instruction, two lanes)
+    uint64_t* jf = jfrag + 2 * ((uint64_t)row * ns + s) + (lane == 63 ? 1 : 0);
+    const uint64_t jstride = 2 * (uint64_t)g.rows * ns;
+    const uint64_t eol = s + 1 == ns ? BIC_MSB >> esh : 0;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       if (!NP8 && b >= np) break;
@@ -707,32 +708,28 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
         if (row == 0 && w == 0) R &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
         up[b] = pw[b];
       }
-      if (STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = R;
-      if constexpr (EGW && FULL) {
+      if (!EGS && STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = R;
+      if constexpr (EGS && FULL) {
         const uint64_t E = ~R;
+        uint64_t fr;
         if (esh == 0) {
           eo[(uint64_t)b * eg_stride] = bswap64(E);
+          fr = lane == 63 ? eol : 0;
         } else {
           const uint64_t En = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(E >> 32), 0x130, 0xf, 0xf, true) << 32) |
                               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)E, 0x130, 0xf, 0xf, true);
-          if (lane != 63) eo[(uint64_t)b * eg_stride + 1] = bswap64((E << (64 - esh)) | (En >> esh));
+          if (lane != 63) eo[(uint64_t)b * eg_stride + 1] = bswap64(funnel64(E, En, esh));
+          fr = lane == 0 ? E >> esh : (E << (64 - esh)) | eol;
         }
+        if (lane == 0 || lane == 63) jf[(uint64_t)b * jstride] = fr;
       }
       strip_word_put(tb, b, R, (int32_t)(w * 64));
     }
-    if constexpr (kGrayPipe) {
-      // the previous row's records (its table was completed before the last barrier); none at r = 0
-      strip_records(tw + ((r + 1) & 1) * 1024, r ? np : 0, krec, kpos, sones, (uint64_t)(row - (r ? 1 : 0)) * ns + s,
-                    (uint64_t)g.rows * ns);
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    } else {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      strip_records(tw, np, krec, kpos, sones, (uint64_t)row * ns + s, (uint64_t)g.rows * ns);
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row rewrites the table
-      __builtin_amdgcn_wave_barrier();
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    strip_records(tw, np, krec, kpos, sones, (uint64_t)row * ns + s, (uint64_t)g.rows * ns);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row rewrites the table
+    __builtin_amdgcn_wave_barrier();
     if constexpr (kGrayPrefetch) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
@@ -741,21 +738,19 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
       load(row + 1, cur, clb);
     }
   }
-  if constexpr (kGrayPipe)
-    strip_records(tw + ((nr - 1) & 1) * 1024, np, krec, kpos, sones, (uint64_t)(r0 + nr - 1) * ns + s,
-                  (uint64_t)g.rows * ns);
 }
 
 #ifndef BIC_GRAY_WAVES
 #define BIC_GRAY_WAVES 4
 #endif
-template <bool PREDICT, bool STORE_R, bool EGW, bool MIS = false>
+template <bool PREDICT, bool STORE_R, bool EGS, bool MIS = false>
 __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const uint8_t* __restrict__ gray, size_t pitch, Geom g,
                                                         uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
                                                         uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero,
-                                                        uint64_t* __restrict__ out_e, uint64_t eg_stride) {
-  __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][kGrayPipe ? 2048 : 1024];  // strip_word_put tables
+                                                        uint64_t* __restrict__ out_e, uint64_t eg_stride,
+                                                        uint64_t* __restrict__ jfrag) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   uint32_t* tw = tab[threadIdx.x >> 6];
   const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
@@ -764,17 +759,17 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
   if (r0 >= g.rows) return;  // whole wave
   // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
   if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
-    gray_strip_rows<PREDICT, true, STORE_R, true, EGW, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
-                                                            tw, out_e, eg_stride);
+    gray_strip_rows<PREDICT, true, STORE_R, true, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
+                                                            tw, out_e, eg_stride, jfrag);
   else if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
-    gray_strip_rows<PREDICT, true, STORE_R, false, EGW, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
-                                                             tw, out_e, eg_stride);
-  else if constexpr (!EGW)  // (EGW launches have whole strips only: gray_eg_supported)
+    gray_strip_rows<PREDICT, true, STORE_R, false, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
+                                                             tw, out_e, eg_stride, jfrag);
+  else if constexpr (!EGS)  // (EGS launches have whole strips only: gray_eg_supported)
     gray_strip_rows<PREDICT, false, STORE_R, false, false, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec,
-                                                                kpos, tw, nullptr, 0);
+                                                                kpos, tw, nullptr, 0, nullptr);
 }
 
-bool gray_eg_supported(const Geom& g) { return g.trail == ~0ull && g.used % 64 == 0; }
+bool gray_eg_supported(const Geom& g) { return g.trail == ~0ull && g.used % 64 == 0 && g.used / 64 <= kMaxStrips; }
 
 // any gray alignment and pitch (rows not 16-byte aligned: load64_mis); every row must hold used * 64
 // readable bytes
@@ -785,18 +780,19 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
 
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero, bool store_resid,
-                      uint64_t* out_e, uint64_t eg_stride) {
+                      uint64_t* out_e, uint64_t eg_stride, uint64_t* jfrag) {
   const uint32_t ns = gray_strips(g);
   const uint32_t rpw = predict && store_resid ? gray_rows_per_wave<true, true>() : gray_rows_per_wave<true, false>();
   const uint64_t units = (uint64_t)(g.rows + rpw - 1) / rpw;  // row groups per strip
   const uint32_t grid = (uint32_t)((units * ns + kWaves - 1) / kWaves);
   const bool mis = pitch % 16 != 0 || reinterpret_cast<uintptr_t>(gray) % 16 != 0;  // e.g. a P5 raster in its file
-  const bool egw = out_e && gray_eg_supported(g) && !mis;
+  const bool egs = out_e && jfrag && predict && store_resid && gray_eg_supported(g);
 #define BIC_GS(P, R, E, M) \
   k_gray_strips<P, R, E, M><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, \
-                                                    zero, out_e, eg_stride)
-#define BIC_GS2(P, R) { if (mis) BIC_GS(P, R, false, true); else if (egw) BIC_GS(P, R, true, false); else BIC_GS(P, R, false, false); }
-  if (predict) { if (store_resid) BIC_GS2(true, true) else BIC_GS2(true, false) }
+                                                    zero, out_e, eg_stride, jfrag)
+#define BIC_GS2(P, R) { if (mis) BIC_GS(P, R, false, true); else BIC_GS(P, R, false, false); }
+  if (egs) { if (mis) BIC_GS(true, true, true, true); else BIC_GS(true, true, true, false); }
+  else if (predict) { if (store_resid) BIC_GS2(true, true) else BIC_GS2(true, false) }
   else BIC_GS2(false, false)  // without prediction R = P
 #undef BIC_GS2
 #undef BIC_GS

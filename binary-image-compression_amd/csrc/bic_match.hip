@@ -20,6 +20,8 @@
 // (golomb_match / golomb_nomatch, :256 / :269) in raster order.
 #include "bic_device.h"
 
+#include <algorithm>
+
 namespace bic {
 
 #ifdef BIC_STAMPS  // diagnostic build only (make stamps): per-tile phase clocks of the row workgroup
@@ -73,6 +75,20 @@ __device__ __forceinline__ uint32_t key_dist(unsigned long long key, uint32_t in
   return (uint32_t)(key & (inv ? 0xfffu : 0x1fffu));
 }
 __device__ __forceinline__ int key_flip(unsigned long long key, uint32_t inv) { return inv ? (int)((key >> 12) & 1) : 0; }
+// compress5_test.cpp:94,109,126: a window replaces the best when (d - worstd) > (bestd - worstd) in idx_t
+// (worstd = W*W/2, bestd from W*W+1): every d < worstd beats every d >= worstd and the initial value,
+// and among those a larger d wins (ties: the earlier window). Two keys per window: the ranking one
+// (worstd - 1 - d, never for d >= worstd) and the first window with d < worstd, whose distance decides
+// whether the search ends there (the replacements only grow d, so bestd <= T can only hold after the
+// first one: if it does not, no window ever ends the search).
+constexpr uint32_t kRankNone = 0x1fffu;
+__device__ __forceinline__ unsigned long long win_key5(uint32_t d, uint32_t worstd, uint64_t pos) {
+  const uint32_t rank = d < worstd ? worstd - 1 - d : kRankNone;
+  return ((unsigned long long)rank << kDpShift) | ((unsigned long long)pos << kIdxShift) | d;
+}
+__device__ __forceinline__ unsigned long long win_key5_first(uint32_t d, uint32_t worstd, uint64_t pos) {
+  return ((unsigned long long)(d < worstd ? 0u : 1u) << kDpShift) | ((unsigned long long)pos << kIdxShift) | d;
+}
 // compress8_test.cpp:137: a tile of weight <= T or >= M - T (idx_t arithmetic) is a "perfect match"
 // before any window is searched
 __device__ __forceinline__ bool perfect_before(const MatchArgs& a, uint32_t w0) {
@@ -98,7 +114,8 @@ __device__ __forceinline__ Region make_region(const MatchArgs& a, uint32_t t) {
   g.minj = g.j0 > R ? g.j0 - R : 0;
   g.maxj = (g.j0 + R > cols - W) ? cols - W : g.j0 + R;
   g.mini2 = g.i0 > W ? g.i0 - W : 0;
-  g.maxj2 = g.j0 > W ? g.j0 - W : 0;
+  // compress4/5/6_test.cpp start the first loop at int(j0 - W) (none at j0 = 0; :104 / :105 / :126)
+  g.maxj2 = a.var ? g.j0 - W : (g.j0 > W ? g.j0 - W : 0);
   g.swin = (int64_t)(g.i0 - g.mini2) * (g.maxj2 - g.minj) + (int64_t)(g.mini2 - g.mini) * (g.maxj - g.minj);
   const int n1r = g.i0 - g.mini2 + 1, n1c = g.maxj2 - g.minj + 1;
   const int n2r = g.i0 - W - g.mini + 1, n2c = g.maxj - g.minj + 1;
@@ -183,6 +200,34 @@ __device__ uint64_t decide_tile(const MatchArgs& a, const double* enuml, const R
                                 int bj, uint32_t bd, int flip, uint64_t p, uint64_t b, int r) {
   const int W = (int)a.W;
   const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
+  if (a.var) {  // compress4_test.cpp:143-168, compress5_test.cpp:144-169, compress6_test.cpp:166-207
+    const uint32_t M = (uint32_t)(W * W);
+    const uint64_t p3 = p ^ b;  // (b = 0 without a window: compress6's P3 = P)
+    const uint32_t s0 = wave_total_u32((uint32_t)__popcll(p) | (uint32_t)__popcll(p3) << 16);
+    const uint32_t wP = s0 & 0xffff, w3 = s0 >> 16;
+    // ceil(log2(li)) of the tile's raster index: li = 0 gives -inf, 2^63 as idx_t on x86-64
+    const uint64_t idx_len = t == 0 ? (1ull << 63) : t == 1 ? 0 : 64 - (uint64_t)__clzll((unsigned long long)(t - 1));
+    const uint64_t nomatch_len = (uint64_t)(1.0 + enuml[wP]);
+    uint64_t match_len;
+    uint32_t mw;
+    if (a.var == 6) {
+      match_len = (uint64_t)((double)(1 + idx_len) + enuml[w3]);
+      mw = w3;
+    } else {
+      match_len = bd <= M ? (uint64_t)((double)(1 + idx_len) + enuml[bd]) : 100000;
+      mw = bd;
+    }
+    const bool take = nomatch_len > match_len;
+    if (r == 0) {
+      a.besti[t] = (uint32_t)bi;
+      a.bestj[t] = (uint32_t)bj;
+      a.bestd[t] = bd;
+      a.weights[t] = take ? mw : wP;
+      a.lens[t] = (uint32_t)(take ? match_len : nomatch_len);
+      a.modes[t] = take ? 'x' : 'o';
+    }
+    return take ? p3 : p;  // (the tile is written back unchanged without a match)
+  }
   bool inv = false;
   if (a.inv) {  // compress8_test.cpp:136, :163, :207-210
     inv = flip >= 0 ? flip != 0 : wave_total_u32((uint32_t)__popcll(p)) == (uint32_t)(W * W);
@@ -225,7 +270,7 @@ __device__ uint64_t decide_tile(const MatchArgs& a, const double* enuml, const R
 template <bool LDS>
 __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint32_t part, uint64_t* S,
                            uint64_t* Pl) {
-  __shared__ unsigned long long red[kMB / 64];
+  __shared__ unsigned long long red[kMB / 64], redA[kMB / 64];
   __shared__ int sh_last;
   const int W = (int)a.W;
   const uint32_t tid = threadIdx.x;
@@ -249,10 +294,13 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
     skip = perfect_before(a, w0);
   }
   const uint32_t M = (uint32_t)(W * W);
+  const bool v5 = a.var == 5;
+  const uint32_t worstd = M / 2;
 
-  // this part's share of the scan, in chunks; a window at distance <= T ends the search
+  // this part's share of the scan, in chunks; a window at distance <= T ends the search (variant 5:
+  // every window is scanned and the first-window rule applied by the tile's finish)
   const uint64_t lo = part * g.n / a.G, hi = skip ? lo : (part + 1) * g.n / a.G;
-  unsigned long long best = ~0ull;
+  unsigned long long best = ~0ull, bestA = ~0ull;
   uint32_t chunk = 0;
   for (uint64_t base = lo; base < hi; base += kChunk, ++chunk) {
 #pragma unroll
@@ -264,12 +312,18 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
         pos_window(g, W, pos, i2, j2);
         uint32_t d = 0;
         for (int r = 0; r < W; ++r) d += (uint32_t)__popcll((row_bits<LDS>(a, g, S, i2 + r, j2) ^ Pl[r]) & topW);
-        const unsigned long long key = win_key(d, a.T, pos, M, a.inv);
-        best = key < best ? key : best;
+        if (v5) {
+          const unsigned long long ka = win_key5_first(d, worstd, pos), kb = win_key5(d, worstd, pos);
+          bestA = ka < bestA ? ka : bestA;
+          best = kb < best ? kb : best;
+        } else {
+          const unsigned long long key = win_key(d, a.T, pos, M, a.inv);
+          best = key < best ? key : best;
+        }
       }
     }
-    int stop = (best >> kDpShift) == 0;
-    if ((chunk & 7) == 7 && tid == 0 && !stop) {  // a lower part already found one
+    int stop = !v5 && (best >> kDpShift) == 0;
+    if (!v5 && (chunk & 7) == 7 && tid == 0 && !stop) {  // a lower part already found one
       const unsigned long long k = __hip_atomic_load(&a.key[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       stop = (k >> kDpShift) == 0 && key_pos(k) < flat_pos(g, (uint32_t)base);
     }
@@ -277,11 +331,19 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
   }
   best = wave_min_u64(best);
   if (lane_id() == 0) red[tid >> 6] = best;
+  if (v5) {
+    bestA = wave_min_u64(bestA);
+    if (lane_id() == 0) redA[tid >> 6] = bestA;
+  }
   __syncthreads();
   if (tid == 0) {
     for (int w = 1; w < kMB / 64; ++w) best = red[w] < best ? red[w] : best;
     best = red[0] < best ? red[0] : best;
     if (best != ~0ull) atomicMin(&a.key[t], best);
+    if (v5) {
+      for (int w = 0; w < kMB / 64; ++w) bestA = redA[w] < bestA ? redA[w] : bestA;
+      if (bestA != ~0ull) atomicMin(&a.key2[t], bestA);
+    }
     stores_done();
     const uint32_t old = atomicAdd(&a.arrive[t], 1u);
     sh_last = old + 1 == a.G;
@@ -290,7 +352,20 @@ __device__ void match_tile(const MatchArgs& a, const Region& g, uint32_t t, uint
   if (!sh_last || tid >= 64) return;
 
   // ---- the last workgroup finishes the tile (one lane per tile row) ----
-  const unsigned long long key = __hip_atomic_load(&a.key[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long key = __hip_atomic_load(&a.key[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (v5) {  // compress5_test.cpp:104-136 (see win_key5)
+    const unsigned long long kA = __hip_atomic_load(&a.key2[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool firstA = kA != ~0ull && (kA >> kDpShift) == 0;  // some window with d < worstd
+    unsigned long long ch = ~0ull;
+    if (a.T > M) {  // bestd <= T after the first window: it alone decides (replacing W*W+1 or not)
+      if (firstA && key_pos(kA) == flat_pos(g, 0)) ch = kA;
+    } else if (firstA && key_dist(kA, 0) <= a.T) {
+      ch = kA;
+    } else if (key != ~0ull && (key >> kDpShift) != kRankNone) {
+      ch = key;
+    }
+    key = ch;
+  }
   const int r = (int)tid;
   uint32_t bd = M + 1;
   int bi = 0, bj = 0, flip = -1;
@@ -935,8 +1010,22 @@ bool match_rows_fit(uint32_t W, uint32_t R, uint32_t cols) {
   return nr * ((cols + 31) / 32 + 2) <= kRowLds;
 }
 
-MatchSched match_schedule(uint32_t W, uint32_t R, uint32_t cols, uint32_t code) {
+MatchSched match_schedule(uint32_t W, uint32_t R, uint32_t cols, uint32_t code, uint32_t var, uint32_t rows) {
   MatchSched m{};
+  if (var) {  // compress4/5/6 loops: per-tile workgroups (k_match_tiles); R bounded by the image
+    if (code >= 1 && code <= 256) {
+      m.kind = kSchedTiles;
+      m.G = code;
+      return m;
+    }
+    const uint64_t Rr = std::min<uint64_t>(R, std::max<uint64_t>(rows, cols));
+    const uint64_t r1 = Rr >= W ? Rr - W + 1 : 0;
+    const uint64_t nmax = r1 * std::min<uint64_t>(2 * Rr + 1, cols) + (uint64_t)(W + 1) * (r1 + 1);
+    const uint64_t g = (nmax + 2 * kChunk - 1) / (2 * kChunk);
+    m.kind = kSchedTiles;
+    m.G = (uint32_t)(g < 1 ? 1 : g > 64 ? 64 : g);
+    return m;
+  }
   // windows of the largest region: (R-W+1) rows above at 2R+1 columns, W+1 rows at R-W+1 columns
   const uint64_t r1 = R >= W ? (uint64_t)(R - W + 1) : 0;
   const uint64_t nmax = r1 * (2ull * R + 1) + (uint64_t)(W + 1) * (r1 + 1);
@@ -967,7 +1056,7 @@ MatchSched match_schedule(uint32_t W, uint32_t R, uint32_t cols, uint32_t code) 
 }
 
 size_t match_scratch_bytes(size_t ntiles, const MatchSched& m) {
-  return 512 + ntiles * (8 + 4 * 7 + 1) + ntiles * (size_t)m.H * 8 + 256;
+  return 512 + ntiles * (8 + 4 * 7 + 1) + ntiles * (size_t)m.H * 8 + 256 + ntiles * 8 + 256;  // (+ key2)
 }
 
 void launch_match_tiles(hipStream_t s, MatchArgs& a, const MatchSched& m, void* scratch) {
@@ -986,11 +1075,14 @@ void launch_match_tiles(hipStream_t s, MatchArgs& a, const MatchSched& m, void* 
   if (!a.modes) a.modes = reinterpret_cast<uint8_t*>(spare + 4 * ntiles);
   unsigned long long* slots = reinterpret_cast<unsigned long long*>(
       (reinterpret_cast<uintptr_t>(spare + 4 * ntiles) + ntiles + 255) & ~(uintptr_t)255);
+  a.key2 = reinterpret_cast<unsigned long long*>(
+      (reinterpret_cast<uintptr_t>(slots + (size_t)ntiles * m.H) + 255) & ~(uintptr_t)255);
   a.G = m.G;
   a.H = m.H;
   a.K = m.K;
   (void)hipMemsetAsync(a.counter, 0, 4, s);
   (void)hipMemsetAsync(a.key, 0xff, (size_t)ntiles * 8, s);
+  if (a.var == 5) (void)hipMemsetAsync(a.key2, 0xff, (size_t)ntiles * 8, s);
   (void)hipMemsetAsync(a.done, 0, (size_t)ntiles * 8, s);  // done + arrive (row schedules: progress)
   uint32_t* progress = a.done;
   switch (m.kind) {

@@ -29,7 +29,7 @@ EXPORTS = [
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
     "bic_bitplanes_u8_range", "bic_encode_gray_range", "bic_encode_planes_packed", "bic_encode_gray_packed",
     "bic_row_index", "bic_decode_planes", "bic_pgm_bitplanes", "bic_pnm_parse_header",
-    "bic_gf2_transpose", "bic_gf2_mul", "bic_planes_to_gray", "bic_match_encode_inv",
+    "bic_gf2_transpose", "bic_gf2_mul", "bic_planes_to_gray", "bic_match_encode_inv", "bic_match_encode_var",
 ]
 
 # bic_gf2_mul ops (include/bic.h)
@@ -106,6 +106,7 @@ def load(path=LIB_PATH):
     sig("bic_match_encode", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_set_match_parts", i32, [vp, u32])
     sig("bic_match_encode_inv", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
+    sig("bic_match_encode_var", i32, [vp, i32, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_encode_gray", i32, [vp, vp, sz, sz, sz, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
     sig("bic_bitplanes_u8_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz])
     sig("bic_encode_gray_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
@@ -392,6 +393,12 @@ class Context:
         (BIC_OPT_ONE_STREAM) instead of side by side on a second stream"""
         self._chk(self.lib.bic_ctx_set_option(self.h, 5, int(on)), "bic_ctx_set_option")
 
+    def set_eg_source(self, on=True):
+        """bic_encode_gray* without planes: the count pass writes the EG stream and the Golomb kernels
+        read the residual rows back from it (BIC_OPT_EG_SOURCE, default on) -- off: the residual
+        planes in a context buffer"""
+        self._chk(self.lib.bic_ctx_set_option(self.h, 6, int(on)), "bic_ctx_set_option")
+
     def set_multipass(self, on=True):
         self._chk(self.lib.bic_ctx_set_option(self.h, 1, int(on)), "bic_ctx_set_option")
 
@@ -462,9 +469,11 @@ class Context:
                   "bic_patch_search")
         return tuple(out)
 
-    def match_encode(self, plane, cols, W, T=0, R=128, enuml=None, cap_words=None, resid=None, invert=False):
+    def match_encode(self, plane, cols, W, T=0, R=128, enuml=None, cap_words=None, resid=None, invert=False,
+                     variant=7):
         """compress7_test.cpp's tile loop with search window R and threshold T (bic_match_encode);
-        invert: compress8_test.cpp's patch-inversion variant (bic_match_encode_inv, `inverted` per tile).
+        invert: compress8_test.cpp's patch-inversion variant (bic_match_encode_inv, `inverted` per tile);
+        variant 4 / 5 / 6: the loops of compress4/5/6_test.cpp (bic_match_encode_var).
         plane: int64 [rows, wpr] device tensor (not modified); enuml: numpy float64 [W*W+1] (host),
         default enumL from this build. Returns device tensors per tile and the two streams."""
         rows, wpr = plane.shape
@@ -479,7 +488,12 @@ class Context:
         e = enum_table(W) if enuml is None else np.ascontiguousarray(enuml, np.float64)
         inv = t.empty(nt, dtype=t.uint8, device=self.dev) if invert else None
         self._bind_stream()
-        if invert:
+        if variant in (4, 5, 6):
+            self._chk(self.lib.bic_match_encode_var(self.h, variant, _p(plane), rows, cols, wpr, W, T, R,
+                                                    e.ctypes.data_as(C.c_void_p), _p(bi), _p(bj), _p(bd), _p(wt),
+                                                    _p(modes), _p(resid), _p(sm), _p(sn), cap_words, _p(stats)),
+                      "bic_match_encode_var")
+        elif invert:
             self._chk(self.lib.bic_match_encode_inv(self.h, _p(plane), rows, cols, wpr, W, T, R,
                                                     e.ctypes.data_as(C.c_void_p), _p(bi), _p(bj), _p(bd), _p(wt),
                                                     _p(modes), _p(inv), _p(resid), _p(sm), _p(sn), cap_words,

@@ -89,6 +89,11 @@ int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
  * the ctx stream instead of side by side on a second stream (same output; a test hook for the
  * launch ordering). */
 #define BIC_OPT_ONE_STREAM 5
+/* BIC_OPT_EG_SOURCE = 0: bic_encode_gray* without planes stores the med residual planes in a ctx
+ * buffer for the encoder (the round-3 path) instead of writing the EG stream from the count pass
+ * and reading the residual rows back from it (default 1, slot output with the EG coder; same
+ * streams: a cross-check and A/B hook). */
+#define BIC_OPT_EG_SOURCE 6
 int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
 
 /* ---- a2: bitplane extraction (bitplane_tool.cpp:24-30) -----------------------------------
@@ -255,6 +260,24 @@ int bic_match_encode_inv(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_
                          unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
                          uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint8_t* inverted, uint64_t* resid,
                          uint64_t* stream_match, uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats);
+/* The tile loops of the other windowed-search drivers, otherwise as bic_match_encode (same
+ * arguments and outputs; the driver's W, T, R; variant 7 = bic_match_encode, 8 = bic_match_encode_inv
+ * without the per-tile inversion flags):
+ *   4: compress4_test.cpp:89-170 -- no med: the first loop starts at column j0 - W (none at j0 = 0),
+ *      idx_len = ceil(log2(li)) of the tile's raster index li (li = 0: 2^63, never a match),
+ *      nomatch_len = 1 + enumL(M, P.weight()), match_len = 1 + idx_len + enumL(M, bestd) when bestd
+ *      <= M, else 100000; a match codes bestd with golomb_match and writes P ^ window back, no match
+ *      codes P.weight() with golomb_nomatch and leaves the tile; modes 'x' / 'o';
+ *   5: compress5_test.cpp:89-170 -- 4 with a window kept when (d - worstd) > (bestd - worstd) in
+ *      idx_t arithmetic, worstd = W*W/2 (:94, :109, :126);
+ *   6: compress6_test.cpp:111-208 -- 4 with P3 = P when no window and match_len = 1 + idx_len +
+ *      enumL(M, P3.weight()) (no 100000 guard); its D / iD matrices (:64-76) are built but unused
+ *      (#if 0, :172-182).
+ * Schedule: per-tile workgroups (bic_set_match_parts 1..256, or automatic). */
+int bic_match_encode_var(bic_ctx* ctx, int variant, const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
+                         unsigned W, unsigned T, unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                         uint32_t* bestd, uint32_t* weights, uint8_t* modes, uint64_t* resid, uint64_t* stream_match,
+                         uint64_t* stream_nomatch, size_t cap_words, uint64_t* stats);
 /* Schedule of bic_match_encode (every schedule gives the same result): 0 (default) = automatic;
  * N in 1..256 = N workgroups per tile, tiles in raster order with flags between them;
  * 0x10000 | H = one workgroup per tile row walking its tiles, plus H helper workgroups that search

@@ -740,6 +740,105 @@ int bo_match_encode_v(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigne
     return 0;
 }
 
+/* The loops of compress4_test.cpp:89-170 (variant 4), compress5_test.cpp:89-170 (5) and
+ * compress6_test.cpp:111-208 (6): no med, one coder decision, the residual written back only on a
+ * match. Against compress7_test.cpp (bo_match_encode_v) they differ in
+ *  - the first loop's columns j2 = j0 - W .. minj (int(j0-W), :104 / :104 / :126: none at j0 = 0);
+ *  - idx_len = ceil(log2(li)) of the tile's raster index (:147 / :148 / :187; li = 0: log2(0) = -inf,
+ *    converted to idx_t: 2^63 on x86-64, so the first tile never matches);
+ *  - nomatch_len = 1 + enumL(M, P.weight()); variants 4/5: match_len = 1 + idx_len + enumL(M, bestd)
+ *    when bestd <= M, else 100000 (:154 / :155); variant 6: match_len = 1 + idx_len + enumL(M,
+ *    P3.weight()) with P3 = P ^ best window, or P itself when no window (:166-194);
+ *  - a match codes bestd (4/5) / P3.weight() (6) with golomb_match and writes P3 back (:164 / :165 /
+ *    :203); otherwise P.weight() with golomb_nomatch and the tile is left as it is;
+ *  - variant 5 keeps a window when (d - worstd) > (bestd - worstd) in idx_t arithmetic, worstd =
+ *    W*W/2 (compress5_test.cpp:94,109,126): unsigned wrap makes every d < worstd beat every d >= worstd
+ *    and the initial W*W+1, and among those the larger d win.
+ * modes: 'x' match, 'o' no match. Returns 0, -1 on a bad argument or stream overflow. */
+int bo_match_encode_var(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T, unsigned R,
+                        const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
+                        uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
+                        uint8_t* stream_nomatch, size_t cap_bytes, int variant) {
+    if (W == 0 || W > 64 || rows % W || cols % W || variant < 4 || variant > 6) return -1;
+    const size_t Ny = rows / W, Nx = cols / W, M = (size_t)W * W;
+    const uint64_t worstd = (uint64_t)(W * W / 2);
+    const uint64_t topW = W >= 64 ? ~0ull : ~(~0ull >> W);
+    uint64_t P[64], P2[64], P3[64];
+    bo_bw bwm, bwn;
+    bo_bw_init(&bwm, stream_match, cap_bytes);
+    bo_bw_init(&bwn, stream_nomatch, cap_bytes);
+    bo_golomb gm, gn;
+    bo_golomb_init(&gm);
+    bo_golomb_init(&gn);
+    uint64_t L = 0, matches = 0;
+    size_t li = 0;
+    const int iW = (int)W, iR = (int)R, icols = (int)cols;
+    for (size_t i = 0; i < Ny; i++)
+        for (size_t j = 0; j < Nx; j++, li++) {
+            const int i0 = (int)(i * W), j0 = (int)(j * W);
+            bo_get_submatrix(I, rows, cols, wpr, (size_t)i0, (size_t)i0 + W, (size_t)j0, (size_t)j0 + W, P, 1);
+            for (unsigned r = 0; r < W; r++) P[r] &= topW;
+            uint64_t bi = 0, bj = 0, bd = M + 1;
+            int perfect = 0;
+            const int mini = i0 > iR ? i0 - iR : 0;
+            const int mini2 = i0 > iW ? i0 - iW : 0;
+            const int minj = j0 > iR ? j0 - iR : 0;
+            const int maxj = (j0 + iR > icols - iW) ? icols - iW : j0 + iR;
+            for (int pass = 0; pass < 2 && !perfect; pass++) {
+                const int ihi = pass ? i0 - iW : i0, ilo = pass ? mini : mini2, jhi = pass ? maxj : j0 - iW;
+                for (int i2 = ihi; i2 >= ilo && !perfect; i2--)
+                    for (int j2 = jhi; j2 >= minj; j2--) {
+                        bo_get_submatrix(I, rows, cols, wpr, (size_t)i2, (size_t)i2 + W, (size_t)j2, (size_t)j2 + W, P2, 1);
+                        uint64_t d = 0;
+                        for (unsigned r = 0; r < W; r++) d += (uint64_t)__builtin_popcountll((P[r] ^ P2[r]) & topW);
+                        const int better = variant == 5 ? (d - worstd) > (bd - worstd) : d < bd;
+                        if (better) { bd = d; bi = (uint64_t)i2; bj = (uint64_t)j2; }
+                        if (bd <= T) { perfect = 1; break; }
+                    }
+            }
+            if (variant == 6 && bd > M) {
+                for (unsigned r = 0; r < W; r++) P3[r] = P[r];
+            } else {
+                bo_get_submatrix(I, rows, cols, wpr, bi, bi + W, bj, bj + W, P2, 1);
+                for (unsigned r = 0; r < W; r++) P3[r] = (P[r] ^ P2[r]) & topW;
+            }
+            const uint64_t wP = bo_weight(P, W, W, 1), w3 = bo_weight(P3, W, W, 1);
+            const uint64_t idx_len = li == 0 ? 0x8000000000000000ull : li == 1 ? 0 : 64 - (uint64_t)__builtin_clzll((uint64_t)(li - 1));
+            const uint64_t nomatch_len = (uint64_t)(1.0 + enumL[wP]);
+            uint64_t match_len, match_w;
+            if (variant == 6) {
+                match_len = (uint64_t)((double)(1 + idx_len) + enumL[w3]);
+                match_w = w3;
+            } else {
+                match_len = bd <= M ? (uint64_t)((double)(1 + idx_len) + enumL[bd]) : 100000;
+                match_w = bd;
+            }
+            const int take = nomatch_len > match_len;
+            if (take) {
+                bo_golomb_code(&gm, (uint32_t)match_w, &bwm);
+                matches++;
+                L += match_len;
+                bo_set_submatrix(I, rows, cols, wpr, (size_t)i0, (size_t)j0, P3, W, W, 1);
+            } else {
+                bo_golomb_code(&gn, (uint32_t)wP, &bwn);
+                L += nomatch_len;
+            }
+            if (besti) besti[li] = (uint32_t)bi;
+            if (bestj) bestj[li] = (uint32_t)bj;
+            if (bestd) bestd[li] = (uint32_t)bd;
+            if (weights) weights[li] = (uint32_t)(take ? match_w : wP);
+            if (modes) modes[li] = take ? 'x' : 'o';
+        }
+    if (stats) {
+        stats[0] = matches;
+        stats[1] = (uint64_t)gm.bitcount;
+        stats[2] = (uint64_t)gn.bitcount;
+        stats[3] = L;
+    }
+    if ((stream_match && bwm.overflow) || (stream_nomatch && bwn.overflow)) return -1;
+    return 0;
+}
+
 /* ---- binary_matrix algebra over GF(2) ---------------------------------------------------- */
 
 static int gf2_bit(const uint64_t* M, size_t wpr, size_t i, size_t j) {

@@ -187,6 +187,13 @@ int bo_match_encode_v(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigne
                       uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
                       uint8_t* stream_nomatch, size_t cap_bytes, int invert, uint8_t* inverted);
 
+/* the loops of compress4_test.cpp (variant 4), compress5_test.cpp (5), compress6_test.cpp (6):
+ * no med, the residual written back on a match only; modes 'x' / 'o' (see bic_oracle.c). */
+int bo_match_encode_var(uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T, unsigned R,
+                        const double* enumL, uint32_t* besti, uint32_t* bestj, uint32_t* bestd,
+                        uint32_t* weights, char* modes, uint64_t* stats, uint8_t* stream_match,
+                        uint8_t* stream_nomatch, size_t cap_bytes, int variant);
+
 /* ---- binary_matrix algebra over GF(2) ----------------- */
 /* Reference layout only: wpr = ceil(cols/64) for every operand (the loops index words flat).
  * bo_gf2_transpose: binmat.cpp:199-214 (copy_col_to + set_row): dst (cols x rows). bo_gf2_mul:

@@ -473,6 +473,99 @@ extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr
   return 0;
 }
 
+// The tile loops of compress4_test.cpp:89-170 (variant 4), compress5_test.cpp:89-170 (5) and
+// compress6_test.cpp:111-208 (6) over the reference's own objects (get_submatrix, dist, add, weight,
+// set_submatrix, GolombCoder), statement for statement; enumL from the caller (GSL is absent).
+// modes: 'x' match, 'o' no match.
+extern "C" int ref_match_loop_var(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
+                                  unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                                  uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats, int variant) {
+  if (variant < 4 || variant > 6) return -1;
+  binary_matrix I = from_words(Iw, rows, cols, wpr);
+  const int iW = (int)W, iR = (int)R;
+  const idx_t M = (idx_t)W * W;
+  const idx_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
+  binary_matrix P, P2;
+  binary_matrix P3(W, W);
+  GolombCoder golomb_match, golomb_nomatch;
+  uint64_t L = 0, matches = 0;
+  idx_t li = 0;
+  for (idx_t i = 0; i < Ny; i++)
+    for (idx_t j = 0; j < Nx; j++, li++) {
+      const int i0 = i * W, j0 = j * W;
+      P = I.get_submatrix(i0, i0 + W, j0, j0 + W);
+      const idx_t worstd = W * W / 2;
+      idx_t bi = 0, bj = 0, bd = M + 1;
+      int i2;
+      bool perfect = false;
+      const int mini = i0 > iR ? (i0 - iR) : 0;
+      const int mini2 = (i0 > iW) ? (i0 - iW) : 0;
+      const int minj = (j0 > iR) ? (j0 - iR) : 0;
+      const int maxj = ((j0 + iR) > (int(cols) - iW)) ? (cols - W) : (j0 + iR);
+      for (i2 = i0; (i2 >= mini2) && !perfect; i2--)
+        for (int j2 = int(j0 - W); j2 >= minj; j2--) {
+          P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+          const idx_t d = dist(P, P2);
+          if (variant == 5 ? ((d - worstd) > (bd - worstd)) : (d < bd)) { bd = d; bi = i2; bj = j2; }
+          if (bd <= T) { perfect = true; break; }
+        }
+      for (i2 = i0 - iW; (i2 >= mini) && !perfect; i2--)
+        for (int j2 = maxj; j2 >= minj; j2--) {
+          P2 = I.get_submatrix(i2, i2 + W, j2, j2 + W);
+          const idx_t d = dist(P, P2);
+          if (variant == 5 ? ((d - worstd) > (bd - worstd)) : (d < bd)) { bd = d; bi = i2; bj = j2; }
+          if (bd <= T) { perfect = true; break; }
+        }
+      idx_t match_len, nomatch_len, match_weight;
+      const idx_t idx_len = ceil(log2(li));
+      if (variant == 6) {  // compress6_test.cpp:166-194
+        if (bd <= M) {
+          P2 = I.get_submatrix(bi, bi + W, bj, bj + W);
+          add(P, P2, P3);
+        } else {
+          P3 = P.get_copy();
+        }
+        match_weight = P3.weight();
+        nomatch_len = 1 + enuml[P.weight()];
+        match_len = 1 + idx_len + enuml[match_weight];
+      } else {  // compress4_test.cpp:143-155
+        P2 = I.get_submatrix(bi, bi + W, bj, bj + W);
+        add(P, P2, P3);
+        match_weight = bd;
+        nomatch_len = 1 + enuml[P.weight()];
+        match_len = (bd <= M) ? (idx_t)(1 + idx_len + enuml[bd]) : 100000;
+      }
+      const idx_t wP = P.weight();
+      const bool take = nomatch_len > match_len;
+      if (take) {
+        golomb_match.codeSample(match_weight);
+        matches++;
+        L += match_len;
+        I.set_submatrix(i0, j0, P3);
+      } else {
+        golomb_nomatch.codeSample(wP);
+        L += nomatch_len;
+      }
+      if (besti) besti[li] = (uint32_t)bi;
+      if (bestj) bestj[li] = (uint32_t)bj;
+      if (bestd) bestd[li] = (uint32_t)bd;
+      if (weights) weights[li] = (uint32_t)(take ? match_weight : wP);
+      if (modes) modes[li] = take ? 'x' : 'o';
+    }
+  to_words(I, Iw, wpr);
+  if (stats) {
+    stats[0] = matches;
+    stats[1] = (uint64_t)golomb_match.bitcount;
+    stats[2] = (uint64_t)golomb_nomatch.bitcount;
+    stats[3] = L;
+  }
+  P.destroy();
+  P2.destroy();
+  P3.destroy();
+  I.destroy();
+  return 0;
+}
+
 // compress8_test.cpp:126-272's tile loop over the reference's own objects (get_submatrix, dist,
 // flip, add, med, weight, set_submatrix, GolombCoder); enumL from the caller (GSL is absent). As
 // written except that a window's `inv` (left uninitialised by the driver when the window is not

@@ -64,6 +64,9 @@ class Oracle:
         _sig(L, "bo_match_encode_v", C.c_int,
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p,
               u8p, u8p, sz, C.c_int, u8p])
+        _sig(L, "bo_match_encode_var", C.c_int,
+             [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p,
+              u8p, u8p, sz, C.c_int])
 
     # -- inputs ----------------------------------------------------------
     def gen_plane(self, seed, p, rows, cols, wpr=None):
@@ -311,6 +314,37 @@ class Oracle:
         return out
 
 
+def _match_var(lib_fn, I, cols, W, T, R, enuml, variant, cap):
+    I = np.array(I, copy=True)
+    rows, wpr = I.shape
+    n = (rows // W) * (cols // W)
+    bi, bj, bd, wt = (np.zeros(n, np.uint32) for _ in range(4))
+    modes = C.create_string_buffer(n + 1)
+    stats = np.zeros(4, np.uint64)
+    streams = [np.zeros(cap, np.uint8), np.zeros(cap, np.uint8)] if cap else [None, None]
+    rc = lib_fn(I, rows, wpr, bi, bj, bd, wt, modes, stats, streams, n)
+    assert rc == 0, rc
+    out = dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes.raw[:n].decode(), residual=I,
+               matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]))
+    if cap:
+        out["stream_match"] = streams[0][: ((out["bits_match"] + 63) // 64) * 8].copy()
+        out["stream_nomatch"] = streams[1][: ((out["bits_nomatch"] + 63) // 64) * 8].copy()
+    return out
+
+
+def match_encode_var(oracle, I, cols, W, T, R, enuml, variant, want_stream=True):
+    """compress4/5/6_test.cpp's loops (bo_match_encode_var: variant 4, 5 or 6)"""
+    enuml = np.ascontiguousarray(enuml, np.float64)
+
+    def call(I, rows, wpr, bi, bj, bd, wt, modes, stats, streams, n):
+        cap = len(streams[0]) if streams[0] is not None else 0
+        return oracle.lib.bo_match_encode_var(ptr(I, u64p), rows, cols, wpr, W, T, R, ptr(enuml, dp), ptr(bi, u32p),
+                                              ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(stats, u64p),
+                                              ptr(streams[0], u8p), ptr(streams[1], u8p), cap, variant)
+    n = (I.shape[0] // W) * (cols // W)
+    return _match_var(call, I, cols, W, T, R, enuml, variant, n * 8 + 4096 if want_stream else 0)
+
+
 class Ref:
     """The reference's own objects (oracle/_ref/libref.so): compiled in the build container from the
     reference's sources (oracle/Makefile ref); the built library travels to the GPU box with the
@@ -333,6 +367,8 @@ class Ref:
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p])
         _sig(L, "ref_match_loop8", C.c_int,
              [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u8p, u64p])
+        _sig(L, "ref_match_loop_var", C.c_int,
+             [u64p, sz, sz, sz, C.c_uint, C.c_uint, C.c_uint, dp, u32p, u32p, u32p, u32p, C.c_char_p, u64p, C.c_int])
         _sig(L, "ref_gf2_mul", C.c_int, [C.c_int, u64p, sz, sz, u64p, sz, sz, u64p, sz, sz])
         _sig(L, "ref_gf2_transpose", C.c_int, [u64p, sz, sz, u64p])
         _sig(L, "ref_baseline_planes", C.c_double,
@@ -450,6 +486,16 @@ class Ref:
                                 ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(stats, u64p))
         return dict(besti=bi, bestj=bj, bestd=bd, weights=wt, modes=modes.raw[:n].decode(), residual=I,
                     matches=int(stats[0]), bits_match=int(stats[1]), bits_nomatch=int(stats[2]), L=int(stats[3]))
+
+    def match_loop_var(self, I, cols, W, T, R, enuml, variant):
+        """compress4/5/6_test.cpp's loops over the reference's objects (ref_match_loop_var)"""
+        enuml = np.ascontiguousarray(enuml, np.float64)
+
+        def call(I, rows, wpr, bi, bj, bd, wt, modes, stats, streams, n):
+            return self.lib.ref_match_loop_var(ptr(I, u64p), rows, cols, wpr, W, T, R, ptr(enuml, dp), ptr(bi, u32p),
+                                               ptr(bj, u32p), ptr(bd, u32p), ptr(wt, u32p), modes, ptr(stats, u64p),
+                                               variant)
+        return _match_var(call, I, cols, W, T, R, enuml, variant, 0)
 
     def match_loop8(self, I, cols, W, T, R, enuml):
         """compress8_test.cpp:126-272 over the reference's objects (ref_match_loop8)"""

@@ -1,0 +1,93 @@
+"""The EG source path of bic_encode_gray without planes (BIC_OPT_EG_SOURCE, the default C3 step):
+the count pass writes each plane's EG stream (eg.cpp:20-37 with the block size fixed at 1) in its
+uniform layout -- row r at bit r (cols + 1) + 1 -- and the Golomb kernels read the residual rows
+back from it; the ONES scan assembles the words across strip edges and one bit per plane is
+cleared after the emission (bic_fused.hip eg_src_junctions / eg_fix_bit). Against the oracle and
+against the round-3 path (residual planes in a context buffer), at every row-offset phase (rows
+>= 64: offsets whose bit is 0 and 63 in their word), 1 to 4 strips per row, the plane's first 1 at
+column 0 of a later row, on a strip edge, far down the plane, and planes without a residual 1."""
+import numpy as np
+import pytest
+
+from pybic import as_u64, stream_bytes  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def staged(ctx):
+    ctx.set_encoder("staged")
+    yield
+    ctx.set_encoder("auto")
+    ctx.set_eg_source(True)
+
+
+def _img(oracle, seed, rows, cols, kind):
+    u = oracle.gen_bytes(seed, rows * cols).reshape(rows, cols)
+    if kind == "uniform":
+        return u
+    if kind == "smooth":
+        i, j = np.mgrid[0:rows, 0:cols]
+        return ((i * 3 + j // 5 + u % 7) % 256).astype(np.uint8)
+    if kind == "constant":  # no residual 1 in any plane
+        return np.full((rows, cols), 0x5C, np.uint8)
+    img = u.copy()
+    if kind == "first_col0":  # every plane's first 1 at column 0 of row rows // 2
+        img[: rows // 2] = 0
+        img[rows // 2:, 0] = 0xFF
+        img[rows // 2, 1:] = 0xFF
+        return img
+    if kind == "first_edge":  # first 1 on the second strip's first column
+        img[: rows // 3] = 0
+        img[rows // 3, :4096] = 0
+        return img
+    if kind == "sparse":  # high planes blank, low planes rare
+        return (u > 250).astype(np.uint8) * (u & 3)
+    raise ValueError(kind)
+
+
+def _check(ctx, oracle, g, img, nplanes, plane0, golomb, eg):
+    cols = img.shape[1]
+    P = oracle.bitplanes(np.ascontiguousarray(img), 8)[plane0:plane0 + nplanes]
+    _, rg, re = ctx.encode_gray(g, cols=cols, nplanes=nplanes, plane0=plane0, store_planes=False, golomb=golomb, eg=eg)
+    ctx.sync()
+    for k in range(nplanes):
+        for coder, res in ((0, rg), (1, re)):
+            if res is None:
+                continue
+            out, bits = res
+            eb, est, _ = oracle.encode_plane(P[k], cols, 1, coder)
+            assert int(as_u64(bits)[k]) == eb, (k, coder)
+            assert stream_bytes(out[k], eb) == est.tobytes(), (k, coder)
+
+
+@pytest.mark.parametrize("rows,cols,kind", [
+    (70, 4096, "uniform"), (130, 4096, "smooth"), (66, 8192, "uniform"), (65, 12288, "smooth"),
+    (64, 16384, "uniform"), (33, 16384, "smooth"), (90, 4096, "first_col0"), (40, 8192, "first_edge"),
+    (70, 4096, "constant"), (70, 8192, "sparse"), (1, 4096, "uniform"), (2, 16384, "smooth"),
+])
+def test_eg_source(ctx, oracle, staged, rows, cols, kind):
+    img = _img(oracle, rows * 13 + cols, rows, cols, kind)
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    for golomb, eg in ((True, True), (False, True), (True, False)):
+        _check(ctx, oracle, g, img, 8, 0, golomb, eg)
+    _check(ctx, oracle, g, img, 3, 4, True, True)
+
+
+def test_eg_source_matches_resid_path(ctx, oracle, staged):
+    """both paths of planes = NULL give the same streams (every word of every slot compared, so the
+    words past each stream's end too)"""
+    rows, cols = 200, 8192
+    img = _img(oracle, 77, rows, cols, "smooth")
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    res = []
+    for on in (True, False):
+        ctx.set_eg_source(on)
+        _, (og, bg), (oe, be) = ctx.encode_gray(g, store_planes=False)
+        ctx.sync()
+        res.append((as_u64(og).copy(), as_u64(bg).copy(), as_u64(oe).copy(), as_u64(be).copy()))
+    for k in range(8):
+        assert np.array_equal(res[0][1], res[1][1]) and np.array_equal(res[0][3], res[1][3])
+        nw = (int(res[0][1][k]) + 63) // 64
+        assert np.array_equal(res[0][0][k][:nw], res[1][0][k][:nw])
+    assert np.array_equal(res[0][2], res[1][2])

@@ -134,3 +134,41 @@ def test_match_repeat_and_in_place(ctx, oracle):
         ctx.sync()
         assert np.array_equal(as_u64(d), exp["residual"])
         assert got["modes"].cpu().numpy().tobytes().decode() == exp["modes"]
+
+
+VAR_CASES = CASES[:8] + [
+    (4, 32, 64, 0, 10000, ("random", 0.03)),    # the drivers' default R: the whole image above
+    (8, 64, 64, 3, 10000, ("periodic", 8, 16, 0.5, 0.02)),
+    (6, 36, 72, 18, 20, ("random", 0.5)),       # T = worstd: compress5's exit at its first replacement
+    (6, 36, 72, 37, 20, ("random", 0.5)),       # T >= M + 1: every search ends after its first window
+    (16, 256, 256, 0, 10000, ("periodic", 24, 40, 0.5, 0.001)),  # region beyond the LDS image
+    (8, 96, 200, 0, 10000, ("text",)),
+]
+
+
+@pytest.mark.parametrize("parts", [0, 1, 5])
+@pytest.mark.parametrize("variant", [4, 5, 6])
+@pytest.mark.parametrize("case", range(len(VAR_CASES)))
+def test_match_encode_variants(ctx, oracle, case, variant, parts):
+    """bic_match_encode_var (the loops of compress4/5/6_test.cpp) against the oracle's
+    bo_match_encode_var, itself pinned to each driver's loop over the reference objects
+    (test_ref_crosscheck.py::test_match_encode_variants); automatic and fixed per-tile splits"""
+    from oracle_lib import match_encode_var
+    W, rows, cols, T, R, spec = VAR_CASES[case]
+    I = make_input(oracle, 7000 + case, rows, cols, spec)
+    e = oracle.enum_table(W)
+    exp = match_encode_var(oracle, I, cols, W, T, R, e, variant)
+    ctx.set_match_parts(parts)
+    try:
+        got = ctx.match_encode(ctx.to_dev(I), cols, W, T, R, e, variant=variant)
+        ctx.sync()
+    finally:
+        ctx.set_match_parts(0)
+    for k in ("besti", "bestj", "bestd", "weights"):
+        assert np.array_equal(got[k].cpu().numpy().view(np.uint32), exp[k]), k
+    assert got["modes"].cpu().numpy().tobytes().decode() == exp["modes"]
+    assert np.array_equal(as_u64(got["resid"]), exp["residual"])
+    st = as_u64(got["stats"])
+    assert [int(x) for x in st] == [exp["matches"], exp["bits_match"], exp["bits_nomatch"], exp["L"]]
+    assert stream_bytes(got["stream_match"], st[1]) == exp["stream_match"].tobytes()
+    assert stream_bytes(got["stream_nomatch"], st[2]) == exp["stream_nomatch"].tobytes()

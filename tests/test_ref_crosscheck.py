@@ -127,6 +127,33 @@ def test_match_encode_inverted(oracle, ref, case):
         assert a["inverted"].any()  # the inputs exercise the inversion
 
 
+VAR_CASES = MATCH_CASES + [
+    (4, 32, 64, 0, 10000, ("random", 0.03)),   # the drivers' default R: the whole image above
+    (8, 64, 64, 3, 10000, ("periodic", 8, 16, 0.5, 0.02)),
+    (6, 36, 72, 18, 20, ("random", 0.5)),      # T = worstd: compress5's exit at its first replacement
+    (6, 36, 72, 37, 20, ("random", 0.5)),      # T >= M + 1: every search ends after its first window
+]
+
+
+@pytest.mark.parametrize("variant", [4, 5, 6])
+@pytest.mark.parametrize("case", range(len(VAR_CASES)))
+def test_match_encode_variants(oracle, ref, variant, case):
+    """compress4/5/6_test.cpp's loops: the oracle's bo_match_encode_var == each driver's loop over the
+    reference's own get_submatrix / dist / add / weight / set_submatrix / GolombCoder"""
+    from oracle_lib import match_encode_var
+    W, rows, cols, T, R, spec = VAR_CASES[case]
+    I = match_input(oracle, 6000 + case, rows, cols, spec)
+    e = oracle.enum_table(W)
+    a = match_encode_var(oracle, I, cols, W, T, R, e, variant, want_stream=False)
+    b = ref.match_loop_var(I, cols, W, T, R, e, variant)
+    for k in ("besti", "bestj", "bestd", "weights", "residual"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in ("modes", "matches", "bits_match", "bits_nomatch", "L"):
+        assert a[k] == b[k], k
+    if spec[0] == "periodic" and variant != 5:  # (compress5 prefers windows at distance just below M / 2)
+        assert a["matches"] > 0  # the inputs exercise the match branch
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_gf2_algebra(oracle, ref, seed):
     """bo_gf2_mul / bo_gf2_transpose vs the reference's mul() and transpose_to on fresh shapes
