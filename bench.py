@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--plane-count", type=int, default=8,
                     help="c3 --shard planes: encode planes 0..P-1 of the image (split over the ranks); P = 1 or 2 at "
                          "N = 1 measures the per-rank step of a plane-sharded 8- or 4-GPU run")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="c4 / c3 --shard planes at N > 1: encode a rank's units in this many chunks, each chunk's "
+                         "streams sent to rank 0 while the next encodes (pybic.parallel.ChunkedGather); 0 = auto "
+                         "(2 for c4, 1 per plane for --shard planes), 1 = one gather after the encode")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
@@ -348,6 +352,12 @@ class C3Planes(C3):
         # a rank with no plane (N > P) sends an empty stream: its offsets stay zero
         self.off_g, self.off_e = (ctx.torch.zeros(n + 1, dtype=t.int64, device=ctx.dev) for _ in range(2))
         self.gathered = (None, None)
+        # overlapped gather (N > 1): the rank's planes in chunks (default one per plane), each chunk's
+        # packed streams sent while the next chunk encodes
+        nch = max(1, min(args.chunks or self.nplanes, self.nplanes)) if world > 1 else 1
+        self.chunks = [(i * self.nplanes // nch, (i + 1) * self.nplanes // nch) for i in range(nch)]
+        self.chunk_off = [[ctx.torch.zeros(b - a + 1, dtype=t.int64, device=ctx.dev) for _ in range(2)]
+                          for a, b in self.chunks]
         ctx.reserve(n, self.rows, self.cols)
         self.k = 0
         self.separate = False
@@ -357,8 +367,23 @@ class C3Planes(C3):
                          f"rank 0")
 
     def step(self):
-        from pybic.parallel import gather_streams
+        from pybic.parallel import ChunkedGather, gather_streams
         c = self.ctx
+        if self.world > 1 and len(self.chunks) > 1:
+            cgs = (ChunkedGather(c.dev, self.world, self.rank), ChunkedGather(c.dev, self.world, self.rank))
+            for (a, b), (fg, fe) in zip(self.chunks, self.chunk_off):
+                rg = self.out_g[a * self.slot_g:b * self.slot_g]
+                re = self.out_e[a * self.slot_e:b * self.slot_e]
+                c.encode_gray_packed(self.gray[self.k & 1], nplanes=b - a, plane0=self.lo + a,
+                                     planes=None if self.planes is None else self.planes[a:b],
+                                     slots=(self.slot_g, self.slot_e), outs=(rg, re),
+                                     bits=(self.bits_g[a:b], self.bits_e[a:b]), offs=(fg, fe),
+                                     store_planes=self.store_planes)
+                cgs[0].add(rg, fg[-1:])
+                cgs[1].add(re, fe[-1:])
+            self.gathered = (cgs[0].finish(), cgs[1].finish())
+            self.k += 1
+            return
         if self.nplanes:  # both streams written packed (word-aligned, plane order): the gather sends them as is
             c.encode_gray_packed(self.gray[self.k & 1], nplanes=self.nplanes, plane0=self.lo, planes=self.planes,
                                  slots=(self.slot_g, self.slot_e), outs=(self.out_g, self.out_e),
@@ -565,6 +590,11 @@ class C4(C3):
         self.packed = ctx.empty_i64(max(1, self.nplanes) * self.slot_g)  # the streams, word-aligned back to back
         self.word_off = ctx.torch.zeros(self.nplanes + 1, dtype=t.int64, device=ctx.dev)
         self.gathered = (None, None)
+        # overlapped gather (N > 1): the rank's frames in chunks, each chunk's packed streams in its own
+        # region of `packed`, sent while the next chunk encodes
+        nch = max(1, min(args.chunks or 2, self.nplanes)) if world > 1 else 1
+        self.chunks = [(i * self.nplanes // nch, (i + 1) * self.nplanes // nch) for i in range(nch)]
+        self.chunk_off = [ctx.torch.zeros(b - a + 1, dtype=t.int64, device=ctx.dev) for a, b in self.chunks]
         ctx.reserve(max(1, self.nplanes), self.rows, self.cols)
         self.k = 0
         self.pixels = self.rows * self.cols * self.nplanes
@@ -582,16 +612,29 @@ class C4(C3):
         return rand_words(t, (max(1, len(self.share(r))), self.rows, self.wpr), self.ctx.dev, g)
 
     def step(self):
-        from pybic.parallel import gather_streams
+        from pybic.parallel import ChunkedGather, gather_streams
         c = self.ctx
         # packed output: the encoder writes each frame's stream at its packed word offset (no slots, no
         # pack kernel), ready for the gather
-        if self.nplanes:
-            c.encode_planes_packed(self.planes[:self.nplanes], self.cols, True, golomb=True, eg=False,
-                                   slots=(self.slot_g, None), outs=(self.packed, None), bits=(self.bits_g, None),
-                                   offs=(self.word_off, None))
-        if self.world > 1:
-            self.gathered = gather_streams(self.packed, self.word_off[-1:], self.world, self.rank)
+        if self.world > 1 and len(self.chunks) > 1:
+            cg = ChunkedGather(c.dev, self.world, self.rank)
+            for (a, b), off in zip(self.chunks, self.chunk_off):
+                if b > a:
+                    region = self.packed[a * self.slot_g:b * self.slot_g]
+                    c.encode_planes_packed(self.planes[a:b], self.cols, True, golomb=True, eg=False,
+                                           slots=(self.slot_g, None), outs=(region, None),
+                                           bits=(self.bits_g[a:b], None), offs=(off, None))
+                    cg.add(region, off[-1:])
+                else:
+                    cg.add(self.packed[:0], 0)
+            self.gathered = cg.finish()
+        else:
+            if self.nplanes:
+                c.encode_planes_packed(self.planes[:self.nplanes], self.cols, True, golomb=True, eg=False,
+                                       slots=(self.slot_g, None), outs=(self.packed, None),
+                                       bits=(self.bits_g, None), offs=(self.word_off, None))
+            if self.world > 1:
+                self.gathered = gather_streams(self.packed, self.word_off[-1:], self.world, self.rank)
         self.k += 1
 
     def collect(self):

@@ -55,6 +55,7 @@ struct bic_ctx {
   bool force_staged = false;   // BIC_OPT_STAGED: the staged encoder whatever the batch size
   bool one_stream = false;     // BIC_OPT_ONE_STREAM: no second stream for the staged encoder's emission
   bool eg_src_off = false;     // BIC_OPT_EG_SOURCE = 0: bic_encode_gray* stores R instead of writing EG
+  bool eg_src_one = false;     // BIC_OPT_EG_SOURCE = 2: one emission kernel for every row class
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -353,6 +354,7 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
   }
   if (option == BIC_OPT_EG_SOURCE) {
     ctx->eg_src_off = value == 0;
+    ctx->eg_src_one = value == 2;
     return BIC_OK;
   }
   return BIC_EINVAL;
@@ -587,6 +589,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   fs.off_e = off_eg;
   fs.index = out_golomb ? row_index : nullptr;
   fs.eg_src = eg_src;
+  fs.eg_src_one = ctx->eg_src_one;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
@@ -595,7 +598,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   stage(bic::kFusedPrep);
   timed(ctx, "bitplanes_count", [&] {
     bic::launch_gray_rows(ctx->cur, gray, pitch, g, predict ? 1 : 0, plane0, planes, fs.sones, fs.krec, fs.kpos,
-                          fs.counter, store_resid, eg_src ? out_eg : nullptr, slot_eg, eg_src ? fs.jfrag : nullptr);
+                          fs.counter, store_resid, eg_src ? out_eg : nullptr, slot_eg);
   });
   timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
   // (EG source: the emission is Golomb's alone, reading the residual rows from the EG stream)
@@ -666,14 +669,14 @@ int bic_decode_planes(bic_ctx* ctx, int coder, const uint64_t* streams, size_t s
                       size_t wpr, int predict, const uint8_t* p00, uint64_t* planes) {
   int rc = bind(ctx);
   if (rc) return rc;
-  if (coder != BIC_CODER_GOLOMB && coder != BIC_CODER_EG) return BIC_EINVAL;
+  if (coder != BIC_CODER_GOLOMB && coder != BIC_CODER_EG && coder != BIC_CODER_EG_ADAPTIVE) return BIC_EINVAL;
   if (nplanes < 1 || !geom_ok(rows, cols, wpr) || !bic::decode_supported((uint32_t)cols)) return BIC_EINVAL;
   if (rows == 0) return BIC_OK;
   if (!streams || !plane_bits || !planes || (slot_words == 0 && !word_off)) return BIC_EINVAL;
-  if (coder == BIC_CODER_GOLOMB && !index) return BIC_EINVAL;
+  if ((coder == BIC_CODER_GOLOMB || coder == BIC_CODER_EG_ADAPTIVE) && !index) return BIC_EINVAL;
   if ((rc = ensure_scratch(ctx, bic::decode_scratch_bytes((uint32_t)rows, (uint32_t)wpr, (uint32_t)nplanes)))) return rc;
   timed(ctx, "decode", [&] {
-    bic::launch_decode(ctx->cur, coder == BIC_CODER_GOLOMB ? 0 : 1, streams, slot_words, word_off, plane_bits, index,
+    bic::launch_decode(ctx->cur, coder == BIC_CODER_GOLOMB ? 0 : coder == BIC_CODER_EG ? 1 : 2, streams, slot_words, word_off, plane_bits, index,
                        p00, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, (uint32_t)nplanes, predict ? 1 : 0, planes,
                        ctx->scratch, ctx->flags);
   });
@@ -715,6 +718,27 @@ int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t 
     return BIC_OK;
   }
   return BIC_EINVAL;
+}
+
+int bic_egad_row_index(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
+                       int predict, uint64_t* index) {
+  int rc = bind(ctx);
+  if (rc) return rc;
+  if (nplanes < 1 || !geom_ok(rows, cols, wpr) || (rows && (!planes || !index))) return BIC_EINVAL;
+  if (rows == 0) return BIC_OK;
+  const uint64_t n = (uint64_t)rows * nplanes;
+  const size_t sb = (bic::egad_scratch_bytes(n) + 255) & ~(size_t)255;
+  if ((rc = ensure_scratch(ctx, sb + (size_t)nplanes * 8))) return rc;
+  // a slot no row can overflow: <= 17 bits per column and end-of-row (a '1' per zero or block, a
+  // '0' and <= 15 remainder bits per 1)
+  const uint64_t slot = ((uint64_t)rows * (cols + 1) * 17 + 63) / 64;
+  uint64_t* bits = reinterpret_cast<uint64_t*>(static_cast<char*>(ctx->scratch) + sb);
+  timed(ctx, "egad_row_index", [&] {
+    bic::launch_egad(ctx->cur, planes, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, (uint32_t)nplanes,
+                     predict ? 1 : 0, nullptr, slot, bits, ctx->scratch, ctx->flags, index);
+  });
+  BIC_HIP(hipGetLastError());
+  return BIC_OK;
 }
 
 int bic_golomb_encode_samples(bic_ctx* ctx, const uint32_t* samples, size_t n, uint64_t n0,

@@ -222,6 +222,115 @@ __global__ __launch_bounds__(256) void k_dec_golomb_lanes(DecArgs a) {
   if (bad) atomicOr(&a.flags[1], 2u);                     // malformed stream (bic_sync: BIC_EDATA)
 }
 
+// EG adaptive (BIC_CODER_EG_ADAPTIVE: eg.cpp:20-37 with incBlockSize enabled) in the read order of the
+// #if 0 decoder (eg.cpp:41-55): per run '1' = a full block (len += blockSize, then incBlockSize), until
+// a '0' and the g-bit remainder (then decBlockSize) -- or until a block passes the columns left,
+// which is the end-of-row '1' (no incBlockSize after it, as the encoder writes it). The lutIndex
+// saturates at 31 as in the encoder. The coder state is serial across the plane, so rows are decoded
+// independently from the egad row index (bic_egad_row_index: per row its first bit and the state
+// there; 32 = a fresh coder: index 0 but g = 1, eg.h:9). One lane per row; the leading 1s of the
+// next 64 stream bits are counted at once (the blocks), the remainder read as one field.
+__device__ __forceinline__ uint32_t egad_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
+__global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (uint64_t)a.rows * a.nplanes) return;
+  const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
+  const uint64_t* st = plane_stream(a, plane);
+  const uint64_t G = a.index[2 * id], S0 = a.index[2 * id + 1];
+  const uint64_t E = row + 1 < a.rows ? a.index[2 * id + 2] : a.plane_bits[plane];
+  bool over;
+  const uint64_t maxw = plane_words(a, plane, over);
+  uint64_t* dst = a.out + ((uint64_t)plane * a.rows + row) * a.wpr;
+  bool bad = over || E < G + 1 || S0 > 32;  // every row has at least its end-of-row '1'
+  const uint64_t len = bad ? 0 : E - G;
+  auto ld = [&](uint64_t i) -> uint64_t { return i < maxw ? bswap64(st[i]) : 0ull; };
+  uint64_t wi = G >> 6;
+  uint64_t w0 = bad ? 0 : ld(wi), w1 = bad ? 0 : ld(wi + 1);
+  uint32_t b = (uint32_t)(G & 63);
+  uint64_t used_bits = 0;
+  auto peek = [&]() -> uint64_t { return b ? (w0 << b) | (w1 >> (64 - b)) : w0; };
+  auto advance = [&](uint32_t nb) {  // nb <= 64
+    used_bits += nb;
+    b += nb;
+    if (b >= 64) {
+      b -= 64;
+      w0 = w1;
+      ++wi;
+      w1 = ld(wi + 1);
+    }
+  };
+  const bool pred = a.predict != 0;
+  const uint64_t p00 = (pred && row == 0 && a.p00 && a.p00[plane]) ? BIC_MSB : 0ull;
+  uint32_t ow = 0, carry = 0;
+  uint64_t acc = 0;
+  auto flush = [&]() {  // store word ow (as D when predicting: the row's prefix XOR)
+    uint64_t x = acc;
+    if (pred) {
+      if (row == 0 && ow == 0) x = (x & ~BIC_MSB) | p00;
+      x ^= x >> 1;
+      x ^= x >> 2;
+      x ^= x >> 4;
+      x ^= x >> 8;
+      x ^= x >> 16;
+      x ^= x >> 32;
+      const uint32_t par = (uint32_t)(x & 1ull);
+      if (carry) x = ~x;
+      carry ^= par;
+    }
+    if (ow == a.used - 1) x &= a.trail;
+    dst[ow] = x;
+    ++ow;
+    acc = 0;
+  };
+  uint32_t idx = S0 == 32 ? 0u : (uint32_t)S0, g = S0 == 32 ? 1u : egad_j(idx);
+  uint64_t bs = 1ull << g;
+  uint32_t j = 0;  // the row's next column
+  while (!bad) {
+    const uint64_t maxlen = (uint64_t)(a.cols - j);
+    uint64_t L = 0;
+    bool eol = false;
+    for (;;) {  // the run's '1's: full blocks, or the one that passes the row's end
+      const uint64_t y = peek();
+      const uint32_t c = y == ~0ull ? 64u : (uint32_t)__builtin_clzll(~y);
+      uint32_t t = 0;
+      while (t < c) {
+        L += bs;
+        ++t;
+        if (L > maxlen) {
+          eol = true;
+          break;
+        }
+        if (idx < 31) ++idx;
+        g = egad_j(idx);
+        bs = 1ull << g;
+      }
+      if (t) advance(t);
+      if (eol || c < 64 || used_bits > len) break;
+    }
+    if (used_bits > len) bad = true;
+    if (eol || bad) break;
+    advance(1);  // the '0'
+    const uint64_t rem = g ? peek() >> (64 - g) : 0ull;
+    advance(g);
+    L += rem;
+    if (idx > 0) --idx;
+    g = egad_j(idx);
+    bs = 1ull << g;
+    if (L >= maxlen || used_bits > len) {
+      bad = true;
+      break;
+    }
+    const uint32_t c = j + (uint32_t)L;  // the run's 1
+    while ((c >> 6) > ow) flush();
+    acc |= BIC_MSB >> (c & 63);
+    j = c + 1;
+  }
+  if (used_bits != len) bad = true;
+  while (ow < a.used) flush();
+  for (uint32_t w = a.used; w < a.wpr; ++w) dst[w] = 0;  // pad words
+  if (bad) atomicOr(&a.flags[1], 2u);                     // malformed stream (bic_sync: BIC_EDATA)
+}
+
 // Golomb, byte machine: still one lane per row, but every lane consumes its stream 8 bits per
 // step from one table lookup, instead of a codeword's serial chain per codeword.
 // The state between steps: the phase (S: at a codeword start, U0 / U1: inside the unary part of a
@@ -764,6 +873,8 @@ void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t s
 #else
     k_dec_golomb_nib<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
 #endif
+  } else if (coder == 2) {
+    k_dec_egad<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
   } else {
     (void)hipMemsetAsync(a.first_row, 0xff, (size_t)nplanes * 4, s);
     k_dec_eg_first<<<grid, 256, 0, s>>>(a);

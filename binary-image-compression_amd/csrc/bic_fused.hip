@@ -637,8 +637,8 @@ struct FusedArgs {
   // bic_encode_gray without planes (FusedScratch::eg_src): the count pass wrote the EG stream in its
   // uniform layout and the residual rows are read back from it (null: residual from planes)
   const uint64_t* esrc;
-  uint64_t* jfrag;  // the count pass's strip-edge fragments (2 per plane, row, strip)
-  uint64_t* efix;   // per plane: the EG bit to clear after the emission (eg_fix_bit)
+  uint64_t* efix;
+  uint32_t* cls_ids;  // FusedScratch::cls_ids (EG source: the class emission kernels' row lists)   // per plane: the EG bit to clear after the emission (eg_fix_bit)
 #ifdef BIC_STAMPS
   int known;
 #endif
@@ -1359,37 +1359,6 @@ __device__ __forceinline__ bool row_class(const FusedArgs& a, uint64_t id, uint3
   return true;
 }
 
-// EG source (FusedArgs::esrc): the stream words the count pass left as fragments -- one where each
-// strip of row r starts (the previous strip's or row's tail, this strip's head; row 0's strip 0 after
-// the stream's first bit, a '1') and the word holding the last row's end-of-row '1' -- assembled by
-// the thread of row r in the ONES scan (k_gray_strips writes jfrag[2 s] = head, jfrag[2 s + 1] = tail,
-// the last strip's tail with the end-of-row '1'). A strip starting on a word boundary has no head;
-// its predecessor's tail is then a whole word (the row ended at bit 63), stored here.
-__device__ __forceinline__ void eg_src_junctions(const FusedArgs& a, uint32_t plane, uint32_t r) {
-  const Geom& g = a.g;
-  const uint32_t ns = a.ns;
-  uint64_t* eo = a.out_e + (uint64_t)plane * a.slot_e;
-  const uint64_t* jf = a.jfrag + 2 * ((uint64_t)plane * g.rows + r) * ns;
-  uint64_t hd[kMaxStrips], tl[kMaxStrips];
-#pragma unroll
-  for (uint32_t s = 0; s < kMaxStrips; ++s) {
-    hd[s] = s < ns ? jf[2 * s] : 0;
-    tl[s] = s < ns ? jf[2 * s + 1] : 0;
-  }
-  uint64_t prev = r ? jf[-1] : BIC_MSB;  // (row r - 1's last tail)
-  const uint64_t B = eg_src_bit0(g, r);
-#pragma unroll
-  for (uint32_t s = 0; s <= kMaxStrips; ++s) {
-    const bool end = s == ns;  // the word after the row: only for the last row
-    if (s > ns || (end && r + 1 != g.rows)) break;
-    const uint64_t bb = end ? B + g.cols + 1 : B + (uint64_t)s * 4096;
-    const uint64_t v = prev | (end ? 0 : hd[s]);
-    if (bb & 63) eo[bb >> 6] = bswap64(v);
-    else if (s == 0 || end) eo[(bb >> 6) - 1] = bswap64(prev);
-    if (!end) prev = tl[s];
-  }
-}
-
 // Packed output: the planes' start words in each coder's buffer (streams word-aligned, plane order:
 // bic_pack_streams' layout) from the Golomb totals (LEN scan) and the EG lengths (rows (cols + 1), + 1
 // when the plane holds a residual 1: eg.cpp's first-run bit), each capped at the slot size so that an
@@ -1506,7 +1475,6 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       }
       const bool first1 = in && pre == 0 && v[i] > 0;  // the row holding the plane's first 1
       if (a.esrc) {
-        if (in) eg_src_junctions(a, plane, r);
         // EG source: the stream bit eg.cpp's first-run '0' makes differ from the uniform layout: the
         // first 1's own bit (the layout has a '1' there, the shifted ~R of the pixel before it)
         if (first1) {
@@ -1536,6 +1504,25 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
     }
   } else {
     const uint64_t cap = a.slot_g * 64;
+    if (a.cls_ids) {  // EG source: this chunk's k = 0 / k = 1 rows appended to the class lists
+      static_assert(kScanPer == 1, "one row per thread");
+      const uint32_t r = r0;
+      const uint64_t f = r < g.rows ? a.glen[base + r] : 0;
+      const bool ok = pre + v[0] <= cap && v[0] != 0;  // (an overflowing row is written by nobody)
+      const uint32_t c0 = ok && (f & kK0Row) ? 1u : 0u, c1 = ok && (f & kK1Row) ? 1u : 0u;
+      uint32_t t0, t1;
+      const uint32_t x0 = block_excl_scan<uint32_t>(c0, reinterpret_cast<uint32_t*>(tmp), t0);
+      const uint32_t x1 = block_excl_scan<uint32_t>(c1, reinterpret_cast<uint32_t*>(tmp), t1);
+      __shared__ uint32_t lb[2];
+      if (threadIdx.x == 0) {
+        lb[0] = t0 ? atomicAdd(a.counter + 4, t0) : 0u;
+        lb[1] = t1 ? atomicAdd(a.counter + 5, t1) : 0u;
+      }
+      __syncthreads();
+      const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+      if (c0) a.cls_ids[lb[0] + x0] = (uint32_t)(base + r);
+      if (c1) a.cls_ids[nrows + lb[1] + x1] = (uint32_t)(base + r);
+    }
 #pragma unroll
     for (uint32_t i = 0; i < kScanPer; ++i) {
       const uint32_t r = r0 + i;
@@ -1776,6 +1763,133 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   }
 }
 
+// ---- EG source: one light emission kernel per row class ------------------------------------------
+// With the residual rows read back from the EG stream (FusedArgs::esrc) the Golomb emission is split
+// by the class the prefix kernels proved for the row (the LEN scan's lists): rows whose codewords
+// all have k = 0 are shifted copies of the EG stream, inverted (k_emit_k0, no LDS, few registers:
+// many waves in flight per SIMD), rows whose codewords all have k = 1 go through the byte tables and
+// an LDS row image (k_emit_k1); mixed rows stay k_emit_rest's. Persistent waves, one row at a time.
+//
+// k = 0: the row's Golomb bits are R then the end-of-row '1' (GolombCoder.cpp:13-34 with k = 0: each
+// sample's zeros and its '1'), i.e. the EG row ~R '1' (eg.cpp:20-37) with its first cols bits inverted.
+// Output word t of the row (at bit Gb) holds row bits [64 t - g, 64 t - g + 64), g = Gb % 64: the
+// stream bits from Bsrc + 64 t - g (Bsrc: the row in the EG slot), one funnel shift per word.
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  const uint32_t n = __hip_atomic_load(a.counter + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nw = gridDim.x * 4;
+  const uint64_t L = (uint64_t)g.cols + 1;
+  for (uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+    const uint32_t id = a.cls_ids[i];
+    const uint32_t plane = id / g.rows, row = id % g.rows;
+    const uint64_t G = gb_abs(a, id, plane);
+    const uint32_t gs = (uint32_t)(G & 63);
+    const uint64_t w0 = G >> 6, nwo = ((G + L - 1) >> 6) - w0 + 1;  // output words (<= used + 2)
+    // stream bit of output word t's first bit: src = Bsrc - gs + 64 t (Bsrc - gs >= -63)
+    const int64_t s0 = (int64_t)((uint64_t)plane * a.slot_e * 64 + eg_src_bit0(g, row)) - (int64_t)gs;
+    const int64_t si = s0 >> 6;  // (floor: s0 may be negative for row 0 of plane 0)
+    const uint32_t d = (uint32_t)(s0 & 63);
+    const uint64_t* S = a.esrc;
+    // the words holding the row's bits through its end-of-row '1' (none past it: the slot may end there)
+    const int64_t jend = (int64_t)(((uint64_t)plane * a.slot_e * 64 + eg_src_bit0(g, row) + g.cols) >> 6);
+    uint64_t v[WPL + 1];
+#pragma unroll
+    for (int k = 0; k <= WPL; ++k) {
+      const int64_t j = si + 64 * k + lane;
+      v[k] = (j >= 0 && j <= jend) ? S[j] : 0ull;
+    }
+    const uint64_t eolw = (uint64_t)(g.cols + gs) >> 6, eolb = BIC_MSB >> ((g.cols + gs) & 63);
+#pragma unroll
+    for (int k = 0; k <= WPL; ++k) {
+      const uint32_t t = 64 * k + lane;
+      if (64 * k >= (int)nwo) break;
+      uint64_t nx = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v[k] >> 32), 0x130, 0xf, 0xf, true) << 32) |
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v[k], 0x130, 0xf, 0xf, true);
+      if (k < WPL) {
+        const uint64_t n0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v[k + 1 <= WPL ? k + 1 : k] >> 32), 0) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v[k + 1 <= WPL ? k + 1 : k], 0);
+        if (lane == 63) nx = n0;
+      }
+      const uint64_t hi = bswap64(v[k]);
+      uint64_t x = ~(d ? funnel64(hi, bswap64(nx), 64 - d) : hi);
+      // row bits outside [0, cols) are not the row's: before it (word 0's first gs bits) and from the
+      // end-of-row '1' on
+      if (t == 0) x &= ~0ull >> gs;
+      if (t >= eolw) x = t == eolw ? (x & ~((eolb << 1) - 1)) | eolb : 0ull;
+      if (t < nwo) {
+        const bool whole = (t != 0 || gs == 0) && (t != nwo - 1 || ((G + L) & 63) == 0);
+        if (whole) a.out_g[w0 + t] = bswap64(x);
+        else a.gfrag[2 * (uint64_t)id + (t == 0 ? 0 : 1)] = x;
+      }
+    }
+  }
+}
+
+// k = 1 rows: emit_known_row's byte-table path (encode_word_k1b into a 64-bit LDS row image, then
+// write_row64); rows whose image exceeds the window are listed for k_rows_global.
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
+  __shared__ uint32_t s_lut[512];
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
+  for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+  __syncthreads();  // the only workgroup barrier
+  constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  const uint32_t n = __hip_atomic_load(a.counter + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+    const uint32_t id = a.cls_ids[nrows + i];
+    const uint32_t plane = id / g.rows, row = id % g.rows;
+    uint64_t rr[WPL];
+    eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
+    const uint64_t L = a.glen[id] & kLenMask;
+    const uint64_t Gb = gb_abs(a, id, plane);
+    if (L > kCapBits) {  // k_rows_global writes the row
+      if (lane == 0) {
+        a.gslow[id] = a.row_o[id] + row + 1;
+        a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
+      }
+      continue;
+    }
+    uint4* z = reinterpret_cast<uint4*>(gimg);
+    for (int j = lane; j < kGImg / 4; j += 64) z[j] = make_uint4(0, 0, 0, 0);
+    uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
+    int jpc = -1;
+    uint32_t loc = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      if (t * 64 >= (int)g.used) break;
+      const uint32_t w = t * 64 + lane;
+      const uint64_t x = rr[t];
+      const int jp = step_jp(x, w, jpc);
+      const bool eol = w == g.used - 1;
+      const LaneEnc e = encode_word_k1b(x, w, jp, eol, g.cols, s_lut);
+      const uint32_t inc = wave_incl_sum_u32(e.len);
+      const uint32_t off = loc + inc - e.len;
+      loc += lane63_u32(inc);
+      if (!e.lng) {
+        if (e.head) lds_or64(img, off >> 6, BIC_MSB >> (off & 63));
+        place128_64(img, off + 1 + e.z, e.t0, e.t1, e.tlen);
+      } else {
+        LdsSink64 ls{img, 0, 0};
+        emit_word_k1(ls, off, x, w, jp, eol, g.cols);
+        ls.flush();
+      }
+    }
+    if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    write_row64(img, L, Gb, a.out_g, a.gfrag + 2 * (uint64_t)id);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // The rows the prefix kernels leave to this launch: Golomb rows with mixed k (per-codeword k,
 // encode_word; among the walked rows, counter[2]) and the EG row holding the plane's first 1 (with
 // its inserted '0'; walked, or listed by k_scan_rows in counter[3]). One workgroup per row, one word
@@ -1934,7 +2048,7 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
   return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024 + (size_t)g.nplanes * 8 * 4 + 64 +
-         n * kMaxStrips * 16;  // (jfrag: the EG source's strip-edge fragments)
+         n * 4 * 2 + 64;  // (cls_ids)
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -1967,7 +2081,7 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
     fs.gbase = fs.pones + g.nplanes;
     fs.ebase = fs.gbase + g.nplanes;
     fs.efix = fs.ebase + g.nplanes;
-    fs.jfrag = fs.efix + g.nplanes;
+    fs.cls_ids = reinterpret_cast<uint32_t*>(fs.efix + g.nplanes);
   }
   fs.ns = 1;
   fs.counted = false;
@@ -2007,8 +2121,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   // Golomb's alone and reads the residual rows from it
   const bool es = mode == kEncStaged && fs.eg_src && out_e && !a.off_e && !predict;
   a.esrc = es ? out_e : nullptr;
-  a.jfrag = es ? fs.jfrag : nullptr;
   a.efix = es ? fs.efix : nullptr;
+  a.cls_ids = es && out_g && !fs.eg_src_one ? fs.cls_ids : nullptr;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
 #endif
@@ -2089,9 +2203,20 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   if (dg && de) BIC_EMIT1(W, P, true, true, false) else if (dg) BIC_EMIT1(W, P, true, false, false) else BIC_EMIT1(W, P, false, true, false)
     if (predict) {
       if (wpl == 1) { BIC_EMIT(1, true); } else if (wpl == 2) { BIC_EMIT(2, true); } else { BIC_EMIT(4, true); }
-    } else if (es) {  // Golomb alone, the residual rows from the EG stream
+    } else if (es && !a.cls_ids) {  // Golomb alone, the residual rows from the EG stream, one kernel
       if (wpl == 1) { BIC_EMIT1(1, false, true, false, true); } else if (wpl == 2) { BIC_EMIT1(2, false, true, false, true); }
       else { BIC_EMIT1(4, false, true, false, true); }
+    } else if (es) {  // Golomb alone, the residual rows from the EG stream: one kernel per row class
+#define BIC_EMITC(W)                                                                                      \
+  {                                                                                                    \
+    k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                    \
+    static const int o0_ = occ_of(reinterpret_cast<const void*>(&k_emit_k0<W>));                      \
+    static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1<W>));                      \
+    k_emit_k0<W><<<egrid_of(o0_), 256, 0, s>>>(a);                                                     \
+    k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                     \
+  }
+      if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
+#undef BIC_EMITC
     } else {
       if (wpl == 1) { BIC_EMIT(1, false); } else if (wpl == 2) { BIC_EMIT(2, false); } else { BIC_EMIT(4, false); }
     }

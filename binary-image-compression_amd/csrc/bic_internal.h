@@ -53,8 +53,11 @@ void launch_scan_rows(hipStream_t s, const Geom& g, const ChunkScratch& cs);
 bool med_rows_supported(const Geom& g, const void* planes, const void* resid);
 // a9 adaptive EG (bic_egad.hip)
 size_t egad_scratch_bytes(uint64_t nrows);
+// out null: no emission (index only); index (nullable): per row its first bit in the plane's stream and
+// the coder state there (bic_egad_row_index)
 void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t nplanes,
-                 int predict, uint64_t* out, uint64_t slot, uint64_t* bits, void* scratch, uint32_t* flags);
+                 int predict, uint64_t* out, uint64_t slot, uint64_t* bits, void* scratch, uint32_t* flags,
+                 uint64_t* index = nullptr);
 // f1 decoders (bic_decode.hip)
 bool decode_supported(uint32_t cols);
 size_t decode_scratch_bytes(uint32_t rows, uint32_t wpr, uint32_t nplanes);
@@ -136,12 +139,14 @@ struct FusedScratch {
   uint64_t* index = nullptr;
   // EG source (bic_encode_gray without planes, slot output): the count pass (launch_gray_rows with
   // out_e) wrote the EG stream in its uniform layout (row r at bit r (cols + 1) + 1) instead of the
-  // residual planes, leaving the words across strip edges as fragments in jfrag (2 per plane, row,
-  // strip); the ONES scan assembles those, the Golomb kernels read the residual rows back from the
-  // stream, and one bit per plane (efix) is cleared after them (bic_fused.hip eg_src_junctions)
+  // residual planes; the Golomb kernels read the residual rows back from the stream, and one bit per
+  // plane (efix, found by the ONES scan) is cleared after them (bic_fused.hip eg_fix_bit)
   bool eg_src = false;
-  uint64_t* jfrag = nullptr;
   uint64_t* efix = nullptr;
+  // EG source: the LEN scan lists the rows whose codewords all have k = 0 (cls_ids[0 .. counter[4]))
+  // and all k = 1 (cls_ids[n ..], counter[5]) for the two class emission kernels (n = rows * planes)
+  uint32_t* cls_ids = nullptr;
+  bool eg_src_one = false;  // (A/B: the one emission kernel k_emit_known for every class instead)
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
@@ -169,12 +174,11 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
 uint32_t gray_strips(const Geom& g);
 // store_resid: the words stored are the med residual R (planes = the caller's bitplanes are not
 // wanted; the encoder then reads R with predict off), not the bitplanes P. out_e (with predict, the
-// bitplanes not wanted): the EG stream instead of R (FusedScratch::eg_src; slot eg_stride words,
-// strip-edge fragments to jfrag); planes is then unused
+// bitplanes not wanted): the EG stream instead of R (FusedScratch::eg_src; slots of eg_stride
+// words); planes is then unused
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero,
-                      bool store_resid = false, uint64_t* out_e = nullptr, uint64_t eg_stride = 0,
-                      uint64_t* jfrag = nullptr);
+                      bool store_resid = false, uint64_t* out_e = nullptr, uint64_t eg_stride = 0);
 // the count pass can write the EG stream (FusedScratch::eg_src): rows of whole 64-word strips only
 bool gray_eg_supported(const Geom& g);
 

@@ -546,10 +546,12 @@ constexpr bool kGrayByteMed = BIC_GRAY_BYTEMED != 0;
 // EGS (FULL strips of rows of whole strips, BM): the EG stream instead of R (eg.cpp:20-37 with the
 // block size fixed at 1: per row ~R then the end-of-row '1'), in the uniform layout -- bit 0 a '1', row
 // r at bit r (cols + 1) + 1 of plane b's slot (word b * eg_stride) -- which is the stream but for one
-// bit (bic_fused.hip eg_src_junctions / eg_fix_bit). With the strip's first bit at offset e of a word,
-// lane l < 63 stores the word that starts inside its own row word (its bits and lane l + 1's); the
-// two words across the strip's edges are left as fragments: head (lane 0's bits in the first word),
-// tail (lane 63's bits, and on a row's last strip its '1', in the word after) -> jfrag.
+// bit (bic_fused.hip eg_fix_bit). With the strip's first bit at offset e of a word, lane l stores the
+// word that starts inside its own row word: its bits and lane l + 1's; lane 63's word crosses the
+// strip's end, so the wave also forms the first word of what follows -- the next strip's, or after
+// the row's '1' the next row's -- from one pixel per lane of that segment (two byte loads, the med on
+// the bytes, one ballot per plane): every stream word is stored whole, by exactly one wave, and the
+// wave of row 0's first strip also stores word 0 (the stream's first bit, then the row's first bits).
 template <bool PREDICT, bool STORE_R>
 constexpr int gray_rows_per_wave() { return kGrayByteMed && PREDICT && STORE_R ? kGrayRowsBM : kGrayRowsP; }
 // 64 bytes from src at any alignment (MIS: src not 16-byte aligned): the aligned 16-byte chunks that
@@ -596,8 +598,7 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
                                                 uint32_t ns, uint32_t s, uint32_t r0, uint32_t plane0,
                                                 uint64_t* __restrict__ planes, uint32_t* __restrict__ sones,
                                                 int4* __restrict__ krec, uint32_t* __restrict__ kpos, uint32_t* tw,
-                                                uint64_t* __restrict__ out_e, uint64_t eg_stride,
-                                                uint64_t* __restrict__ jfrag) {
+                                                uint64_t* __restrict__ out_e, uint64_t eg_stride) {
   const int lane = lane_id();
   const int np = NP8 ? 8 : (int)g.nplanes;
   const uint32_t w = s * 64 + lane;
@@ -650,6 +651,16 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
     uint4 nxt[4];
     uint32_t nlb = 0;
     if (kGrayPrefetch && r + 1 < nr) load(row + 1, nxt, nlb);
+    // EGS: the D byte of pixel `lane` of the segment after this strip (the next strip of the row, or
+    // the next row's first pixels; none after the last row)
+    const bool lastS = s + 1 == ns;
+    const uint32_t rn = lastS ? row + 1 : row;
+    uint32_t gn = 0;
+    if (EGS && FULL && rn < g.rows) {
+      const uint8_t* cp = gray + (uint64_t)rn * pitch + (lastS ? 0u : (s + 1) * 4096u) + lane;
+      uint32_t cb = cp[0], ub = rn ? cp[-(int64_t)pitch] : 0u;
+      gn = (cb ^ ub) >> plane0;
+    }
     // D bits (8 planes per byte) of the pixel left of the word: lane l - 1's last, or the strip's
     // preceding pixel for lane 0 (0 at column 0)
     uint64_t pw[8];
@@ -671,6 +682,12 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
 #pragma unroll
       for (int d = 1; d < 16; ++d) hd[d] = gd[d] ^ __builtin_amdgcn_alignbyte(gd[d], gd[d - 1], 3);
       if (row == 0 && w == 0) hd[0] &= ~0xffu;  // pred.cpp never writes pP(0,0)
+      if constexpr (EGS && FULL) {  // the next segment's residual bytes: left of its first pixel this
+                                    // strip's last one (same row), or none (a row's first pixel)
+        uint32_t gl2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gn, 0x138, 0xf, 0xf, true);
+        if (lane == 0) gl2 = lastS ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)gd[15], 63) >> 24;
+        gn = (gn ^ gl2) & 0xffu;
+      }
       uint4 hv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) hv[q] = make_uint4(hd[4 * q], hd[4 * q + 1], hd[4 * q + 2], hd[4 * q + 3]);
@@ -692,10 +709,6 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
     const uint64_t ep = (uint64_t)row * (g.cols + 1) + 1 + (uint64_t)s * 4096;
     const uint32_t esh = (uint32_t)(ep & 63);
     uint64_t* eo = out_e + (ep >> 6) + lane;
-    // fragments: lane 0 the head, lane 63 the tail (one store instruction, two lanes)
-    uint64_t* jf = jfrag + 2 * ((uint64_t)row * ns + s) + (lane == 63 ? 1 : 0);
-    const uint64_t jstride = 2 * (uint64_t)g.rows * ns;
-    const uint64_t eol = s + 1 == ns ? BIC_MSB >> esh : 0;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       if (!NP8 && b >= np) break;
@@ -711,17 +724,21 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
       if (!EGS && STORE_R && in) planes[(uint64_t)b * g.plane_words + (uint64_t)row * g.wpr + w] = R;
       if constexpr (EGS && FULL) {
         const uint64_t E = ~R;
-        uint64_t fr;
+        // the 64 stream bits after this strip's: the next strip's first word, or the row's '1' and the
+        // next row's first 63 bits (the '1' alone after the last row)
+        uint64_t N = ~__builtin_bitreverse64(__ballot((gn >> b) & 1u));
+        if (lastS) N = BIC_MSB | (rn < g.rows ? N >> 1 : 0ull);
+        uint64_t* eb = eo + (uint64_t)b * eg_stride;
         if (esh == 0) {
-          eo[(uint64_t)b * eg_stride] = bswap64(E);
-          fr = lane == 63 ? eol : 0;
+          eb[0] = bswap64(E);
+          if (lastS && lane == 63) eb[1] = bswap64(N);  // the word the '1' opens (the next row's first)
         } else {
-          const uint64_t En = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(E >> 32), 0x130, 0xf, 0xf, true) << 32) |
-                              (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)E, 0x130, 0xf, 0xf, true);
-          if (lane != 63) eo[(uint64_t)b * eg_stride + 1] = bswap64(funnel64(E, En, esh));
-          fr = lane == 0 ? E >> esh : (E << (64 - esh)) | eol;
+          uint64_t En = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(E >> 32), 0x130, 0xf, 0xf, true) << 32) |
+                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)E, 0x130, 0xf, 0xf, true);
+          if (lane == 63) En = N;
+          eb[1] = bswap64(funnel64(E, En, esh));
+          if (row == 0 && s == 0 && lane == 0) eb[0] = bswap64(BIC_MSB | (E >> 1));  // stream bit 0, row 0
         }
-        if (lane == 0 || lane == 63) jf[(uint64_t)b * jstride] = fr;
       }
       strip_word_put(tb, b, R, (int32_t)(w * 64));
     }
@@ -748,8 +765,7 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
                                                         uint32_t ns, uint32_t plane0, uint64_t* __restrict__ planes,
                                                         uint32_t* __restrict__ sones, int4* __restrict__ krec,
                                                         uint32_t* __restrict__ kpos, uint32_t* __restrict__ zero,
-                                                        uint64_t* __restrict__ out_e, uint64_t eg_stride,
-                                                        uint64_t* __restrict__ jfrag) {
+                                                        uint64_t* __restrict__ out_e, uint64_t eg_stride) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   uint32_t* tw = tab[threadIdx.x >> 6];
@@ -760,13 +776,13 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
   // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
   if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
     gray_strip_rows<PREDICT, true, STORE_R, true, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
-                                                            tw, out_e, eg_stride, jfrag);
+                                                            tw, out_e, eg_stride);
   else if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
     gray_strip_rows<PREDICT, true, STORE_R, false, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
-                                                             tw, out_e, eg_stride, jfrag);
+                                                             tw, out_e, eg_stride);
   else if constexpr (!EGS)  // (EGS launches have whole strips only: gray_eg_supported)
     gray_strip_rows<PREDICT, false, STORE_R, false, false, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec,
-                                                                kpos, tw, nullptr, 0, nullptr);
+                                                                kpos, tw, nullptr, 0);
 }
 
 bool gray_eg_supported(const Geom& g) { return g.trail == ~0ull && g.used % 64 == 0 && g.used / 64 <= kMaxStrips; }
@@ -780,16 +796,16 @@ bool gray_rows_supported(const Geom& g, const void* gray, size_t pitch, const vo
 
 void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Geom& g, int predict, int plane0,
                       uint64_t* planes, uint32_t* sones, int4* krec, uint32_t* kpos, uint32_t* zero, bool store_resid,
-                      uint64_t* out_e, uint64_t eg_stride, uint64_t* jfrag) {
+                      uint64_t* out_e, uint64_t eg_stride) {
   const uint32_t ns = gray_strips(g);
   const uint32_t rpw = predict && store_resid ? gray_rows_per_wave<true, true>() : gray_rows_per_wave<true, false>();
   const uint64_t units = (uint64_t)(g.rows + rpw - 1) / rpw;  // row groups per strip
   const uint32_t grid = (uint32_t)((units * ns + kWaves - 1) / kWaves);
   const bool mis = pitch % 16 != 0 || reinterpret_cast<uintptr_t>(gray) % 16 != 0;  // e.g. a P5 raster in its file
-  const bool egs = out_e && jfrag && predict && store_resid && gray_eg_supported(g);
+  const bool egs = out_e && predict && store_resid && gray_eg_supported(g);
 #define BIC_GS(P, R, E, M) \
   k_gray_strips<P, R, E, M><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, \
-                                                    zero, out_e, eg_stride, jfrag)
+                                                    zero, out_e, eg_stride)
 #define BIC_GS2(P, R) { if (mis) BIC_GS(P, R, false, true); else BIC_GS(P, R, false, false); }
   if (egs) { if (mis) BIC_GS(true, true, true, true); else BIC_GS(true, true, true, false); }
   else if (predict) { if (store_resid) BIC_GS2(true, true) else BIC_GS2(true, false) }

@@ -29,7 +29,7 @@ EXPORTS = [
     "bic_patch_search", "bic_match_encode", "bic_set_match_parts", "bic_encode_gray",
     "bic_bitplanes_u8_range", "bic_encode_gray_range", "bic_encode_planes_packed", "bic_encode_gray_packed",
     "bic_row_index", "bic_decode_planes", "bic_pgm_bitplanes", "bic_pnm_parse_header",
-    "bic_gf2_transpose", "bic_gf2_mul", "bic_planes_to_gray", "bic_match_encode_inv", "bic_match_encode_var",
+    "bic_gf2_transpose", "bic_gf2_mul", "bic_planes_to_gray", "bic_match_encode_inv", "bic_match_encode_var", "bic_egad_row_index",
 ]
 
 # bic_gf2_mul ops (include/bic.h)
@@ -106,6 +106,7 @@ def load(path=LIB_PATH):
     sig("bic_match_encode", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_set_match_parts", i32, [vp, u32])
     sig("bic_match_encode_inv", i32, [vp, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
+    sig("bic_egad_row_index", i32, [vp, vp, i32, sz, sz, sz, i32, vp])
     sig("bic_match_encode_var", i32, [vp, i32, vp, sz, sz, sz, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp])
     sig("bic_encode_gray", i32, [vp, vp, sz, sz, sz, i32, vp, sz, i32, vp, sz, vp, vp, sz, vp])
     sig("bic_bitplanes_u8_range", i32, [vp, vp, sz, sz, sz, i32, i32, vp, sz])
@@ -353,6 +354,17 @@ class Context:
         self._chk(self.lib.bic_row_index(self.h, _p(planes), n, rows, cols, wpr, int(predict), _p(out)), "bic_row_index")
         return out
 
+    def egad_row_index(self, planes, cols, predict=True, out=None):
+        """bic_egad_row_index: int64 [nplanes * rows * 2] (per row: bit offset in the adaptive EG stream,
+        the coder state there)"""
+        planes = planes if planes.dim() == 3 else planes.unsqueeze(0)
+        n, rows, wpr = planes.shape
+        out = self.empty_i64(n * rows * 2) if out is None else out
+        self._bind_stream()
+        self._chk(self.lib.bic_egad_row_index(self.h, _p(planes), n, rows, cols, wpr, int(predict), _p(out)),
+                  "bic_egad_row_index")
+        return out
+
     def decode_planes(self, coder, streams, plane_bits, nplanes, rows, cols, predict=True, word_off=None,
                       row_index=None, p00=None, out=None, wpr=None):
         """bic_decode_planes: streams int64 [nplanes, slot] (slots) or [words] with word_off (packed)
@@ -396,7 +408,7 @@ class Context:
     def set_eg_source(self, on=True):
         """bic_encode_gray* without planes: the count pass writes the EG stream and the Golomb kernels
         read the residual rows back from it (BIC_OPT_EG_SOURCE, default on) -- off: the residual
-        planes in a context buffer"""
+        planes in a context buffer; 2: the EG source with one emission kernel for every row class"""
         self._chk(self.lib.bic_ctx_set_option(self.h, 6, int(on)), "bic_ctx_set_option")
 
     def set_multipass(self, on=True):

@@ -51,6 +51,93 @@ def gather_streams(packed, nwords, world=None, rank=None, dst=0):
     return None, None
 
 
+class ChunkedGather:
+    """gather_streams overlapped with the encode: a rank encodes its units (frames, planes) in chunks
+    and hands each chunk's packed words here right after enqueueing its encode (add). finish() then
+    walks the chunks in order: a communication stream waits for the chunk's encode only (an event on
+    the compute stream), exchanges the chunk's size (one small all-gather) and sends it to `dst` --
+    while the compute stream is already encoding the next chunks, so only the last chunk's transfer
+    is exposed. The host blocks on one chunk's size at a time (the receiver must post exact counts).
+    dst receives every (rank, chunk) into its own buffer and concatenates them in rank order, chunk
+    order: (words, offsets per rank) as gather_streams returns them. gloo (CPU tests) runs the same
+    protocol on host tensors, without streams."""
+
+    def __init__(self, device, world=None, rank=None, dst=0):
+        self.world = world or dist.get_world_size()
+        self.rank = dist.get_rank() if rank is None else rank
+        self.dst, self.device = dst, device
+        self.host = _host_only()
+        self.comm = None if self.host or device.type != "cuda" else torch.cuda.Stream(device)
+        self.parts = []
+
+    def add(self, packed, nwords):
+        """packed: this chunk's words (int64, first nwords used); nwords: 1-element int64 tensor (device)
+        or int, final once the encode enqueued on the current stream completes"""
+        ev = None
+        if self.comm is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        self.parts.append((packed, nwords, ev))
+
+    def _sizes(self, nwords):
+        t = nwords.reshape(-1)[:1].to(torch.int64) if torch.is_tensor(nwords) else torch.tensor([int(nwords)])
+        t = t.cpu() if self.host else t.to(self.device)
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(outs, t)
+        return [int(x) for x in torch.cat(outs).cpu()]  # (host sync: this chunk's size exchange only)
+
+    def finish(self):
+        got = {r: [] for r in range(self.world)}  # dst: per rank its chunks' words
+        reqs = []
+        cur = torch.cuda.current_stream(self.device) if self.comm is not None else None
+        for packed, nwords, ev in self.parts:
+            ctx = torch.cuda.stream(self.comm) if self.comm is not None else _null()
+            with ctx:
+                if ev is not None:
+                    self.comm.wait_event(ev)
+                sizes = self._sizes(nwords)
+                n = sizes[self.rank]
+                src = packed.cpu() if self.host else packed
+                if self.rank == self.dst:
+                    ops = []
+                    for r in range(self.world):
+                        if r == self.rank:
+                            got[r].append(src[:n])
+                        elif sizes[r]:
+                            buf = torch.empty(sizes[r], dtype=packed.dtype, device=src.device)
+                            got[r].append(buf)
+                            ops.append(dist.P2POp(dist.irecv, buf, r))
+                    if ops:
+                        reqs += dist.batch_isend_irecv(ops)
+                elif n:
+                    reqs += dist.batch_isend_irecv([dist.P2POp(dist.isend, src[:n].contiguous(), self.dst)])
+        with (torch.cuda.stream(self.comm) if self.comm is not None else _null()):
+            for q in reqs:
+                q.wait()
+            if self.rank != self.dst:
+                out = None
+            else:
+                offs = [0]
+                for r in range(self.world):
+                    offs.append(offs[-1] + sum(int(x.numel()) for x in got[r]))
+                chunks = [x for r in range(self.world) for x in got[r]]
+                out = torch.cat(chunks) if chunks else torch.empty(0, dtype=torch.int64)
+        if cur is not None:
+            cur.wait_stream(self.comm)  # the step ends with the streams on dst (and the sends done)
+        self.parts = []
+        if out is None:
+            return None, None
+        return out.to(self.device), offs
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def shard_state(count, total, device):
     """Exclusive prefix over ranks of (samples, accumulated error): the GolombCoder state a
     rank's first sample sees (Golomb.h:21-24) when the sequence is split in rank order."""

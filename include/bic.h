@@ -92,7 +92,8 @@ int bic_reserve(bic_ctx* ctx, int nplanes, size_t rows, size_t cols);
 /* BIC_OPT_EG_SOURCE = 0: bic_encode_gray* without planes stores the med residual planes in a ctx
  * buffer for the encoder (the round-3 path) instead of writing the EG stream from the count pass
  * and reading the residual rows back from it (default 1, slot output with the EG coder; same
- * streams: a cross-check and A/B hook). */
+ * streams: a cross-check and A/B hook); 2: the EG source with one emission kernel for every row
+ * class instead of one per class (A/B hook). */
 #define BIC_OPT_EG_SOURCE 6
 int bic_ctx_set_option(bic_ctx* ctx, int option, long value);
 
@@ -174,11 +175,18 @@ int bic_encode_gray_packed(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size
  * 16-byte aligned). */
 int bic_row_index(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
                   int predict, uint64_t* index);
+/* The row index of the adaptive EG coder (BIC_CODER_EG_ADAPTIVE; eg.cpp:20-37 with incBlockSize):
+ * [2 (p rows + r)] = the bit offset of row r's first codeword in plane p's stream, [2 (p rows + r) + 1]
+ * = the coder state there (eg.h's lutIndex, 0..31; 32 = a fresh coder, row 0: index 0, g = 1). From
+ * the planes (the encoder's map / resolve / length passes, no stream written). */
+int bic_egad_row_index(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t rows, size_t cols, size_t wpr,
+                       int predict, uint64_t* index);
 /* streams -> planes (device): slot_words > 0: plane p's stream at streams + p * slot_words;
  * slot_words == 0: packed, at streams + word_off[p], word_off[0..nplanes] as the packed encoders write
  * it (plane p owns words word_off[p] .. word_off[p + 1]). plane_bits: each stream's length; a length
  * past the plane's slot or packed words is malformed (nothing beyond them is read). Golomb needs
- * row_index (rows decode independently); EG finds the row of the plane's first 1 itself. predict:
+ * row_index (rows decode independently); EG finds the row of the plane's first 1 itself;
+ * BIC_CODER_EG_ADAPTIVE needs bic_egad_row_index's index (eg.cpp:41-55's read order). predict:
  * the streams code the med residual; P(0, 0), which med discards, comes from p00 (device, one byte
  * per plane; nullable: 0). cols <= 16384. A malformed stream (bad codeword, wrong length, missing
  * end-of-row bit) is reported by bic_sync as BIC_EDATA; the planes are then undefined. */

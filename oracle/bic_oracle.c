@@ -328,6 +328,32 @@ void bo_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, i
     free(R);
 }
 
+/* The adaptive EG coder (coder 2) with its state recorded at every row start: [2 i] = the stream bits
+ * before row i, [2 i + 1] = eg.h's lutIndex there, 32 for a fresh coder (lutIndex 0 with g = 1, eg.h:9). */
+void bo_egad_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, int predict, uint64_t* index) {
+    const uint64_t* src = plane;
+    uint64_t* R = NULL;
+    if (predict) {
+        R = (uint64_t*)malloc(sizeof(uint64_t) * rows * wpr + 8);
+        bo_med(plane, R, rows, cols, wpr);
+        src = R;
+    }
+    bo_eg e;
+    bo_eg_init(&e, 1);
+    for (size_t i = 0; i < rows; ++i) {
+        index[2 * i] = e.bitcount;
+        index[2 * i + 1] = (e.lutIndex == 0 && e.g == 1) ? 32u : (uint64_t)e.lutIndex;
+        long last = -1;
+        for (size_t j = 0; j < cols; ++j)
+            if (bo_get(src, wpr, i, j)) {
+                bo_eg_code(&e, (int)((long)j - last - 1), 0, NULL);
+                last = (long)j;
+            }
+        bo_eg_code(&e, (int)((long)cols - 1 - last), 1, NULL);
+    }
+    free(R);
+}
+
 size_t bo_plane_runs(const uint64_t* plane, size_t rows, size_t cols, size_t wpr,
                      uint32_t* runs, uint8_t* eols, size_t cap) {
     size_t n = 0;

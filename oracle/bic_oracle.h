@@ -133,6 +133,9 @@ int64_t bo_eg_runs(const int32_t* len, const uint8_t* eol, size_t n, int adaptiv
 /* The decoders' row index (bic.h bic_row_index): per row, the Golomb stream's bit offset of
  * the row's first codeword and the residual 1s of the plane before the row. */
 void bo_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, int predict, uint64_t* index);
+/* the adaptive EG coder's row index: per row the stream bits before it and the coder state (lutIndex,
+ * 32 = fresh) at its start */
+void bo_egad_row_index(const uint64_t* plane, size_t rows, size_t cols, size_t wpr, int predict, uint64_t* index);
 /* inverse med with P(0,0) = corner */
 void bo_unmed(const uint64_t* R, uint64_t* P, size_t rows, size_t cols, size_t wpr, int corner);
 

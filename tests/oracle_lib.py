@@ -45,6 +45,7 @@ class Oracle:
         _sig(L, "bo_decode_plane_golomb", C.c_int, [u8p, C.c_uint64, sz, sz, sz, C.c_int, C.c_int, u64p])
         _sig(L, "bo_unmed", None, [u64p, u64p, sz, sz, sz, C.c_int])
         _sig(L, "bo_row_index", None, [u64p, sz, sz, sz, C.c_int, u64p])
+        _sig(L, "bo_egad_row_index", None, [u64p, sz, sz, sz, C.c_int, u64p])
         _sig(L, "bo_eg_runs", C.c_int64, [i32p, u8p, sz, C.c_int, u8p, sz, u32p])
         _sig(L, "cf_encode_planes", C.c_uint64, [u64p, C.c_int, sz, sz, sz, C.c_int, C.c_int, u64p, C.c_uint64, u64p,
                                                   C.c_uint64, u64p, u64p, C.POINTER(C.c_int)])
@@ -186,6 +187,14 @@ class Oracle:
         rows, wpr = P.shape
         out = np.zeros(2 * rows, np.uint64)
         self.lib.bo_row_index(ptr(P, u64p), rows, cols, wpr, predict, ptr(out, u64p))
+        return out
+
+    def egad_row_index(self, P, cols, predict):
+        """per row: (adaptive EG bit offset of its first codeword, coder state there: lutIndex, 32 fresh)"""
+        P = np.ascontiguousarray(P)
+        rows, wpr = P.shape
+        out = np.zeros(2 * rows, np.uint64)
+        self.lib.bo_egad_row_index(ptr(P, u64p), rows, cols, wpr, predict, ptr(out, u64p))
         return out
 
     def get_submatrix(self, I, cols, i0, i1, j0, j1):

@@ -128,3 +128,45 @@ def test_decode_rejects(ctx):
         ctx.decode_planes(CODER_GOLOMB, t, b, 4, 10, 64, True)  # Golomb without a row index
     with pytest.raises(pybic.BicError):
         ctx.decode_planes(CODER_EG, t, b, 4, 10, 20000, True)  # rows wider than 16384 columns
+
+
+@pytest.mark.parametrize("n,rows,cols,ps", [
+    (3, 40, 1000, (0.5, 0.2, 0.02)), (2, 17, 16384, (0.5, 0.05)), (4, 1, 64, (0.5, 0.0, 1.0, 0.3)),
+    (3, 70, 65, (0.5, 0.01, 0.9)), (2, 33, 4096, (0.0, 0.001)), (2, 9, 20000, (0.5, 0.03)),
+])
+@pytest.mark.parametrize("pred", [1, 0])
+def test_round_trip_eg_adaptive(ctx, oracle, n, rows, cols, ps, pred):
+    """BIC_CODER_EG_ADAPTIVE: GPU encode -> bic_egad_row_index (== the oracle's coder states at every
+    row start) -> GPU decode in eg.cpp:41-55's read order == the planes"""
+    P = _planes(oracle, n, rows, cols, ps, seed=0xEAD)
+    d = ctx.to_dev(P)
+    out, bits = ctx.encode_planes(d, cols, pred, pybic.CODER_EG_ADAPTIVE)
+    idx = ctx.egad_row_index(d, cols, pred)
+    ctx.sync()
+    ri = as_u64(idx).reshape(n, 2 * rows)
+    for k in range(n):
+        assert np.array_equal(ri[k], oracle.egad_row_index(P[k], cols, pred)), k
+    if cols > 16384:
+        return  # (the decoders take rows of up to 16384 columns)
+    back = ctx.decode_planes(pybic.CODER_EG_ADAPTIVE, out, bits, n, rows, cols, pred, row_index=idx,
+                             p00=_p00(ctx, P) if pred else None)
+    ctx.sync()
+    assert np.array_equal(as_u64(back), P)
+
+
+def test_malformed_eg_adaptive(ctx, oracle):
+    rows, cols = 30, 500
+    P = _planes(oracle, 1, rows, cols, (0.3,))
+    d = ctx.to_dev(P)
+    out, bits = ctx.encode_planes(d, cols, True, pybic.CODER_EG_ADAPTIVE)
+    idx = ctx.egad_row_index(d, cols, True)
+    ctx.sync()
+    bad_bits = bits.clone()
+    bad_bits[0] -= 1
+    ctx.decode_planes(pybic.CODER_EG_ADAPTIVE, out, bad_bits, 1, rows, cols, True, row_index=idx)
+    with pytest.raises(pybic.BicError) as e:
+        ctx.sync()
+    assert e.value.code == pybic.BIC_EDATA
+    back = ctx.decode_planes(pybic.CODER_EG_ADAPTIVE, out, bits, 1, rows, cols, True, row_index=idx, p00=_p00(ctx, P))
+    ctx.sync()
+    assert np.array_equal(as_u64(back), P)

@@ -188,6 +188,27 @@ def test_c2_full_eg_adaptive(ctx, oracle, p):
     assert stream_bytes(out[0], eb) == est.tobytes()
 
 
+def test_c3_full_eg_adaptive_round_trip(ctx, oracle):
+    """the adaptive EG coder at configs[2]'s size: the 8 planes of a 16384^2 gray image -> adaptive EG
+    streams -> the row index (coder state per row) -> decoded on the device == the planes; one plane's
+    stream and index against the oracle"""
+    import pybic
+    rows = cols = 16384
+    img = _gray(oracle, 0x5EED0006, rows, cols, "smooth")
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    planes = ctx.bitplanes_u8(g, nplanes=8)
+    out, bits = ctx.encode_planes(planes, cols, True, pybic.CODER_EG_ADAPTIVE)
+    idx = ctx.egad_row_index(planes, cols, True)
+    p00 = ctx.torch.from_numpy(((img[0, 0] >> np.arange(8)) & 1).astype(np.uint8)).to(ctx.dev)
+    back = ctx.decode_planes(pybic.CODER_EG_ADAPTIVE, out, bits, 8, rows, cols, True, row_index=idx, p00=p00)
+    ctx.sync()
+    assert ctx.torch.equal(back, planes)
+    P6 = pybic.as_u64(planes[6])
+    eb, est, _ = oracle.encode_plane(P6, cols, 1, 2)
+    assert int(as_u64(bits)[6]) == eb and stream_bytes(out[6], eb) == est.tobytes()
+    assert np.array_equal(as_u64(idx).reshape(8, 2 * rows)[6], oracle.egad_row_index(P6, cols, 1))
+
+
 def test_c3_p5_file_full(ctx, oracle):
     """configs[2] from a P5 file's bytes on the device: header parsed on the host, the planes of the
     raster in place (it starts 19 bytes into the file), both streams of every plane"""
