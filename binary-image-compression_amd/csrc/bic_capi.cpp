@@ -140,6 +140,18 @@ void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
       (void)hipStreamDestroy(st);
       return;
     }
+    // one fork / join round trip with a no-op launch before the stream carries work: measured on the
+    // pool's boxes, the first encode of a PROCESS whose k_emit_rest went to a fresh second stream came
+    // out wrong (its rows raced the prefix kernels) while every later one, and any first encode after
+    // such a round trip, was bit-exact (tools/dbg_egsrc5.py)
+    if (hipEventRecord(a, ctx->cur) != hipSuccess || hipStreamWaitEvent(st, a, 0) != hipSuccess ||
+        bic::launch_noop(st) != 0 || hipEventRecord(b, st) != hipSuccess || hipStreamWaitEvent(ctx->cur, b, 0) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+      (void)hipStreamDestroy(st);
+      return;
+    }
     ctx->aux = st;
     ctx->ev_fork = a;
     ctx->ev_join = b;

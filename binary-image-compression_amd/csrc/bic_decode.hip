@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
     acc = 0;
   };
   uint32_t idx = S0 == 32 ? 0u : (uint32_t)S0, g = S0 == 32 ? 1u : egad_j(idx);
-  uint64_t bs = 1ull << g;
+  uint64_t bs = S0 == 32 ? 1ull : 1ull << g;  // (a fresh coder's block is 1 with g = 1: eg.h:9)
   uint32_t j = 0;  // the row's next column
   while (!bad) {
     const uint64_t maxlen = (uint64_t)(a.cols - j);

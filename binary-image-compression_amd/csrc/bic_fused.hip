@@ -1510,6 +1510,12 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       const uint64_t f = r < g.rows ? a.glen[base + r] : 0;
       const bool ok = pre + v[0] <= cap && v[0] != 0;  // (an overflowing row is written by nobody)
       const uint32_t c0 = ok && (f & kK0Row) ? 1u : 0u, c1 = ok && (f & kK1Row) ? 1u : 0u;
+      // a mixed row too long for k_emit_rest's LDS image goes to k_rows_global (k_emit_k1 lists its own)
+      constexpr uint32_t kCapBitsRest = (kGImg - kPad) * 32;
+      if (ok && !(f & (kK0Row | kK1Row)) && v[0] > kCapBitsRest) {
+        a.gslow[base + r] = a.row_o[base + r] + r + 1;
+        a.slow_ids[atomicAdd(a.slow_n, 1u)] = base + r;
+      }
       uint32_t t0, t1;
       const uint32_t x0 = block_excl_scan<uint32_t>(c0, reinterpret_cast<uint32_t*>(tmp), t0);
       const uint32_t x1 = block_excl_scan<uint32_t>(c1, reinterpret_cast<uint32_t*>(tmp), t1);
@@ -2042,6 +2048,12 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
                        uint32_t rows, uint64_t nrows) {
   const uint32_t grid = (uint32_t)((nrows + 255) / 256);
   k_fixup<<<grid, 256, 0, s>>>(boff, len, frag, out, boff, len, frag, out, rows, nrows, 0xffffffffu);
+}
+
+__global__ void k_noop() {}
+int launch_noop(hipStream_t s) {
+  k_noop<<<1, 64, 0, s>>>();
+  return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 // ------------------------------------------------------------------------------------

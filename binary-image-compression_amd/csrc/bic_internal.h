@@ -148,6 +148,8 @@ struct FusedScratch {
   uint32_t* cls_ids = nullptr;
   bool eg_src_one = false;  // (A/B: the one emission kernel k_emit_known for every class instead)
 };
+// an empty launch on stream s (0 when it was enqueued)
+int launch_noop(hipStream_t s);
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
 bool fused_supported(const Geom& g);
