@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--store-planes", action="store_true",
                     help="c3: bic_encode_gray also returns the 8 bitplanes (planes != NULL; +256 MiB written per "
                          "image); default: planes NULL, the count pass keeps the residual planes for the encoder")
+    ap.add_argument("--eg-source-mode", type=int, default=1,
+                    help="BIC_OPT_EG_SOURCE value when the EG source is on (1: row-class kernels, 2: one kernel)")
     ap.add_argument("--no-eg-source", action="store_true",
                     help="c3 (planes NULL): the round-3 path -- the count pass stores the med residual planes for "
                          "the encoder -- instead of writing the EG stream and reading the residual rows back from it")
@@ -226,7 +228,7 @@ class C3:
         # planes NULL: the count pass writes the EG stream and the Golomb emission reads the residual rows
         # from it (BIC_OPT_EG_SOURCE; off: the residual planes stored in a context buffer)
         self.eg_src = not self.store_planes and not args.no_eg_source
-        ctx.set_eg_source(self.eg_src)
+        ctx.set_eg_source(args.eg_source_mode if self.eg_src else 0)
         self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr) if self.store_planes else None
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)
@@ -488,7 +490,7 @@ class C3File(C3):
         self.separate = args.separate
         self.store_planes = args.separate or args.store_planes
         self.eg_src = not self.store_planes and not args.no_eg_source
-        ctx.set_eg_source(self.eg_src)
+        ctx.set_eg_source(args.eg_source_mode if self.eg_src else 0)
         self.planes = ctx.empty_i64(self.nplanes, self.rows, self.wpr) if self.store_planes else None
         self.slot_g = ctx.slot_words(self.rows, self.cols, pybic.CODER_GOLOMB)
         self.slot_e = ctx.slot_words(self.rows, self.cols, pybic.CODER_EG)

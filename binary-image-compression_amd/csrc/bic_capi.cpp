@@ -56,6 +56,7 @@ struct bic_ctx {
   bool one_stream = false;     // BIC_OPT_ONE_STREAM: no second stream for the staged encoder's emission
   bool eg_src_off = false;     // BIC_OPT_EG_SOURCE = 0: bic_encode_gray* stores R instead of writing EG
   bool eg_src_one = false;     // BIC_OPT_EG_SOURCE = 2: one emission kernel for every row class
+  int rest_order = 0;          // BIC_OPT_EG_SOURCE = 3 / 4 (diagnostic): k_emit_rest after / before the class kernels
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -132,23 +133,13 @@ void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
     hipStream_t st = nullptr;
     hipEvent_t a = nullptr, b = nullptr;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
-    // device-scope events: the fork / join only order two streams of this device (a system-scope
-    // release would write back L2 at every fork)
-    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+    // the fork / join events keep HIP's default (system-scope) fences: with device-scope events
+    // (hipEventDisableSystemFence) the first encode of a process read stale prefix data on the
+    // second stream (rows of the class kernels came out wrong; tools/dbg_egsrc8.py, 15 of 16 first
+    // encodes), with the default fences none did
+    const unsigned fl = hipEventDisableTiming;
     if (hipEventCreateWithFlags(&a, fl) != hipSuccess || hipEventCreateWithFlags(&b, fl) != hipSuccess) {
       if (a) (void)hipEventDestroy(a);
-      (void)hipStreamDestroy(st);
-      return;
-    }
-    // one fork / join round trip with a no-op launch before the stream carries work: measured on the
-    // pool's boxes, the first encode of a PROCESS whose k_emit_rest went to a fresh second stream came
-    // out wrong (its rows raced the prefix kernels) while every later one, and any first encode after
-    // such a round trip, was bit-exact (tools/dbg_egsrc5.py)
-    if (hipEventRecord(a, ctx->cur) != hipSuccess || hipStreamWaitEvent(st, a, 0) != hipSuccess ||
-        bic::launch_noop(st) != 0 || hipEventRecord(b, st) != hipSuccess || hipStreamWaitEvent(ctx->cur, b, 0) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-      (void)hipEventDestroy(a);
-      (void)hipEventDestroy(b);
       (void)hipStreamDestroy(st);
       return;
     }
@@ -367,6 +358,7 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
   if (option == BIC_OPT_EG_SOURCE) {
     ctx->eg_src_off = value == 0;
     ctx->eg_src_one = value == 2;
+    ctx->rest_order = value == 3 ? 1 : (value == 4 ? 2 : 0);
     return BIC_OK;
   }
   return BIC_EINVAL;
@@ -602,6 +594,7 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   fs.index = out_golomb ? row_index : nullptr;
   fs.eg_src = eg_src;
   fs.eg_src_one = ctx->eg_src_one;
+  fs.rest_order = ctx->rest_order;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,

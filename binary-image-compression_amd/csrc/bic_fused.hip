@@ -2050,12 +2050,6 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
   k_fixup<<<grid, 256, 0, s>>>(boff, len, frag, out, boff, len, frag, out, rows, nrows, 0xffffffffu);
 }
 
-__global__ void k_noop() {}
-int launch_noop(hipStream_t s) {
-  k_noop<<<1, 64, 0, s>>>();
-  return hipGetLastError() == hipSuccess ? 0 : 1;
-}
-
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
@@ -2221,11 +2215,20 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     } else if (es) {  // Golomb alone, the residual rows from the EG stream: one kernel per row class
 #define BIC_EMITC(W)                                                                                      \
   {                                                                                                    \
-    k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                    \
+    if (fs.rest_order == 2) {                                                                          \
+      k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
+      if (rs != s) { (void)hipEventRecord(fs.ev_join, rs); (void)hipStreamWaitEvent(s, fs.ev_join, 0); } \
+    } else if (fs.rest_order == 0) {                                                                   \
+      k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
+    }                                                                                                  \
     static const int o0_ = occ_of(reinterpret_cast<const void*>(&k_emit_k0<W>));                      \
     static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1<W>));                      \
     k_emit_k0<W><<<egrid_of(o0_), 256, 0, s>>>(a);                                                     \
     k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                     \
+    if (fs.rest_order == 1) {                                                                          \
+      if (rs != s) { (void)hipEventRecord(fs.ev_fork, s); (void)hipStreamWaitEvent(rs, fs.ev_fork, 0); } \
+      k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
+    }                                                                                                  \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
 #undef BIC_EMITC

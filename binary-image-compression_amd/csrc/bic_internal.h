@@ -147,9 +147,8 @@ struct FusedScratch {
   // and all k = 1 (cls_ids[n ..], counter[5]) for the two class emission kernels (n = rows * planes)
   uint32_t* cls_ids = nullptr;
   bool eg_src_one = false;  // (A/B: the one emission kernel k_emit_known for every class instead)
+  int rest_order = 0;       // (diagnostic: 1 = k_emit_rest after the class kernels, 2 = before them)
 };
-// an empty launch on stream s (0 when it was enqueued)
-int launch_noop(hipStream_t s);
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);
 bool fused_supported(const Geom& g);

@@ -769,26 +769,20 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
   __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   uint32_t* tw = tab[threadIdx.x >> 6];
-  // persistent waves (a resident set of workgroups): a wave's unit of work -- one strip of a row group
-  // -- is short, and one workgroup per four units left the SIMDs' wave slots mostly empty, waiting on
-  // dispatch (r03 SQ counters: 1.6 waves resident per SIMD on average)
-  const uint64_t nunits = (uint64_t)((g.rows + gray_rows_per_wave<PREDICT, STORE_R>() - 1) /
-                                     gray_rows_per_wave<PREDICT, STORE_R>()) * ns;
-  const uint64_t stride = (uint64_t)gridDim.x * kWaves;
-  for (uint64_t u = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6); u < nunits; u += stride) {
-    const uint32_t s = (uint32_t)(u % ns);  // the strips of one row block are neighbouring waves
-    const uint32_t r0 = (uint32_t)(u / ns) * gray_rows_per_wave<PREDICT, STORE_R>();
-    // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
-    if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
-      gray_strip_rows<PREDICT, true, STORE_R, true, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec,
-                                                              kpos, tw, out_e, eg_stride);
-    else if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
-      gray_strip_rows<PREDICT, true, STORE_R, false, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec,
-                                                               kpos, tw, out_e, eg_stride);
-    else if constexpr (!EGS)  // (EGS launches have whole strips only: gray_eg_supported)
-      gray_strip_rows<PREDICT, false, STORE_R, false, false, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones,
-                                                                  krec, kpos, tw, nullptr, 0);
-  }
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  const uint32_t s = (uint32_t)(gw % ns);  // the strips of one row block are neighbouring waves
+  const uint32_t r0 = (uint32_t)(gw / ns) * gray_rows_per_wave<PREDICT, STORE_R>();
+  if (r0 >= g.rows) return;  // whole wave
+  // strips wholly inside a row without pad bits (every strip of C3) drop the masks and the lane tests
+  if ((s + 1) * 64 <= g.used && g.trail == ~0ull && g.nplanes == 8)
+    gray_strip_rows<PREDICT, true, STORE_R, true, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
+                                                            tw, out_e, eg_stride);
+  else if ((s + 1) * 64 <= g.used && g.trail == ~0ull)
+    gray_strip_rows<PREDICT, true, STORE_R, false, EGS, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec, kpos,
+                                                             tw, out_e, eg_stride);
+  else if constexpr (!EGS)  // (EGS launches have whole strips only: gray_eg_supported)
+    gray_strip_rows<PREDICT, false, STORE_R, false, false, MIS>(gray, pitch, g, ns, s, r0, plane0, planes, sones, krec,
+                                                                kpos, tw, nullptr, 0);
 }
 
 bool gray_eg_supported(const Geom& g) { return g.trail == ~0ull && g.used % 64 == 0 && g.used / 64 <= kMaxStrips; }
@@ -806,29 +800,12 @@ void launch_gray_rows(hipStream_t s, const uint8_t* gray, size_t pitch, const Ge
   const uint32_t ns = gray_strips(g);
   const uint32_t rpw = predict && store_resid ? gray_rows_per_wave<true, true>() : gray_rows_per_wave<true, false>();
   const uint64_t units = (uint64_t)(g.rows + rpw - 1) / rpw;  // row groups per strip
-  const uint32_t full = (uint32_t)((units * ns + kWaves - 1) / kWaves);
+  const uint32_t grid = (uint32_t)((units * ns + kWaves - 1) / kWaves);
   const bool mis = pitch % 16 != 0 || reinterpret_cast<uintptr_t>(gray) % 16 != 0;  // e.g. a P5 raster in its file
   const bool egs = out_e && predict && store_resid && gray_eg_supported(g);
-  // a resident set of workgroups (as many per CU as the instance's registers and LDS allow), or fewer
-  static thread_local int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
-  auto grid_of = [&](const void* fn) {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBlock, 0) != hipSuccess || occ < 1) occ = 4;
-    return (uint32_t)cus * (uint32_t)occ;
-  };
-#define BIC_GS(P, R, E, M)                                                                                     \
-  do {                                                                                                         \
-    static const uint32_t occ_grid_ = grid_of(reinterpret_cast<const void*>(&k_gray_strips<P, R, E, M>));      \
-    const uint32_t grid = std::min(full, occ_grid_);                                                          \
-    k_gray_strips<P, R, E, M><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, \
-                                                      kpos, zero, out_e, eg_stride);                          \
-  } while (0)
+#define BIC_GS(P, R, E, M) \
+  k_gray_strips<P, R, E, M><<<grid, kBlock, 0, s>>>(gray, pitch, g, ns, (uint32_t)plane0, planes, sones, krec, kpos, \
+                                                    zero, out_e, eg_stride)
 #define BIC_GS2(P, R) { if (mis) BIC_GS(P, R, false, true); else BIC_GS(P, R, false, false); }
   if (egs) { if (mis) BIC_GS(true, true, true, true); else BIC_GS(true, true, true, false); }
   else if (predict) { if (store_resid) BIC_GS2(true, true) else BIC_GS2(true, false) }

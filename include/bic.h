@@ -53,7 +53,9 @@ int bic_ctx_create(int device, bic_ctx** out);
 int bic_ctx_destroy(bic_ctx* ctx);
 /* Enqueue on an external hipStream_t (e.g. torch's current stream); NULL is the HIP null
  * (legacy default) stream. A new ctx enqueues on its own non-blocking stream, which
- * bic_ctx_own_stream returns. */
+ * bic_ctx_own_stream returns. A ctx's scratch arena and residual buffer (bic_encode_gray) are
+ * shared by all its calls, whatever stream is bound: calls enqueued on two different streams must
+ * not run concurrently (use one ctx per stream). */
 int bic_ctx_set_stream(bic_ctx* ctx, void* hip_stream);
 void* bic_ctx_get_stream(bic_ctx* ctx);
 void* bic_ctx_own_stream(bic_ctx* ctx);
@@ -138,9 +140,15 @@ int bic_encode_planes2(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
  * once: the bitplane kernel also produces the encoder's per-row counts. Otherwise the same result
  * through the two separate calls.
  * planes may be NULL (also in the _range / _packed forms below): the bitplanes are then formed in
- * registers only and not returned; the count pass stores each plane's med residual instead (in a
- * buffer the context keeps, nplanes * rows * wpr words), from which the encoder writes the same
- * streams without recomputing med (no row above, no prediction in the emission). */
+ * registers only and not returned. With the EG stream requested into slots (out_eg, no packed EG
+ * offsets) and predict = 1, the count pass writes the EG stream itself and the Golomb emission
+ * reads each residual row back out of it (no further buffer). Otherwise the count pass stores each
+ * plane's med residual in a buffer the context keeps (nplanes * rows * wpr words; it grows to the
+ * largest call and lives until bic_ctx_destroy), from which the encoder writes the same streams
+ * without recomputing med (no row above, no prediction in the emission).
+ * Reads of a gray row whose address or pitch is not 16-byte aligned round out to the enclosing
+ * aligned 16-byte chunks (never a chunk without one of the row's readable bytes, so never past the
+ * last page of the buffer, but up to 15 bytes beyond the readable range). */
 int bic_encode_gray(bic_ctx* ctx, const uint8_t* gray, size_t pitch, size_t rows, size_t cols, int nplanes,
                     uint64_t* planes, size_t wpr, int predict, uint64_t* out_golomb, size_t slot_golomb,
                     uint64_t* bits_golomb, uint64_t* out_eg, size_t slot_eg, uint64_t* bits_eg);
