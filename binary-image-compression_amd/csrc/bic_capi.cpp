@@ -56,7 +56,6 @@ struct bic_ctx {
   bool one_stream = false;     // BIC_OPT_ONE_STREAM: no second stream for the staged encoder's emission
   bool eg_src_off = false;     // BIC_OPT_EG_SOURCE = 0: bic_encode_gray* stores R instead of writing EG
   bool eg_src_one = false;     // BIC_OPT_EG_SOURCE = 2: one emission kernel for every row class
-  int rest_order = 0;          // BIC_OPT_EG_SOURCE = 3 / 4 (diagnostic): k_emit_rest after / before the class kernels
   struct Rec { const char* name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -358,7 +357,6 @@ int bic_ctx_set_option(bic_ctx* ctx, int option, long value) {
   if (option == BIC_OPT_EG_SOURCE) {
     ctx->eg_src_off = value == 0;
     ctx->eg_src_one = value == 2;
-    ctx->rest_order = value == 3 ? 1 : (value == 4 ? 2 : 0);
     return BIC_OK;
   }
   return BIC_EINVAL;
@@ -594,7 +592,6 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   fs.index = out_golomb ? row_index : nullptr;
   fs.eg_src = eg_src;
   fs.eg_src_one = ctx->eg_src_one;
-  fs.rest_order = ctx->rest_order;
   set_aux(ctx, fs);
   auto stage = [&](int st) {
     bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,

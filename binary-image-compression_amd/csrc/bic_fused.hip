@@ -638,7 +638,8 @@ struct FusedArgs {
   // uniform layout and the residual rows are read back from it (null: residual from planes)
   const uint64_t* esrc;
   uint64_t* efix;
-  uint32_t* cls_ids;  // FusedScratch::cls_ids (EG source: the class emission kernels' row lists)   // per plane: the EG bit to clear after the emission (eg_fix_bit)
+  uint32_t* cls_ids;  // FusedScratch::cls_ids (EG source: the class emission kernels' row lists)
+  uint64_t* cls_g;    // and each listed row's Golomb offset (gboff's value: one load with the id)
 #ifdef BIC_STAMPS
   int known;
 #endif
@@ -1510,24 +1511,40 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       const uint64_t f = r < g.rows ? a.glen[base + r] : 0;
       const bool ok = pre + v[0] <= cap && v[0] != 0;  // (an overflowing row is written by nobody)
       const uint32_t c0 = ok && (f & kK0Row) ? 1u : 0u, c1 = ok && (f & kK1Row) ? 1u : 0u;
-      // a mixed row too long for k_emit_rest's LDS image goes to k_rows_global (k_emit_k1 lists its own)
-      constexpr uint32_t kCapBitsRest = (kGImg - kPad) * 32;
-      if (ok && !(f & (kK0Row | kK1Row)) && v[0] > kCapBitsRest) {
+      // mixed rows: k_emit_mix's list when the LDS image holds them, else k_rows_global's
+      // (k_emit_k1 lists its own long rows)
+      constexpr uint32_t kCapBitsMix = (kGImg - kPad) * 32;
+      const bool mixed = ok && !(f & (kK0Row | kK1Row));
+      if (mixed && v[0] > kCapBitsMix) {
         a.gslow[base + r] = a.row_o[base + r] + r + 1;
         a.slow_ids[atomicAdd(a.slow_n, 1u)] = base + r;
       }
-      uint32_t t0, t1;
+      const uint32_t c2 = mixed && v[0] <= kCapBitsMix ? 1u : 0u;
+      uint32_t t0, t1, t2;
       const uint32_t x0 = block_excl_scan<uint32_t>(c0, reinterpret_cast<uint32_t*>(tmp), t0);
       const uint32_t x1 = block_excl_scan<uint32_t>(c1, reinterpret_cast<uint32_t*>(tmp), t1);
-      __shared__ uint32_t lb[2];
+      const uint32_t x2 = block_excl_scan<uint32_t>(c2, reinterpret_cast<uint32_t*>(tmp), t2);
+      __shared__ uint32_t lb[3];
       if (threadIdx.x == 0) {
         lb[0] = t0 ? atomicAdd(a.counter + 4, t0) : 0u;
         lb[1] = t1 ? atomicAdd(a.counter + 5, t1) : 0u;
+        lb[2] = t2 ? atomicAdd(a.counter + 6, t2) : 0u;
       }
       __syncthreads();
       const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-      if (c0) a.cls_ids[lb[0] + x0] = (uint32_t)(base + r);
-      if (c1) a.cls_ids[nrows + lb[1] + x1] = (uint32_t)(base + r);
+      const uint64_t G = (uint64_t)plane * cap + pre;  // (gboff's value, written below)
+      if (c0) {
+        a.cls_ids[lb[0] + x0] = (uint32_t)(base + r);
+        a.cls_g[lb[0] + x0] = G;
+      }
+      if (c1) {
+        a.cls_ids[nrows + lb[1] + x1] = (uint32_t)(base + r);
+        a.cls_g[nrows + lb[1] + x1] = G;
+      }
+      if (c2) {
+        a.cls_ids[2 * nrows + lb[2] + x2] = (uint32_t)(base + r);
+        a.cls_g[2 * nrows + lb[2] + x2] = G;
+      }
     }
 #pragma unroll
     for (uint32_t i = 0; i < kScanPer; ++i) {
@@ -1787,10 +1804,15 @@ __global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
   const uint32_t n = __hip_atomic_load(a.counter + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nw = gridDim.x * 4;
   const uint64_t L = (uint64_t)g.cols + 1;
-  for (uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6); i < n; i += nw) {
-    const uint32_t id = a.cls_ids[i];
+  uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  // the list entry (row id, Golomb offset) of the wave's next row is loaded while this one is copied:
+  // a row costs one memory round trip (its words), not three (entry, offset, words)
+  uint32_t id_n = i < n ? a.cls_ids[i] : 0u;
+  uint64_t G_n = i < n ? a.cls_g[i] : 0ull;
+  for (; i < n; i += nw) {
+    const uint32_t id = id_n;
     const uint32_t plane = id / g.rows, row = id % g.rows;
-    const uint64_t G = gb_abs(a, id, plane);
+    const uint64_t G = a.off_g ? G_n - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G_n;
     const uint32_t gs = (uint32_t)(G & 63);
     const uint64_t w0 = G >> 6, nwo = ((G + L - 1) >> 6) - w0 + 1;  // output words (<= used + 2)
     // stream bit of output word t's first bit: src = Bsrc - gs + 64 t (Bsrc - gs >= -63)
@@ -1805,6 +1827,10 @@ __global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
     for (int k = 0; k <= WPL; ++k) {
       const int64_t j = si + 64 * k + lane;
       v[k] = (j >= 0 && j <= jend) ? S[j] : 0ull;
+    }
+    if (i + nw < n) {
+      id_n = a.cls_ids[i + nw];
+      G_n = a.cls_g[i + nw];
     }
     const uint64_t eolw = (uint64_t)(g.cols + gs) >> 6, eolb = BIC_MSB >> ((g.cols + gs) & 63);
 #pragma unroll
@@ -1848,13 +1874,20 @@ __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t n = __hip_atomic_load(a.counter + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nw = gridDim.x * 4;
-  for (uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6); i < n; i += nw) {
-    const uint32_t id = a.cls_ids[nrows + i];
+  uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  uint32_t id_n = i < n ? a.cls_ids[nrows + i] : 0u;  // the next row's list entry, loaded a row ahead (k_emit_k0)
+  uint64_t G_n = i < n ? a.cls_g[nrows + i] : 0ull;
+  for (; i < n; i += nw) {
+    const uint32_t id = id_n;
     const uint32_t plane = id / g.rows, row = id % g.rows;
+    const uint64_t Gb = a.off_g ? G_n - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G_n;
+    const uint64_t L = a.glen[id] & kLenMask;
     uint64_t rr[WPL];
     eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
-    const uint64_t L = a.glen[id] & kLenMask;
-    const uint64_t Gb = gb_abs(a, id, plane);
+    if (i + nw < n) {
+      id_n = a.cls_ids[nrows + i + nw];
+      G_n = a.cls_g[nrows + i + nw];
+    }
     if (L > kCapBits) {  // k_rows_global writes the row
       if (lane == 0) {
         a.gslow[id] = a.row_o[id] + row + 1;
@@ -1891,6 +1924,74 @@ __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
     write_row64(img, L, Gb, a.out_g, a.gfrag + 2 * (uint64_t)id);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Mixed rows (codewords of several k): one wave per row as k_emit_k1, with the general per-word
+// encoder -- each lane's samples before it (n, a wave scan of the popcounts carried across the row's
+// words) and its last 1 (jp) give every codeword's k from the coder state (GolombCoder.cpp:29-34:
+// n = the samples before, A = the zeros before) -- into a 32-bit LDS row image, then write_row.
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_mix(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
+  __shared__ uint32_t s_lut[512];
+  const Geom& g = a.g;
+  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
+  for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+  __syncthreads();  // the only workgroup barrier
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  const uint32_t n = __hip_atomic_load(a.counter + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nw = gridDim.x * 4;
+  uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  uint32_t id_n = i < n ? a.cls_ids[2 * nrows + i] : 0u;  // a row ahead (k_emit_k0)
+  uint64_t G_n = i < n ? a.cls_g[2 * nrows + i] : 0ull;
+  for (; i < n; i += nw) {
+    const uint32_t id = id_n;
+    const uint32_t plane = id / g.rows, row = id % g.rows;
+    const uint64_t Gb = a.off_g ? G_n - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G_n;
+    const uint64_t L = a.glen[id] & kLenMask;
+    const uint32_t O = a.row_o[id];
+    uint64_t rr[WPL];
+    eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
+    if (i + nw < n) {
+      id_n = a.cls_ids[2 * nrows + i + nw];
+      G_n = a.cls_g[2 * nrows + i + nw];
+    }
+    uint4* z = reinterpret_cast<uint4*>(gimg);
+    for (int j = lane_id(); j < kGImg / 4; j += 64) z[j] = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    StepState st{O + row, -1};  // samples before the row: its plane's 1s before it and one EOL per row
+    const uint32_t arow = row * (g.cols + 1);
+    uint32_t loc = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      if (t * 64 >= (int)g.used) break;
+      const uint32_t w = t * 64 + lane_id();
+      const uint64_t x = rr[t];
+      uint32_t nn;
+      int jp;
+      step_prefix(x, w, st, nn, jp);
+      const bool eol = w == g.used - 1;
+      const LaneEnc e = encode_word(x, w, nn, jp, arow, eol, g.cols, ByteTables{s_lut, a.lut});
+      const uint32_t inc = wave_incl_sum_u32(e.len);
+      const uint32_t off = loc + inc - e.len;
+      loc += lane63_u32(inc);
+      if (!e.lng) {
+        place_small(gimg, off, e.head, e.k0);
+        place128(gimg, off + e.k0 + e.z, e.t0, e.t1, e.tlen);
+      } else {
+        LdsSink ls{gimg, 0, 0};
+        emit_word(ls, off, x, w, nn, jp, arow, eol, g.cols);
+        ls.flush();
+      }
+    }
+    if (lane_id() == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    write_row(gimg, L, Gb, -1, a.out_g, a.gfrag + 2 * (uint64_t)id);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
     __builtin_amdgcn_wave_barrier();
   }
@@ -2054,7 +2155,7 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
   return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024 + (size_t)g.nplanes * 8 * 4 + 64 +
-         n * 4 * 2 + 64;  // (cls_ids)
+         n * 4 * 3 + 64 + n * 8 * 3 + 64;  // (cls_ids, cls_g)
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -2088,6 +2189,8 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
     fs.ebase = fs.gbase + g.nplanes;
     fs.efix = fs.ebase + g.nplanes;
     fs.cls_ids = reinterpret_cast<uint32_t*>(fs.efix + g.nplanes);
+    uintptr_t c = reinterpret_cast<uintptr_t>(fs.cls_ids + 3 * n);
+    fs.cls_g = reinterpret_cast<uint64_t*>((c + 7) & ~(uintptr_t)7);
   }
   fs.ns = 1;
   fs.counted = false;
@@ -2129,6 +2232,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   a.esrc = es ? out_e : nullptr;
   a.efix = es ? fs.efix : nullptr;
   a.cls_ids = es && out_g && !fs.eg_src_one ? fs.cls_ids : nullptr;
+  a.cls_g = fs.cls_g;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
 #endif
@@ -2196,7 +2300,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
     const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 32 / nwv);  // 32 waves per CU (16: C4 +6 us; 4: C3 +30 us -- the listed rows are latency-bound)
     hipStream_t rs = s;
-    if (kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
+    const bool classes = es && a.cls_ids;  // (EG source: three class kernels, no k_emit_rest)
+    if (kRestAux && !classes && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
         hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
       rs = fs.aux;
 #define BIC_EMIT1(W, P, DG, DE, ES)                                                                    \
@@ -2215,20 +2320,12 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     } else if (es) {  // Golomb alone, the residual rows from the EG stream: one kernel per row class
 #define BIC_EMITC(W)                                                                                      \
   {                                                                                                    \
-    if (fs.rest_order == 2) {                                                                          \
-      k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
-      if (rs != s) { (void)hipEventRecord(fs.ev_join, rs); (void)hipStreamWaitEvent(s, fs.ev_join, 0); } \
-    } else if (fs.rest_order == 0) {                                                                   \
-      k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
-    }                                                                                                  \
     static const int o0_ = occ_of(reinterpret_cast<const void*>(&k_emit_k0<W>));                      \
     static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1<W>));                      \
+    static const int o2_ = occ_of(reinterpret_cast<const void*>(&k_emit_mix<W>));                     \
     k_emit_k0<W><<<egrid_of(o0_), 256, 0, s>>>(a);                                                     \
     k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                     \
-    if (fs.rest_order == 1) {                                                                          \
-      if (rs != s) { (void)hipEventRecord(fs.ev_fork, s); (void)hipStreamWaitEvent(rs, fs.ev_fork, 0); } \
-      k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
-    }                                                                                                  \
+    k_emit_mix<W><<<egrid_of(o2_), 256, 0, s>>>(a);                                                    \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
 #undef BIC_EMITC

@@ -143,11 +143,12 @@ struct FusedScratch {
   // plane (efix, found by the ONES scan) is cleared after them (bic_fused.hip eg_fix_bit)
   bool eg_src = false;
   uint64_t* efix = nullptr;
-  // EG source: the LEN scan lists the rows whose codewords all have k = 0 (cls_ids[0 .. counter[4]))
-  // and all k = 1 (cls_ids[n ..], counter[5]) for the two class emission kernels (n = rows * planes)
+  // EG source: the LEN scan lists the rows whose codewords all have k = 0 (cls_ids[0 .. counter[4])),
+  // all k = 1 (cls_ids[n ..], counter[5]) and the mixed rows that fit an LDS row image (cls_ids[2n ..],
+  // counter[6]) for the three class emission kernels (n = rows * planes)
   uint32_t* cls_ids = nullptr;
+  uint64_t* cls_g = nullptr;  // beside each listed row its slot-relative Golomb bit offset (as gboff)
   bool eg_src_one = false;  // (A/B: the one emission kernel k_emit_known for every class instead)
-  int rest_order = 0;       // (diagnostic: 1 = k_emit_rest after the class kernels, 2 = before them)
 };
 size_t fused_scratch_bytes(const Geom& g);
 FusedScratch carve_fused_scratch(void* base, const Geom& g);

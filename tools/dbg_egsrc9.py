@@ -1,0 +1,67 @@
+"""diagnostic: one test image (tests/test_gpu_egsrc.py's kinds) through the EG-source modes -- per bad
+Golomb row its class by the oracle's codeword k values, written-or-not (slots pre-filled with 0xaa),
+the first differing bits"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "binary-image-compression_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import pybic  # noqa: E402
+from oracle_lib import Oracle  # noqa: E402
+from test_gpu_egsrc import _img  # noqa: E402
+
+rows, cols, kind = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+o = Oracle()
+img = _img(o, rows * 13 + cols, rows, cols, kind)
+P = o.bitplanes(np.ascontiguousarray(img), 8)
+exp, ris, cls = [], [], []
+for k in range(8):
+    e = o.encode_plane(P[k], cols, 1, 0)
+    exp.append(e)
+    ris.append(list(o.row_index(P[k], cols, 1)[0::2]) + [e[0]])
+    s, eo = o.plane_runs(o.med(P[k], cols), cols)
+    _, _, kk, _ = o.golomb_samples(s)
+    rowid = np.concatenate([[0], np.cumsum(eo)[:-1]])
+    c = []
+    for r in range(rows):
+        u = set(kk[rowid == r].tolist())
+        c.append("k0" if u == {0} else "k1" if u == {1} else "mixed" + str(sorted(u)))
+    cls.append(c)
+ctx = pybic.Context(0)
+ctx.set_encoder("staged")
+g = ctx.torch.from_numpy(np.ascontiguousarray(img)).to(ctx.dev)
+slot = ctx.slot_words(rows, cols, pybic.CODER_GOLOMB)
+og = ctx.empty_i64(8, slot)
+pat = np.unpackbits(np.frombuffer(b"\xaa" * 8, np.uint8))
+for mode, one in ((1, False), (1, False), (2, False), (1, True), (0, False)):
+    ctx.set_eg_source(mode)
+    ctx.set_one_stream(one)
+    og.fill_(-0x5555555555555556)
+    ctx.encode_gray(g, store_planes=False, outs=(og, None))
+    ctx.sync()
+    nbad = 0
+    for k in range(8):
+        eb = exp[k][0]
+        got = np.unpackbits(np.frombuffer(pybic.stream_bytes(og[k], eb), np.uint8))[:eb]
+        ex = np.unpackbits(np.frombuffer(exp[k][1].tobytes(), np.uint8))[:eb]
+        if np.array_equal(got, ex):
+            continue
+        for r in range(rows):
+            a, b = int(ris[k][r]), int(ris[k][r + 1])
+            d = np.nonzero(got[a:b] != ex[a:b])[0]
+            if not len(d):
+                continue
+            nbad += 1
+            if nbad > 12:
+                continue
+            w0 = a + (-a % 64)
+            unwritten = b - w0 >= 64 and np.array_equal(got[w0:w0 + 64], pat)
+            f = int(d[0])
+            print(f"mode {mode} one {one} plane {k} row {r} [{cls[k][r]}]: start {a} (mod64 {a % 64}) len {b - a} "
+                  f"diffs {len(d)} first {f} last {int(d[-1])} {'UNWRITTEN' if unwritten else 'written'} | "
+                  f"exp {''.join(map(str, ex[a + f:a + f + 24]))} got {''.join(map(str, got[a + f:a + f + 24]))}",
+                  flush=True)
+    print(f"mode {mode} one {one}: bad rows {nbad}", flush=True)
