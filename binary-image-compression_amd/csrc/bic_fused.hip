@@ -638,8 +638,10 @@ struct FusedArgs {
   // uniform layout and the residual rows are read back from it (null: residual from planes)
   const uint64_t* esrc;
   uint64_t* efix;
-  uint32_t* cls_ids;  // FusedScratch::cls_ids (EG source: the class emission kernels' row lists)
-  uint64_t* cls_g;    // and each listed row's Golomb offset (gboff's value: one load with the id)
+  uint64_t* cls;  // FusedScratch::cls (EG source: the class emission kernels' row lists, (id, offset)
+                  // pairs; the class kernels store as unsigned long long, a type apart, so the compiler
+                  // keeps these loads on the scalar cache: no wait on the vector memory counter)
+  uint64_t* sink;     // FusedScratch::sink
 #ifdef BIC_STAMPS
   int known;
 #endif
@@ -673,20 +675,28 @@ __device__ __forceinline__ uint64_t eg_src_word(const uint64_t* eplane, const Ge
 }
 // the row's words t * 64 + lane (t < WPL) as resid_row gives them: one load per word, lane l + 1's word
 // through DPP (wave_shl:1), lane 63's from lane 0 of the next word group (the last: one uniform load)
+// (as two halves, so that a wave can issue a row's loads one row ahead: eg_src_load, then
+// eg_src_assemble when the words are needed)
 template <int WPL>
-__device__ __forceinline__ void eg_src_row(const uint64_t* eplane, const Geom& g, uint32_t row, uint64_t (&r)[WPL]) {
+__device__ __forceinline__ void eg_src_load(const uint64_t* eplane, const Geom& g, uint32_t row, uint64_t (&v)[WPL],
+                                            uint64_t& last) {
   const int lane = lane_id();
   const uint64_t b = eg_src_bit0(g, row);
   const uint64_t* p = eplane + (b >> 6);
-  const uint32_t sh = (uint32_t)(b & 63);
-  const uint32_t nw = g.used;  // stream words used: nw (+ 1 when sh != 0)
-  uint64_t v[WPL];
+  const uint32_t nw = g.used;  // stream words used: nw (+ 1 when the row is not word-aligned)
 #pragma unroll
-  for (int t = 0; t < WPL; ++t) {
+  for (int t = 0; t < WPL; ++t) {  // (every lane loads, at a clamped index: eg_src_assemble masks)
     const uint32_t j = t * 64 + lane;
-    v[t] = j < nw ? p[j] : 0;
+    v[t] = p[j < nw ? j : nw - 1];
   }
-  const uint64_t last = sh ? p[nw] : 0;  // (uniform address)
+  last = p[(b & 63) ? nw : nw - 1];  // (uniform address; unused when the row is word-aligned)
+}
+template <int WPL>
+__device__ __forceinline__ void eg_src_assemble(const Geom& g, uint32_t row, const uint64_t (&v)[WPL], uint64_t last,
+                                                uint64_t (&r)[WPL]) {
+  const int lane = lane_id();
+  const uint32_t sh = (uint32_t)(eg_src_bit0(g, row) & 63);
+  const uint32_t nw = g.used;
 #pragma unroll
   for (int t = 0; t < WPL; ++t) {
     const uint32_t j = t * 64 + lane;
@@ -700,9 +710,18 @@ __device__ __forceinline__ void eg_src_row(const uint64_t* eplane, const Geom& g
       else
         nx = last;
     }
+    // (lane j + 1's word is its clamped load when j + 1 >= nw: only its bits past the row are used)
     const uint64_t x = sh ? funnel64(hi, bswap64(nx), 64 - sh) : hi;
     r[t] = j < nw ? ~x & (j == nw - 1 ? g.trail : ~0ull) : 0;
   }
+}
+// the row's words t * 64 + lane (t < WPL) as resid_row gives them: one load per word, lane l + 1's word
+// through DPP (wave_shl:1), lane 63's from lane 0 of the next word group (the last: one uniform load)
+template <int WPL>
+__device__ __forceinline__ void eg_src_row(const uint64_t* eplane, const Geom& g, uint32_t row, uint64_t (&r)[WPL]) {
+  uint64_t v[WPL], last;
+  eg_src_load<WPL>(eplane, g, row, v, last);
+  eg_src_assemble<WPL>(g, row, v, last, r);
 }
 
 // Global-memory emission for a row whose Golomb image does not fit the LDS window: codeword
@@ -1505,45 +1524,36 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
     }
   } else {
     const uint64_t cap = a.slot_g * 64;
-    if (a.cls_ids) {  // EG source: this chunk's k = 0 / k = 1 rows appended to the class lists
+    if (a.cls) {  // EG source: this chunk's k = 0 / k = 1 rows appended to the class lists
       static_assert(kScanPer == 1, "one row per thread");
       const uint32_t r = r0;
       const uint64_t f = r < g.rows ? a.glen[base + r] : 0;
       const bool ok = pre + v[0] <= cap && v[0] != 0;  // (an overflowing row is written by nobody)
       const uint32_t c0 = ok && (f & kK0Row) ? 1u : 0u, c1 = ok && (f & kK1Row) ? 1u : 0u;
-      // mixed rows: k_emit_mix's list when the LDS image holds them, else k_rows_global's
-      // (k_emit_k1 lists its own long rows)
-      constexpr uint32_t kCapBitsMix = (kGImg - kPad) * 32;
-      const bool mixed = ok && !(f & (kK0Row | kK1Row));
-      if (mixed && v[0] > kCapBitsMix) {
+      // a mixed row too long for k_emit_rest's LDS image goes to k_rows_global (k_emit_k1 lists its own)
+      constexpr uint32_t kCapBitsRest = (kGImg - kPad) * 32;
+      if (ok && !(f & (kK0Row | kK1Row)) && v[0] > kCapBitsRest) {
         a.gslow[base + r] = a.row_o[base + r] + r + 1;
         a.slow_ids[atomicAdd(a.slow_n, 1u)] = base + r;
       }
-      const uint32_t c2 = mixed && v[0] <= kCapBitsMix ? 1u : 0u;
-      uint32_t t0, t1, t2;
+      uint32_t t0, t1;
       const uint32_t x0 = block_excl_scan<uint32_t>(c0, reinterpret_cast<uint32_t*>(tmp), t0);
       const uint32_t x1 = block_excl_scan<uint32_t>(c1, reinterpret_cast<uint32_t*>(tmp), t1);
-      const uint32_t x2 = block_excl_scan<uint32_t>(c2, reinterpret_cast<uint32_t*>(tmp), t2);
-      __shared__ uint32_t lb[3];
+      __shared__ uint32_t lb[2];
       if (threadIdx.x == 0) {
         lb[0] = t0 ? atomicAdd(a.counter + 4, t0) : 0u;
         lb[1] = t1 ? atomicAdd(a.counter + 5, t1) : 0u;
-        lb[2] = t2 ? atomicAdd(a.counter + 6, t2) : 0u;
       }
       __syncthreads();
       const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
       const uint64_t G = (uint64_t)plane * cap + pre;  // (gboff's value, written below)
       if (c0) {
-        a.cls_ids[lb[0] + x0] = (uint32_t)(base + r);
-        a.cls_g[lb[0] + x0] = G;
+        a.cls[2 * (lb[0] + x0)] = (base + r) | (v[0] << 32);  // id, Golomb length
+        a.cls[2 * (lb[0] + x0) + 1] = G;
       }
       if (c1) {
-        a.cls_ids[nrows + lb[1] + x1] = (uint32_t)(base + r);
-        a.cls_g[nrows + lb[1] + x1] = G;
-      }
-      if (c2) {
-        a.cls_ids[2 * nrows + lb[2] + x2] = (uint32_t)(base + r);
-        a.cls_g[2 * nrows + lb[2] + x2] = G;
+        a.cls[2 * (nrows + lb[1] + x1)] = (base + r) | (v[0] << 32);
+        a.cls[2 * (nrows + lb[1] + x1) + 1] = G;
       }
     }
 #pragma unroll
@@ -1789,14 +1799,31 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
 // ---- EG source: one light emission kernel per row class ------------------------------------------
 // With the residual rows read back from the EG stream (FusedArgs::esrc) the Golomb emission is split
 // by the class the prefix kernels proved for the row (the LEN scan's lists): rows whose codewords
-// all have k = 0 are shifted copies of the EG stream, inverted (k_emit_k0, no LDS, few registers:
-// many waves in flight per SIMD), rows whose codewords all have k = 1 go through the byte tables and
-// an LDS row image (k_emit_k1); mixed rows stay k_emit_rest's. Persistent waves, one row at a time.
+// all have k = 0 are shifted copies of the EG stream, inverted (k_emit_k0, no LDS), rows whose
+// codewords all have k = 1 go through the byte tables and an LDS row image (k_emit_k1); mixed rows
+// stay k_emit_rest's. Persistent waves, one row at a time, in the list order i, i + nw, ...
 //
+// Both kernels keep the memory system busy the same way: the next row's source words are loaded
+// before the current row's output is stored, into the other of two word buffers (ping-pong, no
+// register copies). gfx9's vmcnt counts stores with loads: a wave that loaded after storing would
+// wait for its stores' acknowledgements every row. With the loads first, every load and store issued
+// unconditionally (clamped indices, idle lanes storing to a.sink), the list entries read through the
+// scalar cache (the kernels' stores are typed unsigned long long, apart from the entries' u64, and
+// they hold no fence or workgroup barrier, so the compiler proves the entries unclobbered), the
+// compiler waits for the loads alone.
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+}
+
 // k = 0: the row's Golomb bits are R then the end-of-row '1' (GolombCoder.cpp:13-34 with k = 0: each
 // sample's zeros and its '1'), i.e. the EG row ~R '1' (eg.cpp:20-37) with its first cols bits inverted.
 // Output word t of the row (at bit Gb) holds row bits [64 t - g, 64 t - g + 64), g = Gb % 64: the
 // stream bits from Bsrc + 64 t - g (Bsrc: the row in the EG slot), one funnel shift per word.
+#ifndef BIC_K0_BATCH
+#define BIC_K0_BATCH 4
+#endif
+constexpr int kK0Batch = BIC_K0_BATCH;
 template <int WPL>
 __global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
   const Geom& g = a.g;
@@ -1804,63 +1831,120 @@ __global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
   const uint32_t n = __hip_atomic_load(a.counter + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nw = gridDim.x * 4;
   const uint64_t L = (uint64_t)g.cols + 1;
-  uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-  // the list entry (row id, Golomb offset) of the wave's next row is loaded while this one is copied:
-  // a row costs one memory round trip (its words), not three (entry, offset, words)
-  uint32_t id_n = i < n ? a.cls_ids[i] : 0u;
-  uint64_t G_n = i < n ? a.cls_g[i] : 0ull;
-  for (; i < n; i += nw) {
-    const uint32_t id = id_n;
-    const uint32_t plane = id / g.rows, row = id % g.rows;
-    const uint64_t G = a.off_g ? G_n - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G_n;
-    const uint32_t gs = (uint32_t)(G & 63);
-    const uint64_t w0 = G >> 6, nwo = ((G + L - 1) >> 6) - w0 + 1;  // output words (<= used + 2)
-    // stream bit of output word t's first bit: src = Bsrc - gs + 64 t (Bsrc - gs >= -63)
-    const int64_t s0 = (int64_t)((uint64_t)plane * a.slot_e * 64 + eg_src_bit0(g, row)) - (int64_t)gs;
-    const int64_t si = s0 >> 6;  // (floor: s0 may be negative for row 0 of plane 0)
-    const uint32_t d = (uint32_t)(s0 & 63);
-    const uint64_t* S = a.esrc;
-    // the words holding the row's bits through its end-of-row '1' (none past it: the slot may end there)
-    const int64_t jend = (int64_t)(((uint64_t)plane * a.slot_e * 64 + eg_src_bit0(g, row) + g.cols) >> 6);
-    uint64_t v[WPL + 1];
+  const uint64_t* S = a.esrc;
+  // (the wave index through readfirstlane: the compiler then knows i, and every branch on it, is uniform)
+  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (i0 >= n) return;
+  const uint32_t R = (n - i0 + nw - 1) / nw;  // the wave's rows
+  struct Row {
+    uint32_t id;
+    uint64_t G;
+    int64_t si;
+    uint32_t d;
+  };
+  // row k of the wave (list entry i0 + k nw): where its output and its source bits are
+  auto place = [&](uint32_t k) {
+    const uint64_t e = i0 + (uint64_t)k * nw;
+    Row r;
+    r.id = (uint32_t)a.cls[2 * e];
+    const uint32_t plane = r.id / g.rows, row = r.id % g.rows;
+    const uint64_t Gs = a.cls[2 * e + 1];
+    r.G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
+    // stream bit of output word t's first bit: Bsrc - G % 64 + 64 t (>= -63: floor below)
+    const int64_t s0 = (int64_t)((uint64_t)plane * a.slot_e * 64 + eg_src_bit0(g, row)) - (int64_t)(r.G & 63);
+    r.si = s0 >> 6;
+    r.d = (uint32_t)(s0 & 63);
+    return r;
+  };
+  // the row's source words (those holding its bits through its end-of-row '1'; the slot may end
+  // there): every lane loads, at a clamped index, the words outside masked where used
+  auto load = [&](const Row& r, uint64_t (&v)[WPL + 1]) {
+    const int64_t jend = r.si + (int64_t)((r.d + (r.G & 63) + g.cols) >> 6);
 #pragma unroll
     for (int k = 0; k <= WPL; ++k) {
-      const int64_t j = si + 64 * k + lane;
-      v[k] = (j >= 0 && j <= jend) ? S[j] : 0ull;
+      const int64_t j = r.si + 64 * k + lane;
+      const int64_t jc = j > jend ? jend : j;
+      v[k] = S[jc < 0 ? 0 : jc];
     }
-    if (i + nw < n) {
-      id_n = a.cls_ids[i + nw];
-      G_n = a.cls_g[i + nw];
-    }
+  };
+  auto emit = [&](const Row& cur, uint64_t (&v)[WPL + 1]) {
+    const uint32_t gs = (uint32_t)(cur.G & 63);
+    const uint64_t w0 = cur.G >> 6, nwo = ((cur.G + L - 1) >> 6) - w0 + 1;  // output words (<= used + 2)
     const uint64_t eolw = (uint64_t)(g.cols + gs) >> 6, eolb = BIC_MSB >> ((g.cols + gs) & 63);
+    const int64_t jend = cur.si + (int64_t)((cur.d + gs + g.cols) >> 6);
+#pragma unroll
+    for (int k = 0; k <= WPL; ++k) {
+      const int64_t j = cur.si + 64 * k + lane;
+      v[k] &= 0ull - (uint64_t)((j >= 0) & (j <= jend));
+    }
 #pragma unroll
     for (int k = 0; k <= WPL; ++k) {
       const uint32_t t = 64 * k + lane;
-      if (64 * k >= (int)nwo) break;
       uint64_t nx = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v[k] >> 32), 0x130, 0xf, 0xf, true) << 32) |
                     (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v[k], 0x130, 0xf, 0xf, true);
       if (k < WPL) {
-        const uint64_t n0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v[k + 1 <= WPL ? k + 1 : k] >> 32), 0) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v[k + 1 <= WPL ? k + 1 : k], 0);
+        const uint64_t n0 = rl64(v[k + 1 <= WPL ? k + 1 : k], 0);
         if (lane == 63) nx = n0;
       }
       const uint64_t hi = bswap64(v[k]);
-      uint64_t x = ~(d ? funnel64(hi, bswap64(nx), 64 - d) : hi);
+      uint64_t x = ~(cur.d ? funnel64(hi, bswap64(nx), 64 - cur.d) : hi);
       // row bits outside [0, cols) are not the row's: before it (word 0's first gs bits) and from the
       // end-of-row '1' on
       if (t == 0) x &= ~0ull >> gs;
       if (t >= eolw) x = t == eolw ? (x & ~((eolb << 1) - 1)) | eolb : 0ull;
-      if (t < nwo) {
-        const bool whole = (t != 0 || gs == 0) && (t != nwo - 1 || ((G + L) & 63) == 0);
-        if (whole) a.out_g[w0 + t] = bswap64(x);
-        else a.gfrag[2 * (uint64_t)id + (t == 0 ? 0 : 1)] = x;
-      }
+      const bool in = t < nwo;
+      const bool whole = in && (t != 0 || gs == 0) && (t != nwo - 1 || ((cur.G + L) & 63) == 0);
+      uint64_t* dst = whole ? a.out_g + w0 + t : (in ? a.gfrag + 2 * (uint64_t)cur.id + (t == 0 ? 0 : 1) : a.sink + lane);
+      // (unsigned long long: a type apart from the u64 loads, so no load is taken to depend on it)
+      *reinterpret_cast<unsigned long long*>(dst) = whole ? bswap64(x) : x;
     }
+  };
+  // rows in batches of kK0Batch: every row's loads issued before the first row's stores, so a wave
+  // waits for its previous stores once per batch
+  for (uint32_t k = 0; k < R; k += kK0Batch) {
+    Row r[kK0Batch];
+    uint64_t v[kK0Batch][WPL + 1];
+#pragma unroll
+    for (int u = 0; u < kK0Batch; ++u) {
+      r[u] = place(k + u < R ? k + u : k);
+      load(r[u], v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kK0Batch; ++u)
+      if (k + u < R) emit(r[u], v[u]);
+  }
+}
+
+// write_row64 with a fixed number of store instructions (MAXT per lane, the idle lanes' to a.sink)
+// and its stores typed unsigned long long (k_emit_k0)
+template <int MAXT>
+__device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t L, uint64_t G, uint64_t* out,
+                                                  uint64_t* frag, uint64_t* sink) {
+  const int lane = lane_id();
+  const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6;
+  const uint32_t nw = (uint32_t)(w1 - w0 + 1), g = (uint32_t)(G & 63);
+  const bool head_whole = g == 0, tail_whole = ((G + L) & 63) == 0;
+#pragma unroll
+  for (int it = 0; it < MAXT; ++it) {
+    const uint32_t t = it * 64 + lane;
+    const bool in = t < nw;
+    const uint32_t tc = in ? t : 0u;
+    // (the image read as unsigned long long, the type its atomics write: ordered after them)
+    const unsigned long long* im = reinterpret_cast<const unsigned long long*>(img);
+    const uint64_t cur = im[tc], prev = tc ? im[tc - 1] : 0ull;
+    const uint64_t v = funnel64(prev, cur, g);
+    const bool whole = in && (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
+    uint64_t* dst = whole ? out + w0 + t : (in ? frag + (t == 0 ? 0 : 1) : sink + lane);
+    *reinterpret_cast<unsigned long long*>(dst) = whole ? bswap64(v) : v;
   }
 }
 
 // k = 1 rows: emit_known_row's byte-table path (encode_word_k1b into a 64-bit LDS row image, then
-// write_row64); rows whose image exceeds the window are listed for k_rows_global.
+// write_row64_fixed); rows whose image exceeds the window are listed for k_rows_global.
+#ifndef BIC_K1_BATCH
+#define BIC_K1_BATCH 2
+#endif
+constexpr int kK1Batch = BIC_K1_BATCH;
 template <int WPL>
 __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
@@ -1868,35 +1952,45 @@ __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
   const Geom& g = a.g;
   const int lane = lane_id();
   uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
-  for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
-  __syncthreads();  // the only workgroup barrier
+  // every wave writes the whole table itself (the same values as the others): its own reads then
+  // follow its own writes, and the kernel needs no workgroup barrier
+  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t n = __hip_atomic_load(a.counter + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nw = gridDim.x * 4;
-  uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-  uint32_t id_n = i < n ? a.cls_ids[nrows + i] : 0u;  // the next row's list entry, loaded a row ahead (k_emit_k0)
-  uint64_t G_n = i < n ? a.cls_g[nrows + i] : 0ull;
-  for (; i < n; i += nw) {
-    const uint32_t id = id_n;
-    const uint32_t plane = id / g.rows, row = id % g.rows;
-    const uint64_t Gb = a.off_g ? G_n - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G_n;
-    const uint64_t L = a.glen[id] & kLenMask;
-    uint64_t rr[WPL];
-    eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
-    if (i + nw < n) {
-      id_n = a.cls_ids[nrows + i + nw];
-      G_n = a.cls_g[nrows + i + nw];
-    }
-    if (L > kCapBits) {  // k_rows_global writes the row
+  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (i0 >= n) return;
+  const uint32_t R = (n - i0 + nw - 1) / nw;
+  struct Row {
+    uint32_t id, plane, row;
+    uint64_t G, L;
+  };
+  auto place = [&](uint32_t k) {
+    const uint64_t e = nrows + i0 + (uint64_t)k * nw;
+    Row r;
+    const uint64_t e0 = a.cls[2 * e];
+    r.id = (uint32_t)e0;
+    r.L = e0 >> 32;
+    r.plane = r.id / g.rows;
+    r.row = r.id % g.rows;
+    const uint64_t Gs = a.cls[2 * e + 1];
+    r.G = a.off_g ? Gs - (uint64_t)r.plane * a.slot_g * 64 + a.gbase[r.plane] * 64 : Gs;
+    return r;
+  };
+  auto emit = [&](const Row& cur, const uint64_t (&v)[WPL], uint64_t last) {
+    if (cur.L > kCapBits) {  // k_rows_global writes the row
       if (lane == 0) {
-        a.gslow[id] = a.row_o[id] + row + 1;
-        a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
+        *reinterpret_cast<unsigned long long*>(a.gslow + cur.id) = a.row_o[cur.id] + cur.row + 1;
+        *reinterpret_cast<unsigned long long*>(a.slow_ids + atomicAdd(a.slow_n, 1u)) = cur.id;
       }
-      continue;
+      return;
     }
-    uint4* z = reinterpret_cast<uint4*>(gimg);
-    for (int j = lane; j < kGImg / 4; j += 64) z[j] = make_uint4(0, 0, 0, 0);
+    // zeroed as unsigned long long, the type of the image's atomics (so ordered before them)
+    unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
+    for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
+    uint64_t rr[WPL];
+    eg_src_assemble<WPL>(g, cur.row, v, last, rr);
     uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
     int jpc = -1;
     uint32_t loc = 0;
@@ -1920,80 +2014,27 @@ __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
         ls.flush();
       }
     }
-    if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    write_row64(img, L, Gb, a.out_g, a.gfrag + 2 * (uint64_t)id);
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// Mixed rows (codewords of several k): one wave per row as k_emit_k1, with the general per-word
-// encoder -- each lane's samples before it (n, a wave scan of the popcounts carried across the row's
-// words) and its last 1 (jp) give every codeword's k from the coder state (GolombCoder.cpp:29-34:
-// n = the samples before, A = the zeros before) -- into a 32-bit LDS row image, then write_row.
-template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_mix(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
-  __shared__ uint32_t s_lut[512];
-  const Geom& g = a.g;
-  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
-  for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
-  __syncthreads();  // the only workgroup barrier
-  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  const uint32_t n = __hip_atomic_load(a.counter + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nw = gridDim.x * 4;
-  uint32_t i = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-  uint32_t id_n = i < n ? a.cls_ids[2 * nrows + i] : 0u;  // a row ahead (k_emit_k0)
-  uint64_t G_n = i < n ? a.cls_g[2 * nrows + i] : 0ull;
-  for (; i < n; i += nw) {
-    const uint32_t id = id_n;
-    const uint32_t plane = id / g.rows, row = id % g.rows;
-    const uint64_t Gb = a.off_g ? G_n - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : G_n;
-    const uint64_t L = a.glen[id] & kLenMask;
-    const uint32_t O = a.row_o[id];
-    uint64_t rr[WPL];
-    eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
-    if (i + nw < n) {
-      id_n = a.cls_ids[2 * nrows + i + nw];
-      G_n = a.cls_g[2 * nrows + i + nw];
-    }
-    uint4* z = reinterpret_cast<uint4*>(gimg);
-    for (int j = lane_id(); j < kGImg / 4; j += 64) z[j] = make_uint4(0, 0, 0, 0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    StepState st{O + row, -1};  // samples before the row: its plane's 1s before it and one EOL per row
-    const uint32_t arow = row * (g.cols + 1);
-    uint32_t loc = 0;
+    if (lane == 0 && loc != cur.L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+    // (no fence: one wave's LDS operations run in order, and the image's zeroing, atomics and reads
+    // share one type, so the compiler keeps their order)
+    // (rows up to kCapBits: at most (kCapBits + 63) / 64 + 1 output words)
+    write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, cur.L, cur.G, a.out_g, a.gfrag + 2 * (uint64_t)cur.id,
+                                                     a.sink);
+  };
+  auto load = [&](const Row& r, uint64_t (&v)[WPL], uint64_t& last) {
+    eg_src_load<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v, last);
+  };
+  for (uint32_t k = 0; k < R; k += kK1Batch) {  // (batches as k_emit_k0)
+    Row r[kK1Batch];
+    uint64_t v[kK1Batch][WPL], l[kK1Batch];
 #pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      if (t * 64 >= (int)g.used) break;
-      const uint32_t w = t * 64 + lane_id();
-      const uint64_t x = rr[t];
-      uint32_t nn;
-      int jp;
-      step_prefix(x, w, st, nn, jp);
-      const bool eol = w == g.used - 1;
-      const LaneEnc e = encode_word(x, w, nn, jp, arow, eol, g.cols, ByteTables{s_lut, a.lut});
-      const uint32_t inc = wave_incl_sum_u32(e.len);
-      const uint32_t off = loc + inc - e.len;
-      loc += lane63_u32(inc);
-      if (!e.lng) {
-        place_small(gimg, off, e.head, e.k0);
-        place128(gimg, off + e.k0 + e.z, e.t0, e.t1, e.tlen);
-      } else {
-        LdsSink ls{gimg, 0, 0};
-        emit_word(ls, off, x, w, nn, jp, arow, eol, g.cols);
-        ls.flush();
-      }
+    for (int u = 0; u < kK1Batch; ++u) {
+      r[u] = place(k + u < R ? k + u : k);
+      load(r[u], v[u], l[u]);
     }
-    if (lane_id() == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    write_row(gimg, L, Gb, -1, a.out_g, a.gfrag + 2 * (uint64_t)id);
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
-    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < kK1Batch; ++u)
+      if (k + u < R) emit(r[u], v[u], l[u]);
   }
 }
 
@@ -2155,7 +2196,7 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
   return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024 + (size_t)g.nplanes * 8 * 4 + 64 +
-         n * 4 * 3 + 64 + n * 8 * 3 + 64;  // (cls_ids, cls_g)
+         n * 16 * 2 + 64 + 512;  // (cls, sink)
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -2188,9 +2229,8 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
     fs.gbase = fs.pones + g.nplanes;
     fs.ebase = fs.gbase + g.nplanes;
     fs.efix = fs.ebase + g.nplanes;
-    fs.cls_ids = reinterpret_cast<uint32_t*>(fs.efix + g.nplanes);
-    uintptr_t c = reinterpret_cast<uintptr_t>(fs.cls_ids + 3 * n);
-    fs.cls_g = reinterpret_cast<uint64_t*>((c + 7) & ~(uintptr_t)7);
+    fs.cls = fs.efix + g.nplanes;
+    fs.sink = fs.cls + 4 * n;
   }
   fs.ns = 1;
   fs.counted = false;
@@ -2231,8 +2271,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   const bool es = mode == kEncStaged && fs.eg_src && out_e && !a.off_e && !predict;
   a.esrc = es ? out_e : nullptr;
   a.efix = es ? fs.efix : nullptr;
-  a.cls_ids = es && out_g && !fs.eg_src_one ? fs.cls_ids : nullptr;
-  a.cls_g = fs.cls_g;
+  a.cls = es && out_g && !fs.eg_src_one ? fs.cls : nullptr;
+  a.sink = fs.sink;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
 #endif
@@ -2300,8 +2340,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
     const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 32 / nwv);  // 32 waves per CU (16: C4 +6 us; 4: C3 +30 us -- the listed rows are latency-bound)
     hipStream_t rs = s;
-    const bool classes = es && a.cls_ids;  // (EG source: three class kernels, no k_emit_rest)
-    if (kRestAux && !classes && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
+    if (kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
         hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
       rs = fs.aux;
 #define BIC_EMIT1(W, P, DG, DE, ES)                                                                    \
@@ -2314,18 +2353,17 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   if (dg && de) BIC_EMIT1(W, P, true, true, false) else if (dg) BIC_EMIT1(W, P, true, false, false) else BIC_EMIT1(W, P, false, true, false)
     if (predict) {
       if (wpl == 1) { BIC_EMIT(1, true); } else if (wpl == 2) { BIC_EMIT(2, true); } else { BIC_EMIT(4, true); }
-    } else if (es && !a.cls_ids) {  // Golomb alone, the residual rows from the EG stream, one kernel
+    } else if (es && !a.cls) {  // Golomb alone, the residual rows from the EG stream, one kernel
       if (wpl == 1) { BIC_EMIT1(1, false, true, false, true); } else if (wpl == 2) { BIC_EMIT1(2, false, true, false, true); }
       else { BIC_EMIT1(4, false, true, false, true); }
     } else if (es) {  // Golomb alone, the residual rows from the EG stream: one kernel per row class
 #define BIC_EMITC(W)                                                                                      \
   {                                                                                                    \
+    k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                    \
     static const int o0_ = occ_of(reinterpret_cast<const void*>(&k_emit_k0<W>));                      \
     static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1<W>));                      \
-    static const int o2_ = occ_of(reinterpret_cast<const void*>(&k_emit_mix<W>));                     \
     k_emit_k0<W><<<egrid_of(o0_), 256, 0, s>>>(a);                                                     \
     k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                     \
-    k_emit_mix<W><<<egrid_of(o2_), 256, 0, s>>>(a);                                                    \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
 #undef BIC_EMITC

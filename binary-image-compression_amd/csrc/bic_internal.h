@@ -143,11 +143,13 @@ struct FusedScratch {
   // plane (efix, found by the ONES scan) is cleared after them (bic_fused.hip eg_fix_bit)
   bool eg_src = false;
   uint64_t* efix = nullptr;
-  // EG source: the LEN scan lists the rows whose codewords all have k = 0 (cls_ids[0 .. counter[4])),
-  // all k = 1 (cls_ids[n ..], counter[5]) and the mixed rows that fit an LDS row image (cls_ids[2n ..],
-  // counter[6]) for the three class emission kernels (n = rows * planes)
-  uint32_t* cls_ids = nullptr;
-  uint64_t* cls_g = nullptr;  // beside each listed row its slot-relative Golomb bit offset (as gboff)
+  // EG source: the LEN scan lists the rows whose codewords all have k = 0 (entries [0 .. counter[4]))
+  // and all k = 1 (entries [n ..], counter[5]) for the two class emission kernels (n = rows * planes),
+  // each entry two u64 words: the row id | its Golomb length << 32, then its slot-relative Golomb bit
+  // offset (gboff's value);
+  // the mixed rows stay k_emit_rest's
+  uint64_t* cls = nullptr;
+  uint64_t* sink = nullptr;   // 64 words the class kernels' idle lanes store to (a fixed store count)
   bool eg_src_one = false;  // (A/B: the one emission kernel k_emit_known for every class instead)
 };
 size_t fused_scratch_bytes(const Geom& g);

@@ -40,8 +40,19 @@ for mode, one in ((1, False), (1, False), (2, False), (1, True), (0, False)):
     ctx.set_eg_source(mode)
     ctx.set_one_stream(one)
     og.fill_(-0x5555555555555556)
-    ctx.encode_gray(g, store_planes=False, outs=(og, None))
+    _, _, (oe, be) = ctx.encode_gray(g, store_planes=False, outs=(og, None))
     ctx.sync()
+    for k in range(8):
+        eb, est, _ = o.encode_plane(P[k], cols, 1, 1)
+        gotb = np.frombuffer(pybic.stream_bytes(oe[k], eb), np.uint8)
+        if gotb.tobytes() != est.tobytes():
+            ge = np.unpackbits(gotb)[:eb]
+            xe = np.unpackbits(np.frombuffer(est.tobytes(), np.uint8))[:eb]
+            d = np.nonzero(ge != xe)[0]
+            f = int(d[0]) if len(d) else -1
+            print(f"mode {mode} one {one} plane {k} EG: diffs {len(d)} first bit {f} row {f // (cols + 1)} col "
+                  f"{f % (cols + 1) - 1} | exp {''.join(map(str, xe[f:f + 24]))} got {''.join(map(str, ge[f:f + 24]))}",
+                  flush=True)
     nbad = 0
     for k in range(8):
         eb = exp[k][0]
