@@ -724,6 +724,34 @@ __device__ __forceinline__ void eg_src_row(const uint64_t* eplane, const Geom& g
   eg_src_assemble<WPL>(g, row, v, last, r);
 }
 
+// The row's words with lane l holding words l WPL .. l WPL + WPL - 1 (consecutive: one prefix per
+// lane over its own words, one wave scan per row instead of one per word group): WPL + 1 loads
+// per lane, the last one lane l + 1's first (clamped: masked in the assembly)
+template <int WPL>
+__device__ __forceinline__ void eg_src_load_lc(const uint64_t* eplane, const Geom& g, uint32_t row,
+                                               uint64_t (&v)[WPL + 1]) {
+  const uint64_t b = eg_src_bit0(g, row);
+  const uint64_t* p = eplane + (b >> 6);
+  const uint32_t jmax = (b & 63) ? g.used : g.used - 1;
+#pragma unroll
+  for (int t = 0; t <= WPL; ++t) {
+    const uint32_t j = (uint32_t)lane_id() * WPL + t;
+    v[t] = p[j < jmax ? j : jmax];
+  }
+}
+template <int WPL>
+__device__ __forceinline__ void eg_src_assemble_lc(const Geom& g, uint32_t row, const uint64_t (&v)[WPL + 1],
+                                                   uint64_t (&r)[WPL]) {
+  const uint32_t sh = (uint32_t)(eg_src_bit0(g, row) & 63);
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = (uint32_t)lane_id() * WPL + t;
+    const uint64_t hi = bswap64(v[t]);
+    const uint64_t x = sh ? funnel64(hi, bswap64(v[t + 1]), 64 - sh) : hi;
+    r[t] = w < g.used ? ~x & (w == g.used - 1 ? g.trail : ~0ull) : 0;
+  }
+}
+
 // Global-memory emission for a row whose Golomb image does not fit the LDS window: codeword
 // bits landing in the row's first/last output word are kept for the fragment table, the rest
 // is OR'd into words this wave zeroed first.
@@ -1811,6 +1839,14 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
 // scalar cache (the kernels' stores are typed unsigned long long, apart from the entries' u64, and
 // they hold no fence or workgroup barrier, so the compiler proves the entries unclobbered), the
 // compiler waits for the loads alone.
+#ifndef BIC_CLASS_NT
+#define BIC_CLASS_NT 0
+#endif
+// the class kernels' output stores (typed unsigned long long; BIC_CLASS_NT: non-temporal)
+__device__ __forceinline__ void class_store(uint64_t* dst, uint64_t v) {
+  if constexpr (BIC_CLASS_NT) __builtin_nontemporal_store((unsigned long long)v, reinterpret_cast<unsigned long long*>(dst));
+  else *reinterpret_cast<unsigned long long*>(dst) = v;
+}
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
@@ -1824,16 +1860,14 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
 #define BIC_K0_BATCH 4
 #endif
 constexpr int kK0Batch = BIC_K0_BATCH;
+// the k = 0 list's entries i0, i0 + nw, ... (one wave; i0 and nw wave-uniform)
 template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
+__device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_t nw) {
   const Geom& g = a.g;
   const int lane = lane_id();
   const uint32_t n = __hip_atomic_load(a.counter + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nw = gridDim.x * 4;
   const uint64_t L = (uint64_t)g.cols + 1;
   const uint64_t* S = a.esrc;
-  // (the wave index through readfirstlane: the compiler then knows i, and every branch on it, is uniform)
-  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (i0 >= n) return;
   const uint32_t R = (n - i0 + nw - 1) / nw;  // the wave's rows
   struct Row {
@@ -1896,7 +1930,7 @@ __global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
       const bool whole = in && (t != 0 || gs == 0) && (t != nwo - 1 || ((cur.G + L) & 63) == 0);
       uint64_t* dst = whole ? a.out_g + w0 + t : (in ? a.gfrag + 2 * (uint64_t)cur.id + (t == 0 ? 0 : 1) : a.sink + lane);
       // (unsigned long long: a type apart from the u64 loads, so no load is taken to depend on it)
-      *reinterpret_cast<unsigned long long*>(dst) = whole ? bswap64(x) : x;
+      class_store(dst, whole ? bswap64(x) : x);
     }
   };
   // rows in batches of kK0Batch: every row's loads issued before the first row's stores, so a wave
@@ -1935,31 +1969,28 @@ __device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t 
     const uint64_t v = funnel64(prev, cur, g);
     const bool whole = in && (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
     uint64_t* dst = whole ? out + w0 + t : (in ? frag + (t == 0 ? 0 : 1) : sink + lane);
-    *reinterpret_cast<unsigned long long*>(dst) = whole ? bswap64(v) : v;
+    class_store(dst, whole ? bswap64(v) : v);
   }
 }
 
 // k = 1 rows: emit_known_row's byte-table path (encode_word_k1b into a 64-bit LDS row image, then
 // write_row64_fixed); rows whose image exceeds the window are listed for k_rows_global.
 #ifndef BIC_K1_BATCH
-#define BIC_K1_BATCH 2
+#define BIC_K1_BATCH 3
+#endif
+#ifndef BIC_K1_LC
+#define BIC_K1_LC 1  // lane l holds the row's words l WPL .. (one wave scan per row, not per word group)
 #endif
 constexpr int kK1Batch = BIC_K1_BATCH;
+// the k = 1 list's entries i0, i0 + nw, ... (one wave, with its LDS row image and the byte table)
 template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
-  __shared__ uint32_t s_lut[512];
+__device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_t nw, uint32_t* gimg,
+                                        const uint32_t* s_lut) {
   const Geom& g = a.g;
   const int lane = lane_id();
-  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
-  // every wave writes the whole table itself (the same values as the others): its own reads then
-  // follow its own writes, and the kernel needs no workgroup barrier
-  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   const uint32_t n = __hip_atomic_load(a.counter + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nw = gridDim.x * 4;
-  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (i0 >= n) return;
   const uint32_t R = (n - i0 + nw - 1) / nw;
   struct Row {
@@ -1978,6 +2009,65 @@ __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
     r.G = a.off_g ? Gs - (uint64_t)r.plane * a.slot_g * 64 + a.gbase[r.plane] * 64 : Gs;
     return r;
   };
+#if BIC_K1_LC
+  auto emit = [&](const Row& cur, const uint64_t (&v)[WPL + 1], uint64_t) {
+    if (cur.L > kCapBits) {  // k_rows_global writes the row
+      if (lane == 0) {
+        *reinterpret_cast<unsigned long long*>(a.gslow + cur.id) = a.row_o[cur.id] + cur.row + 1;
+        *reinterpret_cast<unsigned long long*>(a.slow_ids + atomicAdd(a.slow_n, 1u)) = cur.id;
+      }
+      return;
+    }
+    unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
+    for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
+    uint64_t rr[WPL];
+    eg_src_assemble_lc<WPL>(g, cur.row, v, rr);
+    uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
+    // the lane's words l WPL + t: their last 1s, the wave's exclusive max of the lanes' last 1
+    int lastc[WPL], mxl = -1;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)lane * WPL + t;
+      lastc[t] = rr[t] ? (int)(w * 64 + 63 - __builtin_ctzll(rr[t])) : -1;
+      mxl = max(mxl, lastc[t]);
+    }
+    int jp = dpp_or<0x138>(-1, wave_incl_max(mxl));  // lane 0: -1
+    LaneEnc e[WPL];
+    int jps[WPL];
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)lane * WPL + t;
+      jps[t] = jp;
+      e[t] = encode_word_k1b(rr[t], w, jp, w == g.used - 1, g.cols, s_lut);
+      lsum += e[t].len;
+      jp = max(jp, lastc[t]);
+    }
+    const uint32_t inc = wave_incl_sum_u32(lsum);
+    uint32_t off = inc - lsum;
+    const uint32_t loc = lane63_u32(inc);
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)lane * WPL + t;
+      if (!e[t].lng) {
+        if (e[t].head) lds_or64(img, off >> 6, BIC_MSB >> (off & 63));
+        place128_64(img, off + 1 + e[t].z, e[t].t0, e[t].t1, e[t].tlen);
+      } else {
+        LdsSink64 ls{img, 0, 0};
+        emit_word_k1(ls, off, rr[t], w, jps[t], w == g.used - 1, g.cols);
+        ls.flush();
+      }
+      off += e[t].len;
+    }
+    if (lane == 0 && loc != cur.L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
+    write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, cur.L, cur.G, a.out_g, a.gfrag + 2 * (uint64_t)cur.id,
+                                                     a.sink);
+  };
+  auto load = [&](const Row& r, uint64_t (&v)[WPL + 1], uint64_t&) {
+    eg_src_load_lc<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v);
+  };
+  constexpr int kV = WPL + 1;
+#else
   auto emit = [&](const Row& cur, const uint64_t (&v)[WPL], uint64_t last) {
     if (cur.L > kCapBits) {  // k_rows_global writes the row
       if (lane == 0) {
@@ -2024,9 +2114,11 @@ __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
   auto load = [&](const Row& r, uint64_t (&v)[WPL], uint64_t& last) {
     eg_src_load<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v, last);
   };
+  constexpr int kV = WPL;
+#endif
   for (uint32_t k = 0; k < R; k += kK1Batch) {  // (batches as k_emit_k0)
     Row r[kK1Batch];
-    uint64_t v[kK1Batch][WPL], l[kK1Batch];
+    uint64_t v[kK1Batch][kV], l[kK1Batch];
 #pragma unroll
     for (int u = 0; u < kK1Batch; ++u) {
       r[u] = place(k + u < R ? k + u : k);
@@ -2035,6 +2127,30 @@ __global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
 #pragma unroll
     for (int u = 0; u < kK1Batch; ++u)
       if (k + u < R) emit(r[u], v[u], l[u]);
+  }
+}
+
+// Both classes in one launch: persistent waves take their share of each list, the odd waves the k = 1
+// rows first and the even waves the k = 0 rows first -- the copies (memory-bound) and the byte-table
+// rows (issue-bound) run side by side instead of one launch after the other.
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
+  __shared__ uint32_t s_lut[512];
+  const int lane = lane_id();
+  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
+  // every wave writes the whole table itself (the same values as the others): its own reads then
+  // follow its own writes, and the kernel needs no workgroup barrier
+  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+  const uint32_t nw = gridDim.x * 4;
+  // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
+  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (i0 & 1) {
+    k1_rows<WPL>(a, i0, nw, gimg, s_lut);
+    k0_rows<WPL>(a, i0, nw);
+  } else {
+    k0_rows<WPL>(a, i0, nw);
+    k1_rows<WPL>(a, i0, nw, gimg, s_lut);
   }
 }
 
@@ -2360,10 +2476,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
 #define BIC_EMITC(W)                                                                                      \
   {                                                                                                    \
     k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                    \
-    static const int o0_ = occ_of(reinterpret_cast<const void*>(&k_emit_k0<W>));                      \
-    static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1<W>));                      \
-    k_emit_k0<W><<<egrid_of(o0_), 256, 0, s>>>(a);                                                     \
-    k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                     \
+    static const int o_ = occ_of(reinterpret_cast<const void*>(&k_emit_k01<W>));                      \
+    k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                     \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
 #undef BIC_EMITC

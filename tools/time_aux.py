@@ -1,7 +1,7 @@
 """Timing of the §8 rows beside the encoder (measurement for DESIGN.md §3, not a test): at configs[2]'s
 size (8 planes of 16384^2, Bernoulli(0.5) pixels, device-resident) -- the packed encoder with its row
 index, the device decoders (Golomb from the index, EG, both through unmed), the adaptive EG coder
-(encode), bic_row_index from planes, PBM unpack / pack of one plane, P5 raster -> planes, planes -> gray. HIP events
+(encode, its row index and its device decoder), bic_row_index from planes, PBM unpack / pack of one plane, P5 raster -> planes, planes -> gray. HIP events
 around R launches of each call after a warm-up; every decode is checked against the planes.
 Usage: python tools/time_aux.py [--reps R] > gpurun_out/time_aux.json"""
 import argparse
@@ -85,6 +85,16 @@ def main():
     e2bytes = int(pybic.as_u64(b2).sum()) // 8
     timed("encode_eg_adaptive", lambda: ctx.encode_planes(planes, cols, True, 2, out=o2, plane_bits=b2),
           plane_bytes + e2bytes)
+    ai = ctx.empty_i64(n * rows * 2)
+    timed("egad_row_index", lambda: ctx.egad_row_index(planes, cols, True, out=ai), plane_bytes + n * rows * 16)
+
+    def dec_a():
+        ctx.decode_planes(2, o2, b2, n, rows, cols, True, row_index=ai, p00=p00, out=back)
+    back.zero_()
+    dec_a()
+    ctx.sync()
+    out["decode_eg_adaptive_ok"] = bool(torch.equal(back, planes))
+    timed("decode_eg_adaptive", dec_a, e2bytes + n * rows * 16 + plane_bytes)
 
     p1 = planes[0]
     raster = ctx.pbm_pack(p1, cols)
