@@ -1781,6 +1781,11 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
   }
 }
 
+#ifndef BIC_KNOWN_BATCH
+#define BIC_KNOWN_BATCH 4
+#endif
+template <int WPL>
+constexpr int kKnownBatch = WPL == 1 ? BIC_KNOWN_BATCH : 1;
 // ES: the residual rows from the EG stream the count pass wrote (FusedArgs::esrc; PREDICT false)
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E, bool ES = false>
 __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) {
@@ -1796,7 +1801,41 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   // persistent waves: rows id, id + stride, ...
   const uint64_t stride = (uint64_t)gridDim.x * kEmitWaves;
-  const uint64_t id0 = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves + wave;
+  const uint64_t id0 = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kEmitWaves +
+                       (uint32_t)__builtin_amdgcn_readfirstlane(wave);  // (uniform, as the compiler sees it)
+  if constexpr (!ES && kKnownBatch<WPL> > 1) {
+    // one-word rows (WPL = 1: rows of <= 4096 columns, e.g. C4's frames) are latency-bound: a wave
+    // loads kKnownBatch rows before it stores the first one's output (a wave that loaded after
+    // storing would wait for its stores' acknowledgements every row: vmcnt counts both)
+    constexpr int B = kKnownBatch<WPL>;
+    for (uint64_t id = id0; id < nrows; id += stride * B) {
+      uint64_t cp_[B][WPL], cu_[B][WPL];
+      uint32_t O[B];
+      uint64_t Lf[B], Gb[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const uint64_t iu = id + u * stride < nrows ? id + u * stride : id;
+        const uint32_t plane = (uint32_t)(iu / g.rows), row = (uint32_t)(iu % g.rows);
+        row_load<WPL, PREDICT>(a.planes, g, plane, row, cp_[u], cu_[u]);
+        O[u] = a.row_o[iu];
+        Lf[u] = DO_G ? a.glen[iu] : 0;
+        Gb[u] = DO_G ? gb_abs(a, iu, plane) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const uint64_t iu = id + u * stride;
+        if (iu >= nrows) break;
+        const uint32_t plane = (uint32_t)(iu / g.rows), row = (uint32_t)(iu % g.rows);
+        uint64_t rr[WPL];
+        row_resid<WPL, PREDICT>(g, row, cp_[u], cu_[u], rr);
+        const uint64_t Eb = DO_E ? (a.ebase ? a.ebase[plane] : (uint64_t)plane * a.slot_e * 64) : 0;
+        emit_known_row<WPL, PREDICT, DO_G, DO_E>(a, iu, plane, row, rr, O[u], Lf[u], Gb[u], Eb, gimg, s_lut);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    return;
+  }
   for (uint64_t id = id0; id < nrows; id += stride) {
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     STAMP(0);
