@@ -359,119 +359,20 @@ __device__ __forceinline__ void eg_lane_runs(const EgLane<WPL>& L, uint32_t cols
   if (L.eol) f((uint32_t)((int)cols - 1 - prev), true);
 }
 
-// ---- byte-table walk -------------------------------------------------------------------------
-// The coder pixel by pixel (the same codewords as eg_run's run by run): a 0 pixel adds to the zeros of
-// the current block (c), and a full block is its '1' and incBlockSize; a 1 pixel is the '0' and c in
-// g bits, then decBlockSize; a row's end is its '1'. So the state between pixels is (index, c) with
-// c < block size, and while the index stays <= 7 (block size <= 2, g <= 1) there are 13 states
-// (0-3; 4-7 with c 0 or 1; a fresh coder): one table entry per (state, byte of 8 pixels) gives the
-// byte's codewords (<= 16 bits: <= 2 per pixel), their length and the state after it. Bytes from
-// other states (sparse rows: long runs, the index high), a lane's last partial byte and the pixels
-// the table cannot finish (the index passing 7) go pixel by pixel; a run of zeros costs one step per
-// block. Dense rows -- most runs 0..3 long, the index near 0 -- take one lookup per 8 pixels instead
-// of eg_run's step per run.
-constexpr uint32_t kEgTabStates = 13, kEgTabFresh = 12, kEgTabEsc = 1u << 31;
-__device__ __forceinline__ int eg_tab_state(uint32_t i, uint32_t c) {
-  return i == kFresh ? (int)kEgTabFresh : i < 4 ? (int)i : i < 8 ? (int)(4 + 2 * (i - 4) + c) : -1;
-}
-__device__ __forceinline__ void eg_tab_unstate(uint32_t st, uint32_t& i, uint32_t& c) {
-  i = st == kEgTabFresh ? kFresh : st < 4 ? st : 4 + ((st - 4) >> 1);
-  c = (st >= 4 && st < kEgTabFresh) ? (st - 4) & 1u : 0u;
-}
-// z zeros from (i, c): a '1' per block they complete (put(value, bits))
-template <typename Put>
-__device__ __forceinline__ void eg_zeros(uint32_t& i, uint32_t& c, uint32_t z, Put&& put) {
-  while (z) {
-    const uint32_t bs = i == kFresh ? 1u : 1u << eg_j(i);
-    if (c + z < bs) {
-      c += z;
-      return;
-    }
-    z -= bs - c;
-    c = 0;
-    put(1u, 1u);
-    i = i == kFresh ? 1u : (i < 31 ? i + 1 : 31u);
-  }
-}
-template <typename Put>
-__device__ __forceinline__ void eg_one(uint32_t& i, uint32_t& c, Put&& put) {
-  const uint32_t g = i == kFresh ? 1u : eg_j(i);
-  put(c, 1 + g);  // '0' and the remainder in g bits
-  i = (i == kFresh || i == 0) ? 0u : i - 1;
-  c = 0;
-}
-// entry (state << 8 | byte): codewords | length << 16 | next state << 21, or kEgTabEsc
-__device__ uint32_t eg_tab_entry(uint32_t e) {
-  uint32_t i, c;
-  eg_tab_unstate(e >> 8, i, c);
-  uint32_t pat = 0, len = 0;
-  bool esc = false;
-  auto put = [&](uint32_t v, uint32_t n) {
-    pat = (pat << n) | v;
-    len += n;
-  };
-  for (int q = 0; q < 8; ++q) {
-    if ((e >> (7 - q)) & 1u) eg_one(i, c, put);
-    else eg_zeros(i, c, 1, put);
-    if (i != kFresh && i > 7) esc = true;
-  }
-  return esc ? kEgTabEsc : pat | (len << 16) | ((uint32_t)eg_tab_state(i, c) << 21);
-}
-__device__ __forceinline__ void eg_tab_build(uint32_t* T) {
-  for (uint32_t e = threadIdx.x; e < kEgTabStates * 256; e += blockDim.x) T[e] = eg_tab_entry(e);
-  __syncthreads();
-}
-// The lane's runs from index s (a run boundary) through the table: put(value, bits) per codeword
-// piece; returns the index after the lane's last run (s itself when no run ends in the lane).
-template <int WPL, typename Put>
-__device__ __forceinline__ uint32_t eg_lane_walk_tab(const EgLane<WPL>& L, uint32_t cols, uint32_t s, const uint32_t* T,
-                                                     Put&& put) {
-  int lastc = -1;
-#pragma unroll
-  for (int t = 0; t < WPL; ++t)
-    if (L.R[t]) lastc = (int)((L.w0 + t) * 64 + 63 - __builtin_ctzll(L.R[t]));
-  if (lastc < 0 && !L.eol) return s;  // no run ends here: the identity
-  uint32_t i = s, c = 0;
-  eg_zeros(i, c, L.w0 * 64 - (uint32_t)(L.jp + 1), put);  // the first run's zeros before the lane
-  const uint32_t endc = L.eol ? cols : (uint32_t)lastc + 1;  // the lane's columns [w0 * 64, endc)
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) {
-    const uint64_t x = L.R[t];
-    for (int b = 0; b < 8; ++b) {
-      const uint32_t p0 = (L.w0 + t) * 64 + 8 * b;
-      if (p0 >= endc) break;
-      const uint32_t v = (uint32_t)(x >> (56 - 8 * b)) & 0xffu;
-      const uint32_t np = min(8u, endc - p0);
-      const int st = eg_tab_state(i, c);
-      if (np == 8 && st >= 0) {
-        const uint32_t en = T[(uint32_t)st * 256 + v];
-        if (!(en & kEgTabEsc)) {
-          const uint32_t n = (en >> 16) & 31u;
-          if (n) put(en & 0xffffu, n);
-          eg_tab_unstate(en >> 21, i, c);
-          continue;
-        }
-      }
-      for (uint32_t q = 0; q < np; ++q) {
-        if ((v >> (7 - q)) & 1u) eg_one(i, c, put);
-        else eg_zeros(i, c, 1, put);
-      }
-    }
-  }
-  if (L.eol) put(1u, 1u);  // the end of the row
-  return i;
-}
-
 template <int WPL>
-__device__ __forceinline__ uint32_t eg_lane_walk(const EgLane<WPL>& L, uint32_t cols, uint32_t s, const uint32_t* T) {
-  return eg_lane_walk_tab(L, cols, s, T, [](uint32_t, uint32_t) {});
+__device__ __forceinline__ uint32_t eg_lane_walk(const EgLane<WPL>& L, uint32_t cols, uint32_t s) {
+  eg_lane_runs(L, cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    s = eg_run(s, len, eol, nb, m, g, rem);
+  });
+  return s;
 }
 
 // Every lane's start state for the row start s0 (lane 0 starts at s0): constant maps are known at
 // once; a round hands each known end to the next lane. Returns the lane's start; *end = its end.
 template <int WPL>
 __device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t cols, uint32_t lo, uint32_t hi,
-                                                  uint32_t s0, uint32_t* end, const uint32_t* T) {
+                                                  uint32_t s0, uint32_t* end) {
   const int lane = lane_id();
   const bool ident = lo == kIdent;
   bool done = !ident && lo == hi;
@@ -482,7 +383,7 @@ __device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t
       if (ident) sout = sin;
       else if (sin == 0 || sin == kFresh) sout = lo;  // (a fresh coder steps like index 0)
       else if (sin == 31) sout = hi;
-      else sout = eg_lane_walk(L, cols, sin, T);
+      else sout = eg_lane_walk(L, cols, sin);
       done = true;
     }
     const uint32_t prev = (uint32_t)dpp_or<0x138>((int)kUnk, (int)(done ? sout : kUnk));
@@ -496,23 +397,26 @@ __device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t
 // The lanes' maps and the row's map F_r(0), F_r(31) (lane 63 carries the row's end).
 template <int WPL>
 __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
-  __shared__ uint32_t T[kEgTabStates * 256];
-  eg_tab_build(T);
   const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (id >= (uint64_t)a.rows * a.nplanes) return;  // whole wave
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
-  bool any = L.eol;
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) any |= L.R[t] != 0;
-  uint32_t lo = eg_lane_walk(L, a.cols, 0, T);
-  const uint32_t hi = eg_lane_walk(L, a.cols, 31, T);
-  if (!any) lo = kIdent;
+  uint32_t lo = 0, hi = 31;
+  bool any = false;
+  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    any = true;
+    const bool same = hi == lo;  // met: one trajectory from here on (a branch: the wave skips the
+    lo = eg_run(lo, len, eol, nb, m, g, rem);  // second walk once every lane's two have met)
+    if (same) hi = lo;
+    else hi = eg_run(hi, len, eol, nb, m, g, rem);
+  });
+  if (!any) lo = hi = kIdent;
   a.lane_lo[id * 64 + lane_id()] = (uint8_t)lo;
-  a.lane_hi[id * 64 + lane_id()] = (uint8_t)(any ? hi : kIdent);
+  a.lane_hi[id * 64 + lane_id()] = (uint8_t)hi;
   uint32_t e0, e31;
-  (void)eg_lane_chain(L, a.cols, lo, any ? hi : kIdent, 0, &e0, T);
-  (void)eg_lane_chain(L, a.cols, lo, any ? hi : kIdent, 31, &e31, T);
+  (void)eg_lane_chain(L, a.cols, lo, hi, 0, &e0);
+  (void)eg_lane_chain(L, a.cols, lo, hi, 31, &e31);
   if (lane_id() == 63) {
     a.lo_end[id] = (uint8_t)e0;
     a.hi_end[id] = (uint8_t)e31;
@@ -522,17 +426,19 @@ __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
 // The row's bits from its start state: per lane its start and bits, the row's total.
 template <int WPL>
 __global__ __launch_bounds__(256) void k_egad_llen(EgadArgs a) {
-  __shared__ uint32_t T[kEgTabStates * 256];
-  eg_tab_build(T);
   const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
   const uint32_t lo = a.lane_lo[id * 64 + lane_id()], hi = a.lane_hi[id * 64 + lane_id()];
   uint32_t end;
-  const uint32_t s = eg_lane_chain(L, a.cols, lo, hi, a.start[id], &end, T);
-  uint32_t bits = 0;
-  (void)eg_lane_walk_tab(L, a.cols, s, T, [&](uint32_t, uint32_t n) { bits += n; });
+  const uint32_t s = eg_lane_chain(L, a.cols, lo, hi, a.start[id], &end);
+  uint32_t bits = 0, t = s;
+  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    t = eg_run(t, len, eol, nb, m, g, rem);
+    bits += nb;
+  });
   a.lane_st[id * 64 + lane_id()] = (uint8_t)s;
   a.lane_bits[id * 64 + lane_id()] = bits;
   const uint64_t tot = wave_sum_u64(bits);
@@ -571,8 +477,6 @@ struct EgImgSink {
 template <int WPL>
 __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t imgs[4][kEgImg];
-  __shared__ uint32_t T[kEgTabStates * 256];
-  eg_tab_build(T);
   const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint64_t Ltot = a.len[id];
@@ -593,9 +497,25 @@ __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   uint32_t pos = wave_incl_sum_u32(bits) - bits;  // the lane's first bit in the row
   uint32_t s = a.lane_st[id * 64 + lane_id()];
   EgImgSink k{img, 0, 0};
-  (void)eg_lane_walk_tab(L, a.cols, s, T, [&](uint32_t v, uint32_t n) {
-    k.put(pos, (uint64_t)v, n);
-    pos += n;
+  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
+    uint32_t nb, m, g, rem;
+    s = eg_run(s, len, eol, nb, m, g, rem);
+    while (m >= 64) {  // a '1' per full block
+      k.put(pos, ~0ull, 64);
+      pos += 64;
+      m -= 64;
+    }
+    if (m) {
+      k.put(pos, ~0ull, m);
+      pos += m;
+    }
+    if (eol) {
+      k.put(pos, 1ull, 1);  // end of row
+      pos += 1;
+    } else {
+      k.put(pos, (uint64_t)rem, 1 + g);  // '0' and the g-bit remainder
+      pos += 1 + g;
+    }
   });
   k.flush();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -1782,7 +1782,7 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
 }
 
 #ifndef BIC_KNOWN_BATCH
-#define BIC_KNOWN_BATCH 4
+#define BIC_KNOWN_BATCH 1  // (4: C4 0.272 -> 0.309 ms; kept as a build-time A/B knob)
 #endif
 template <int WPL>
 constexpr int kKnownBatch = WPL == 1 ? BIC_KNOWN_BATCH : 1;
