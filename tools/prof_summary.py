@@ -63,6 +63,7 @@ def main():
     # (the first kernel of each list runs once per launch of the sequence: it gives the count)
     rows = ["k_emit_known", "k_emit_rest", "k_encode_rows", "k_len_rows", "k_emit_rows"]
     timers = {"encode_rows_golomb_eg": rows, "encode_rows_golomb": rows, "encode_rows_eg": rows,
+              "encode_rows_golomb_egsrc": ["k_emit_k01", "k_emit_rest", "k_emit_known"],
               "encode_prefix": ["k_row_walk", "k_scan_rows", "k_med_kstat"],
               "bitplanes_count": ["k_gray_strips"],
               "encode_finish": ["k_rows_global", "k_fixup"],
