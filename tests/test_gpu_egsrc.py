@@ -91,3 +91,39 @@ def test_eg_source_matches_resid_path(ctx, oracle, staged):
         nw = (int(res[0][1][k]) + 63) // 64
         assert np.array_equal(res[0][0][k][:nw], res[1][0][k][:nw])
     assert np.array_equal(res[0][2], res[1][2])
+
+
+_FRESH = r"""
+import sys
+sys.path.insert(0, {pkg!r}); sys.path.insert(0, {tests!r})
+import numpy as np
+import pybic
+from oracle_lib import Oracle
+o = Oracle()
+rows, cols = 70, 4096
+img = o.gen_bytes(rows * 13 + cols, rows * cols).reshape(rows, cols)
+P = o.bitplanes(img, 8)
+ctx = pybic.Context(0)
+ctx.set_encoder("staged")
+g = ctx.torch.from_numpy(img).to(ctx.dev)
+_, (og, bg), _ = ctx.encode_gray(g, store_planes=False)  # the process's first encode
+ctx.sync()
+bad = [k for k in range(8) if pybic.stream_bytes(og[k], o.encode_plane(P[k], cols, 1, 0)[0])
+       != o.encode_plane(P[k], cols, 1, 0)[1].tobytes()]
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
+def test_first_encode_of_a_process():
+    """The first encode of a fresh process: with device-scope fork / join events on the second
+    stream it read stale prefix data (class-kernel rows wrong in 15 of 16 fresh processes on the
+    pool's boxes). Two fresh processes, each checked against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _FRESH.format(pkg=os.path.join(root, "binary-image-compression_amd"), tests=os.path.join(root, "tests"))
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
