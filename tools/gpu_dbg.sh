@@ -1,7 +1,16 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests/test_gpu_egad.py tests/test_gpu_decode.py tests/test_gpu_fused.py tests/test_gpu_egsrc.py > gpurun_out/t14.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest -q -x --timeout 300 --timeout-method thread tests/test_gpu_egsrc.py tests/test_gpu_fused.py tests/test_gpu_fullsize.py tests/test_gpu_multirank.py > gpurun_out/t17.log 2>&1; rc=$?
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-bash tools/bench_lines.sh r04c4 "--workload c4 --steps 20 --no-cpu" "--workload c2 --steps 50 --no-cpu" "--workload c2 --steps 50 --no-cpu --encoder staged" "--steps 20 --no-cpu" "--shard planes --plane-count 1 --steps 20 --no-cpu" "--shard planes --plane-count 2 --steps 20 --no-cpu" "--shard planes --plane-count 4 --steps 20 --no-cpu" > gpurun_out/lines14.log 2>&1 || exit 1
-timeout -k 10 300 python -u tools/time_aux.py --reps 3 > gpurun_out/time_aux14.json 2> gpurun_out/time_aux.err || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
+: > gpurun_out/ab17.log
+for v in libbic exp_wk0 libbic exp_wk0; do
+  for w in c3 c4; do
+  BIC_LIB_PATH=binary-image-compression_amd/lib/$v.so timeout -k 10 240 python -u bench.py --workload $w --steps 20 --warmup 3 --no-cpu > gpurun_out/b17.json 2>> gpurun_out/ab17.err || exit $?
+  python3 -c "
+import json
+j=json.loads([l for l in open('gpurun_out/b17.json') if l.startswith('{')][-1])
+print('$v $w |', j['ms_per_step'], j.get('bit_exact_check'), {k: round(v['avg_us'],1) for k, v in j['kernels'].items()})" >> gpurun_out/ab17.log
+  done
+done
