@@ -143,6 +143,8 @@ VAR_CASES = CASES[:8] + [
     (6, 36, 72, 37, 20, ("random", 0.5)),       # T >= M + 1: every search ends after its first window
     (16, 256, 256, 0, 10000, ("periodic", 24, 40, 0.5, 0.001)),  # region beyond the LDS image
     (8, 96, 200, 0, 10000, ("text",)),
+    (8, 512, 512, 0, 64, ("text",)),             # 512^2, the drivers' W
+    (4, 512, 512, 2, 32, ("random", 0.05)),
 ]
 
 
