@@ -66,6 +66,10 @@ def parse():
                     help="c4 / c3 --shard planes at N > 1: encode a rank's units in this many chunks, each chunk's "
                          "streams sent to rank 0 while the next encodes (pybic.parallel.ChunkedGather); 0 = auto "
                          "(2 for c4, 1 per plane for --shard planes), 1 = one gather after the encode")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="c3 (one-call, planes NULL): images in flight -- this many contexts, each on its own HIP "
+                         "stream, take successive images, so one image's emission overlaps the next one's count "
+                         "pass (serving throughput; the roofline kernel is timed on the first context's launches)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
@@ -220,8 +224,9 @@ class C3:
         g = t.Generator(device=ctx.dev)
         g.manual_seed(0x5EED0000 + rank)
         # two gray buffers, alternated per step, so the Infinity Cache cannot serve re-runs
+        self.inflight = max(1, args.inflight)
         self.gray = [t.randint(0, 256, (self.rows, self.cols), dtype=t.uint8, device=ctx.dev, generator=g)
-                     for _ in range(2)]
+                     for _ in range(max(2, self.inflight))]
         self.wpr = (self.cols + 63) // 64
         self.separate = args.separate
         self.store_planes = args.store_planes or args.separate
@@ -237,22 +242,45 @@ class C3:
         self.bits_g = ctx.empty_i64(self.nplanes)
         self.bits_e = ctx.empty_i64(self.nplanes)
         ctx.reserve(self.nplanes, self.rows, self.cols)
+        self.lanes = None
+        if self.inflight > 1:
+            # images in flight: context i (its own stream, aux stream and scratch) encodes images k = i mod n;
+            # one context per stream (include/bic.h), outputs per context
+            if self.separate or self.store_planes:
+                raise SystemExit("--inflight needs the one-call encode with planes NULL")
+            self.lanes = [(ctx, t.cuda.Stream(ctx.dev), self.out_g, self.out_e, self.bits_g, self.bits_e)]
+            for _ in range(self.inflight - 1):
+                c = pybic.Context(ctx.dev.index)
+                c.set_encoder(args.encoder)
+                c.set_eg_source(args.eg_source_mode if self.eg_src else 0)
+                c.reserve(self.nplanes, self.rows, self.cols)
+                self.lanes.append((c, t.cuda.Stream(ctx.dev), c.empty_i64(self.nplanes, self.slot_g),
+                                   c.empty_i64(self.nplanes, self.slot_e), c.empty_i64(self.nplanes),
+                                   c.empty_i64(self.nplanes)))
         self.k = 0
         self.pixels = self.rows * self.cols * self.nplanes
         self.workload = (f"c3: {self.rows}x{self.cols} 8-bit gray -> 8 bitplanes -> med -> per-row runs "
                          f"-> Golomb + EG streams per plane" +
                          ("" if self.store_planes else " (bitplanes formed in registers, not returned: planes NULL)") +
                          (" -- the count pass writes the EG stream, the Golomb emission reads the residual rows "
-                          "from it" if self.eg_src else ""))
+                          "from it" if self.eg_src else "") +
+                         (f" -- {self.inflight} images in flight (one context and HIP stream each)"
+                          if self.inflight > 1 else ""))
 
     def step(self):
         c = self.ctx
-        if self.separate:
-            c.bitplanes_u8(self.gray[self.k & 1], nplanes=8, out=self.planes)
+        if self.lanes:
+            i = self.k % self.inflight
+            c, s, self.out_g, self.out_e, self.bits_g, self.bits_e = self.lanes[i]  # the last step's outputs
+            with self.ctx.torch.cuda.stream(s):
+                c.encode_gray(self.gray[i], nplanes=8, planes=None, slots=(self.slot_g, self.slot_e),
+                              outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e), store_planes=False)
+        elif self.separate:
+            c.bitplanes_u8(self.gray[self.k % len(self.gray)], nplanes=8, out=self.planes)
             c.encode_planes2(self.planes, self.cols, True, slots=(self.slot_g, self.slot_e),
                              outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e))
         else:  # one call: bitplanes + both streams (bic_encode_gray)
-            c.encode_gray(self.gray[self.k & 1], nplanes=8, planes=self.planes, slots=(self.slot_g, self.slot_e),
+            c.encode_gray(self.gray[self.k % len(self.gray)], nplanes=8, planes=self.planes, slots=(self.slot_g, self.slot_e),
                           outs=(self.out_g, self.out_e), bits=(self.bits_g, self.bits_e),
                           store_planes=self.store_planes)
         self.k += 1
@@ -275,7 +303,7 @@ class C3:
 
     def host_planes(self, rows):
         if self.planes is None:  # the last step's image's planes (device bitplane kernel), for the CPU leg
-            return self.pybic.as_u64(self.ctx.bitplanes_u8(self.gray[(self.k - 1) & 1][:rows], nplanes=self.nplanes))
+            return self.pybic.as_u64(self.ctx.bitplanes_u8(self.gray[(self.k - 1) % len(self.gray)][:rows], nplanes=self.nplanes))
         return self.pybic.as_u64(self.planes[:, :rows])
 
     def predictor_pass(self, reps):
@@ -285,8 +313,8 @@ class C3:
         planes once; not part of `value`. Two plane buffers (the planes of the two gray images)
         alternate, so the 256 MB Infinity Cache cannot hold the input of the next launch
         (SURVEY.md §8 d)."""
-        alt = self.ctx.bitplanes_u8(self.gray[self.k & 1], nplanes=8)  # the other image's planes
-        cur = self.planes if self.planes is not None else self.ctx.bitplanes_u8(self.gray[(self.k - 1) & 1], nplanes=8)
+        alt = self.ctx.bitplanes_u8(self.gray[self.k % len(self.gray)], nplanes=8)  # the other image's planes
+        cur = self.planes if self.planes is not None else self.ctx.bitplanes_u8(self.gray[(self.k - 1) % len(self.gray)], nplanes=8)
         bufs = [cur, alt]
         self.ctx.sync()
         self.ctx.prof_enable(True)
@@ -308,7 +336,7 @@ class C3:
         """every plane of the last step: the planes (when returned) == the oracle's bitplanes of the
         gray image, and each plane's Golomb and EG streams == the oracle's streams of those bitplanes
         (host threads)"""
-        gray = self.gray[(self.k - 1) & 1].cpu().numpy()
+        gray = self.gray[(self.k - 1) % len(self.gray)].cpu().numpy()
         P = oracle.bitplanes_par(gray, self.nplanes)
         if self.planes is not None and not np.array_equal(self.pybic.as_u64(self.planes), P):
             return False

@@ -127,3 +127,31 @@ def test_first_encode_of_a_process():
     for _ in range(2):
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_images_in_flight(ctx, oracle, staged):
+    """bench.py --inflight: two contexts, each on its own HIP stream, encode alternate images with no
+    synchronisation between launches (one image's emission overlapping the next one's count pass);
+    every image's streams == the oracle's"""
+    import pybic
+    t = ctx.torch
+    rows, cols = 96, 8192
+    imgs = [_img(oracle, 900 + i, rows, cols, ("uniform", "smooth", "sparse", "uniform")[i]) for i in range(4)]
+    ctxs = [ctx, pybic.Context(ctx.dev.index)]
+    ctxs[1].set_encoder("staged")
+    streams = [t.cuda.Stream(ctx.dev) for _ in range(2)]
+    gs = [t.from_numpy(im).to(ctx.dev) for im in imgs]
+    t.cuda.synchronize()
+    outs = []
+    for rnd in range(3):
+        for i, g in enumerate(gs):
+            with t.cuda.stream(streams[i & 1]):
+                outs.append((i, ctxs[i & 1].encode_gray(g, store_planes=False)))
+    t.cuda.synchronize()
+    for i, (_, (og, bg), (oe, be)) in outs:
+        P = oracle.bitplanes(imgs[i], 8)
+        for k in range(8):
+            for coder, out, bits in ((0, og, bg), (1, oe, be)):
+                eb, est, _ = oracle.encode_plane(P[k], cols, 1, coder)
+                assert int(as_u64(bits)[k]) == eb, (i, k, coder)
+                assert stream_bytes(out[k], eb) == est.tobytes(), (i, k, coder)
