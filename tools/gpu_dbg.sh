@@ -1,4 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -v -x --timeout 120 --timeout-method thread tests/test_gpu_egsrc.py > gpurun_out/t19.log 2>&1 || exit $?
+bash tools/ab_exp.sh "--steps 30 --warmup 5" s1 s128 s512 > gpurun_out/ab_sink.log 2>&1 || exit $?
