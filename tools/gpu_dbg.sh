@@ -1,4 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash tools/ab_exp.sh "--steps 30 --warmup 5" base b22 wpe4 k1b2 > gpurun_out/ab_k3.log 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/final_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py > gpurun_out/final_bench.log 2>&1 || exit $?
