@@ -2169,9 +2169,10 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
   }
 }
 
-// Both classes in one launch: persistent waves take their share of each list, the odd waves the k = 1
-// rows first and the even waves the k = 0 rows first -- the copies (memory-bound) and the byte-table
-// rows (issue-bound) run side by side instead of one launch after the other.
+// Both classes in one launch: persistent waves take their share of each list, the k = 0 rows first.
+// The waves reach the byte-table rows at different times, so the copies (memory-bound) and the
+// byte-table rows (issue-bound) run side by side instead of one launch after the other. (Odd waves
+// starting on the k = 1 rows measured 196-198 µs against 192-193, round 4.)
 template <int WPL>
 __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
@@ -2184,13 +2185,8 @@ __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   const uint32_t nw = gridDim.x * 4;
   // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
   const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (i0 & 1) {
-    k1_rows<WPL>(a, i0, nw, gimg, s_lut);
-    k0_rows<WPL>(a, i0, nw);
-  } else {
-    k0_rows<WPL>(a, i0, nw);
-    k1_rows<WPL>(a, i0, nw, gimg, s_lut);
-  }
+  k0_rows<WPL>(a, i0, nw);
+  k1_rows<WPL>(a, i0, nw, gimg, s_lut);
 }
 
 // The rows the prefix kernels leave to this launch: Golomb rows with mixed k (per-codeword k,
