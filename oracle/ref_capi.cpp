@@ -15,6 +15,8 @@
 #include "eg.h"
 
 #include <chrono>
+#include <cstring>
+#include <sstream>
 #include <cstdint>
 #include <cstdio>
 #include <vector>
@@ -335,8 +337,9 @@ double ref_baseline_planes(const uint64_t* planes, int nplanes, size_t rows, siz
 }  // extern "C"
 
 // compress_test.cpp:73-111's search on the reference's own binary_matrix (get_submatrix, dist)
-extern "C" int ref_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
-                                uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+// wP (nullable): per tile P.weight() (compress_test.cpp:119-120 prints lengths from it)
+extern "C" int ref_patch_search_w(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                                  uint32_t* besti, uint32_t* bestj, uint32_t* bestd, uint32_t* wP) {
   binary_matrix A = from_words(I, rows, cols, wpr);
   const idx_t Ny = (W - 1 + rows) / W, Nx = (W - 1 + cols) / W;
   binary_matrix P, P2;
@@ -365,9 +368,51 @@ extern "C" int ref_patch_search(const uint64_t* I, size_t rows, size_t cols, siz
       besti[li] = (uint32_t)bi;
       bestj[li] = (uint32_t)bj;
       bestd[li] = (uint32_t)bd;
+      if (wP) wP[li] = (uint32_t)P.weight();
     }
   P.destroy();
   P2.destroy();
+  A.destroy();
+  return 0;
+}
+
+extern "C" int ref_patch_search(const uint64_t* I, size_t rows, size_t cols, size_t wpr, unsigned W,
+                                uint32_t* besti, uint32_t* bestj, uint32_t* bestd) {
+  return ref_patch_search_w(I, rows, cols, wpr, W, besti, bestj, bestd, nullptr);
+}
+
+// compress6_test.cpp:62-78 prints its M x M predictor matrices (D: ones on the diagonal and the first
+// superdiagonal; iD: the upper triangle) through the reference's operator<< (binmat.cpp:624-644) before
+// set_grid_width is called (so with the default grid width). Those lines, into buf (NUL-terminated);
+// returns their length, or -1 when cap is too small.
+extern "C" long ref_print_pred_matrices(unsigned M, char* buf, size_t cap) {
+  binary_matrix D(M, M), iD(M, M);
+  D.clear();
+  iD.clear();
+  for (idx_t i = 0; i < M; i++) {
+    D.set(i, i);
+    if (i > 0) D.set(i - 1, i);
+    for (idx_t j = i; j < M; j++) iD.set(i, j);
+  }
+  set_grid_width(10);  // binmat.cpp:618's initial value, what the driver prints with
+  std::ostringstream os;
+  os << "D:<<" << D << std::endl;
+  os << "iD:<<" << iD << std::endl;
+  D.destroy();
+  iD.destroy();
+  const std::string t = os.str();
+  if (t.size() + 1 > cap) return -1;
+  std::memcpy(buf, t.c_str(), t.size() + 1);
+  return (long)t.size();
+}
+
+// write_pbm (pbm.cpp) of a plane given as words: the file a driver writes for its final image.
+extern "C" int ref_write_pbm(const uint64_t* P, size_t rows, size_t cols, size_t wpr, const char* path) {
+  binary_matrix A = from_words(P, rows, cols, wpr);
+  FILE* o = fopen(path, "w");
+  if (!o) { A.destroy(); return -1; }
+  write_pbm(A, o);
+  fclose(o);
   A.destroy();
   return 0;
 }
@@ -379,9 +424,11 @@ extern "C" int ref_patch_search(const uint64_t* I, size_t rows, size_t cols, siz
 // converted to idx_t the same way; only ceil(log2(search_win_size)) for a size <= 0 (an undefined
 // conversion on x86-64: 2^63) is taken as "no match" directly. dP / dP3 are cleared first (the
 // driver leaves their (0,0) uninitialised). stats [4]: matches, bits match, bits nomatch, L.
-extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
-                              unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
-                              uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats) {
+// w4 (nullable): per tile the four weights the driver prints (compress7_test.cpp:191-209):
+// nonmatch/nonpred, nonmatch/pred, match/nonpred, match/pred.
+extern "C" int ref_match_loop_w4(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
+                                 unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                                 uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats, uint32_t* w4) {
   binary_matrix I = from_words(Iw, rows, cols, wpr);
   const int iW = (int)W, iR = (int)R;
   const idx_t M = (idx_t)W * W;
@@ -431,6 +478,12 @@ extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr
       med(P, dP);
       med(P3, dP3);
       const idx_t w_mp = dP3.weight(), w_np = dP.weight();
+      if (w4) {
+        w4[4 * li] = (uint32_t)w_nn;
+        w4[4 * li + 1] = (uint32_t)w_np;
+        w4[4 * li + 2] = (uint32_t)w_mn;
+        w4[4 * li + 3] = (uint32_t)w_mp;
+      }
       const bool ok = swin > 0;
       const idx_t idx_len = ok ? (idx_t)ceil(log2(swin)) : 0;
       const idx_t nn_len = 1 + 1 + enuml[w_nn], np_len = 1 + 1 + enuml[w_np];
@@ -473,13 +526,22 @@ extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr
   return 0;
 }
 
+extern "C" int ref_match_loop(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
+                              unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                              uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats) {
+  return ref_match_loop_w4(Iw, rows, cols, wpr, W, T, R, enuml, besti, bestj, bestd, weights, modes, stats, nullptr);
+}
+
 // The tile loops of compress4_test.cpp:89-170 (variant 4), compress5_test.cpp:89-170 (5) and
 // compress6_test.cpp:111-208 (6) over the reference's own objects (get_submatrix, dist, add, weight,
 // set_submatrix, GolombCoder), statement for statement; enumL from the caller (GSL is absent).
 // modes: 'x' match, 'o' no match.
-extern "C" int ref_match_loop_var(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
-                                  unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
-                                  uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats, int variant) {
+// w2 (nullable): per tile P.weight() and the match weight (the drivers print both, through their lengths
+// or directly: compress6_test.cpp:189-190).
+extern "C" int ref_match_loop_var_w2(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
+                                     unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                                     uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats, int variant,
+                                     uint32_t* w2) {
   if (variant < 4 || variant > 6) return -1;
   binary_matrix I = from_words(Iw, rows, cols, wpr);
   const int iW = (int)W, iR = (int)R;
@@ -536,6 +598,10 @@ extern "C" int ref_match_loop_var(uint64_t* Iw, size_t rows, size_t cols, size_t
         match_len = (bd <= M) ? (idx_t)(1 + idx_len + enuml[bd]) : 100000;
       }
       const idx_t wP = P.weight();
+      if (w2) {
+        w2[2 * li] = (uint32_t)wP;
+        w2[2 * li + 1] = (uint32_t)match_weight;
+      }
       const bool take = nomatch_len > match_len;
       if (take) {
         golomb_match.codeSample(match_weight);
@@ -564,6 +630,13 @@ extern "C" int ref_match_loop_var(uint64_t* Iw, size_t rows, size_t cols, size_t
   P3.destroy();
   I.destroy();
   return 0;
+}
+
+extern "C" int ref_match_loop_var(uint64_t* Iw, size_t rows, size_t cols, size_t wpr, unsigned W, unsigned T,
+                                  unsigned R, const double* enuml, uint32_t* besti, uint32_t* bestj,
+                                  uint32_t* bestd, uint32_t* weights, char* modes, uint64_t* stats, int variant) {
+  return ref_match_loop_var_w2(Iw, rows, cols, wpr, W, T, R, enuml, besti, bestj, bestd, weights, modes, stats,
+                               variant, nullptr);
 }
 
 // compress8_test.cpp:126-272's tile loop over the reference's own objects (get_submatrix, dist,
