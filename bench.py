@@ -384,8 +384,10 @@ class C3Planes(C3):
         self.gathered = (None, None)
         # overlapped gather (N > 1): the rank's planes in chunks (default one per plane), each chunk's
         # packed streams sent while the next chunk encodes
-        nch = max(1, min(args.chunks or self.nplanes, self.nplanes)) if world > 1 else 1
-        self.chunks = [(i * self.nplanes // nch, (i + 1) * self.nplanes // nch) for i in range(nch)]
+        # (the same chunk count on every rank, empty chunks where a rank has fewer planes: one all-gather
+        # per chunk -- pybic.parallel.plan_chunks)
+        from pybic.parallel import plan_chunks
+        self.chunks = plan_chunks(self.nplanes, P, world, args.chunks) if world > 1 else [(0, self.nplanes)]
         self.chunk_off = [[ctx.torch.zeros(b - a + 1, dtype=t.int64, device=ctx.dev) for _ in range(2)]
                           for a, b in self.chunks]
         ctx.reserve(n, self.rows, self.cols)
@@ -404,6 +406,10 @@ class C3Planes(C3):
             for (a, b), (fg, fe) in zip(self.chunks, self.chunk_off):
                 rg = self.out_g[a * self.slot_g:b * self.slot_g]
                 re = self.out_e[a * self.slot_e:b * self.slot_e]
+                if b == a:  # an empty chunk (this rank holds fewer planes than the plan's chunk count)
+                    cgs[0].add(rg, 0)
+                    cgs[1].add(re, 0)
+                    continue
                 c.encode_gray_packed(self.gray[self.k & 1], nplanes=b - a, plane0=self.lo + a,
                                      planes=None if self.planes is None else self.planes[a:b],
                                      slots=(self.slot_g, self.slot_e), outs=(rg, re),
@@ -622,8 +628,8 @@ class C4(C3):
         self.gathered = (None, None)
         # overlapped gather (N > 1): the rank's frames in chunks, each chunk's packed streams in its own
         # region of `packed`, sent while the next chunk encodes
-        nch = max(1, min(args.chunks or 2, self.nplanes)) if world > 1 else 1
-        self.chunks = [(i * self.nplanes // nch, (i + 1) * self.nplanes // nch) for i in range(nch)]
+        from pybic.parallel import plan_chunks
+        self.chunks = plan_chunks(self.nplanes, self.TOTAL, world, args.chunks or 2) if world > 1 else [(0, self.nplanes)]
         self.chunk_off = [ctx.torch.zeros(b - a + 1, dtype=t.int64, device=ctx.dev) for a, b in self.chunks]
         ctx.reserve(max(1, self.nplanes), self.rows, self.cols)
         self.k = 0

@@ -51,6 +51,16 @@ def gather_streams(packed, nwords, world=None, rank=None, dst=0):
     return None, None
 
 
+def plan_chunks(n_units, total_units, world, chunks=None):
+    """Chunk boundaries [(a, b), ...] over a rank's n_units units, for ChunkedGather. The count is the
+    same on every rank -- min(chunks or ceil(total/world), ceil(total/world)), a function of the job alone
+    -- because every chunk is one collective step (one all-gather of sizes); a rank with fewer units gets
+    empty chunks (a == b), which it still adds (with 0 words)."""
+    per = -(-int(total_units) // int(world))
+    nch = max(1, min(int(chunks) if chunks else per, per))
+    return [(i * n_units // nch, (i + 1) * n_units // nch) for i in range(nch)]
+
+
 class ChunkedGather:
     """gather_streams overlapped with the encode: a rank encodes its units (frames, planes) in chunks
     and hands each chunk's packed words here right after enqueueing its encode (add). finish() then
@@ -60,7 +70,10 @@ class ChunkedGather:
     is exposed. The host blocks on one chunk's size at a time (the receiver must post exact counts).
     dst receives every (rank, chunk) into its own buffer and concatenates them in rank order, chunk
     order: (words, offsets per rank) as gather_streams returns them. gloo (CPU tests) runs the same
-    protocol on host tensors, without streams."""
+    protocol on host tensors, without streams.
+
+    Every rank must add() the same number of chunks (plan_chunks gives such a plan; empty chunks are
+    allowed): each chunk is one all-gather, so unequal counts would leave ranks waiting on each other."""
 
     def __init__(self, device, world=None, rank=None, dst=0):
         self.world = world or dist.get_world_size()

@@ -191,3 +191,71 @@ def test_chunked_gather(world):
         offs.append(len(exp))
     assert res[0][1] == exp and res[0][2] == offs
     assert all(res[r][1] is None for r in range(1, world))
+
+
+def test_plan_chunks_uniform():
+    """pybic.parallel.plan_chunks: the same chunk count on every rank for any split of the units, the
+    chunks of a rank cover its units in order (8 planes over 3, 5, 6 or 7 ranks gave the ranks
+    different chunk counts, i.e. different numbers of collectives)"""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "binary-image-compression_amd"))
+    from pybic.parallel import plan_chunks
+    for total in (8, 64, 3):
+        for world in range(2, 10):
+            for chunks in (None, 1, 2, 3, 16):
+                plans = []
+                for r in range(world):
+                    n = (r + 1) * total // world - r * total // world
+                    p = plan_chunks(n, total, world, chunks)
+                    assert p[0][0] == 0 and p[-1][1] == n
+                    assert all(p[i][1] == p[i + 1][0] and p[i][0] <= p[i][1] for i in range(len(p) - 1))
+                    plans.append(p)
+                assert len({len(p) for p in plans}) == 1, (total, world, chunks, plans)
+
+
+def _uneven_worker(rank, world, port, q, total):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "binary-image-compression_amd"))
+    import torch.distributed as dist
+
+    from pybic.parallel import ChunkedGather, plan_chunks
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = rank * total // world, (rank + 1) * total // world  # bench.py C3Planes' split
+        cg = ChunkedGather(torch.device("cpu"), world, rank)
+        for a, b in plan_chunks(hi - lo, total, world):
+            # a chunk's packed words: unit u contributes 3 + u words valued 1000 u + i
+            words = [1000 * (lo + u) + i for u in range(a, b) for i in range(3 + lo + u)]
+            cg.add(torch.tensor(words + [7] * 5, dtype=torch.int64), len(words))
+        out, offs = cg.finish()
+        q.put((rank, None if out is None else out.tolist(), offs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [3, 5])
+def test_chunked_gather_uneven_units(world):
+    """8 planes over 3 or 5 ranks (2-3 / 1-2 planes per rank) through plan_chunks + ChunkedGather, as bench.py
+    c3 --shard planes runs them: no rank waits on a collective the others never post, and rank 0 ends with
+    every unit's words in unit order"""
+    total = 8
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_uneven_worker, args=(r, world, port, q, total)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = [1000 * u + i for u in range(total) for i in range(3 + u)]
+    assert res[0][1] == exp
+    assert all(res[r][1] is None for r in range(1, world))
