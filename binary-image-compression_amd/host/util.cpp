@@ -9,7 +9,7 @@
 void counting_sort(aux_t* s, idx_t n) {
   idx_t top = 0;
   for (idx_t i = 0; i < n; ++i) top = s[i].first > top ? s[i].first : top;
-  // start[v] = number of keys < v. As in util.cpp:114-123 the elements are dealt from the
+  // start[v] = number of keys < v. As in util.cpp:34-43 the elements are dealt from the
   // back of the input into increasing slots, so equal keys come out in REVERSE input order, and
   // both fields pass through int.
   std::vector<idx_t> start(top + 2, 0);
@@ -24,7 +24,7 @@ void counting_sort(aux_t* s, idx_t n) {
 }
 
 // Row li of D is a vectorised w x w patch, w = floor(sqrt(cols)); patches go on a grid of
-// gn columns and ceil(rows/gn) rows with a one-pixel gutter (util.cpp:133-162).
+// gn columns and ceil(rows/gn) rows with a one-pixel gutter (util.cpp:53-82).
 void render_mosaic(const binary_matrix& D, const char* fname) {
   const idx_t m = D.get_cols();
   const idx_t n = D.get_rows();

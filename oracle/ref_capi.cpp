@@ -2,12 +2,14 @@
 //
 // A thin extern "C" harness over the REFERENCE's own objects, compiled from the
 // read-only sources under /root/reference/src by oracle/Makefile into
-// oracle/_ref/libref.so (git-ignored; it travels to the GPU box only as the
-// prebuilt CPU baseline). No reference source is copied here: this file only
-// calls the reference's binary_matrix / med / GolombCoder / EGCoder / pbm / pnm.
+// oracle/_ref/libref.so (git-ignored; kept off the GPU box by .gpurunignore). No reference
+// source is copied here: this file only calls the reference's binary_matrix / med /
+// GolombCoder / EGCoder / pbm / pnm.
 //
 // Used (1) by tests/golden/make_golden.py to produce the golden vectors that pin
-// oracle/bic_oracle.c, and (2) by bench.py's cpu_baseline leg (kind "reference").
+// oracle/bic_oracle.c, (2) by the in-container cross-checks (tests/test_ref_crosscheck.py,
+// tests/test_dropin_compress.py) and (3) by bench.py's cpu_baseline leg where it is present
+// (kind "reference"; on the GPU box it is not, and the oracle port is timed).
 #include "binmat.h"
 #include "pbm.h"
 #include "pnm.h"

@@ -356,8 +356,8 @@ def match_encode_var(oracle, I, cols, W, T, R, enuml, variant, want_stream=True)
 
 class Ref:
     """The reference's own objects (oracle/_ref/libref.so): compiled in the build container from the
-    reference's sources (oracle/Makefile ref); the built library travels to the GPU box with the
-    tree (git-ignored, never committed), where bench.py times it as the CPU baseline. Test-side only."""
+    reference's sources (oracle/Makefile ref; git-ignored, never committed, and kept off the GPU box
+    by .gpurunignore). Test-side only."""
 
     def __init__(self, path=REF_SO):
         self.lib = L = C.CDLL(path)
