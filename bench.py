@@ -865,11 +865,13 @@ class C1(C3):
         return all((g.cpu().numpy().view(np.uint32)[:nt] == e[:nt]).all() for g, e in zip(self.res, exp))
 
     def cpu_time(self, rows):
-        """the oracle's restatement of the reference's search loop on the first `rows` rows,
-        extrapolated to the whole image by the exact count of visited windows"""
-        from oracle_lib import Oracle
+        """the search loop on the first `rows` rows, extrapolated to the whole image by the exact count of
+        visited windows: the reference's own loop over its binmat.cpp objects (ref_patch_search, kind
+        "reference") where oracle/_ref is built (this container), else the oracle's restatement of it
+        (kind "port": on the GPU box, where .gpurunignore keeps oracle/_ref out)"""
+        from oracle_lib import Oracle, Ref, have_ref
         P = np.ascontiguousarray(self.pybic.as_u64(self.planes[0])[:rows])
-        impl, kind = Oracle(), "port"
+        impl, kind = (Ref(), "reference") if have_ref() else (Oracle(), "port")
         t0 = time.perf_counter()
         impl.patch_search(P, self.cols, self.W)
         dt = time.perf_counter() - t0
