@@ -136,7 +136,10 @@ void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
     // (hipEventDisableSystemFence) the first encode of a process read stale prefix data on the
     // second stream (rows of the class kernels came out wrong; tools/dbg_egsrc8.py, 15 of 16 first
     // encodes), with the default fences none did
-    const unsigned fl = hipEventDisableTiming;
+#ifndef BIC_FORK_EVENT_FLAGS
+#define BIC_FORK_EVENT_FLAGS hipEventDisableTiming
+#endif
+    const unsigned fl = BIC_FORK_EVENT_FLAGS;
     if (hipEventCreateWithFlags(&a, fl) != hipSuccess || hipEventCreateWithFlags(&b, fl) != hipSuccess) {
       if (a) (void)hipEventDestroy(a);
       (void)hipStreamDestroy(st);

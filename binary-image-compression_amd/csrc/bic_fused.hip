@@ -21,6 +21,7 @@
 // Inter-workgroup records are 8-byte {flag, value} granules written and polled with
 // agent-scope atomics (cdna_hip_programming.md §6 Guideline 16, R2), spins bounded.
 #include "bic_device.h"
+#include "bic_k1pi.h"  // the k = 1 rows' backward-parity encoder (host-compilable: tests/cpp/k1pi_check.cpp)
 #include "bic_kstat.h"
 
 #include <algorithm>
@@ -846,18 +847,21 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
 
 // EG source: after every reader of the residual rows, the one bit per plane in which the uniform
 // layout differs from the EG stream (eg_src_junctions' ONES scan found it: the first 1's bit, or the
-// layout's bit past the end of a plane without 1s) is cleared.
-__device__ __forceinline__ void eg_fix_bit(const FusedArgs& a) {
-  if (!a.esrc || blockIdx.x != 0 || threadIdx.x >= a.g.nplanes) return;
-  const uint64_t P = a.efix[threadIdx.x];
-  uint64_t* w = a.out_e + (uint64_t)threadIdx.x * a.slot_e + (P >> 6);
+// layout's bit past the end of a plane without 1s) is cleared. The readers are the Golomb emission
+// (k_emit_k01 / k_emit_known, k_emit_rest) and k_rows_global's slow rows, so with the Golomb stream
+// requested the clear is k_fixup's (block 0, launched after k_rows_global); without it nothing reads
+// the rows and k_rows_global's one block does it.
+__device__ __forceinline__ void eg_fix_bit(const uint64_t* efix, uint64_t* out_e, uint64_t slot_e, uint32_t nplanes) {
+  if (!efix || blockIdx.x != 0 || threadIdx.x >= nplanes) return;
+  const uint64_t P = efix[threadIdx.x];
+  uint64_t* w = out_e + (uint64_t)threadIdx.x * slot_e + (P >> 6);
   *w &= ~bswap64(BIC_MSB >> (P & 63));
 }
 
 template <bool PREDICT>
 __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
   const int lane = lane_id();
-  eg_fix_bit(a);
+  if (!a.out_g) eg_fix_bit(a.esrc ? a.efix : nullptr, a.out_e, a.slot_e, a.g.nplanes);
   const uint32_t nslow = *a.slow_n;
   for (uint32_t li = blockIdx.x * 4 + (threadIdx.x >> 6); li < nslow; li += gridDim.x * 4)
     row_global<PREDICT>(a, a.slow_ids[li], lane);
@@ -1891,6 +1895,14 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
 }
 
+#ifndef BIC_DBG_CLS_VLOAD
+#define BIC_DBG_CLS_VLOAD 0
+#endif
+__device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) {
+  if constexpr (BIC_DBG_CLS_VLOAD) return __hip_atomic_load(a.cls + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return a.cls[i];
+}
+
 // k = 0: the row's Golomb bits are R then the end-of-row '1' (GolombCoder.cpp:13-34 with k = 0: each
 // sample's zeros and its '1'), i.e. the EG row ~R '1' (eg.cpp:20-37) with its first cols bits inverted.
 // Output word t of the row (at bit Gb) holds row bits [64 t - g, 64 t - g + 64), g = Gb % 64: the
@@ -1900,7 +1912,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
 #endif
 constexpr int kK0Batch = BIC_K0_BATCH;
 // the k = 0 list's entries i0, i0 + nw, ... (one wave; i0 and nw wave-uniform)
-template <int WPL>
+template <int WPL, int BATCH = kK0Batch>
 __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_t nw) {
   const Geom& g = a.g;
   const int lane = lane_id();
@@ -1919,9 +1931,9 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
   auto place = [&](uint32_t k) {
     const uint64_t e = i0 + (uint64_t)k * nw;
     Row r;
-    r.id = (uint32_t)a.cls[2 * e];
+    r.id = (uint32_t)cls_ld(a, 2 * e);
     const uint32_t plane = r.id / g.rows, row = r.id % g.rows;
-    const uint64_t Gs = a.cls[2 * e + 1];
+    const uint64_t Gs = cls_ld(a, 2 * e + 1);
     r.G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
     // stream bit of output word t's first bit: Bsrc - G % 64 + 64 t (>= -63: floor below)
     const int64_t s0 = (int64_t)((uint64_t)plane * a.slot_e * 64 + eg_src_bit0(g, row)) - (int64_t)(r.G & 63);
@@ -1972,18 +1984,18 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
       class_store(dst, whole ? bswap64(x) : x);
     }
   };
-  // rows in batches of kK0Batch: every row's loads issued before the first row's stores, so a wave
+  // rows in batches of BATCH: every row's loads issued before the first row's stores, so a wave
   // waits for its previous stores once per batch
-  for (uint32_t k = 0; k < R; k += kK0Batch) {
-    Row r[kK0Batch];
-    uint64_t v[kK0Batch][WPL + 1];
+  for (uint32_t k = 0; k < R; k += BATCH) {
+    Row r[BATCH];
+    uint64_t v[BATCH][WPL + 1];
 #pragma unroll
-    for (int u = 0; u < kK0Batch; ++u) {
+    for (int u = 0; u < BATCH; ++u) {
       r[u] = place(k + u < R ? k + u : k);
       load(r[u], v[u]);
     }
 #pragma unroll
-    for (int u = 0; u < kK0Batch; ++u)
+    for (int u = 0; u < BATCH; ++u)
       if (k + u < R) emit(r[u], v[u]);
   }
 }
@@ -2020,6 +2032,13 @@ __device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t 
 #ifndef BIC_K1_LC
 #define BIC_K1_LC 1  // lane l holds the row's words l WPL .. (one wave scan per row, not per word group)
 #endif
+#ifndef BIC_K1_PI
+#define BIC_K1_PI 1  // k = 1 rows by the backward parity (k1_pi, the [pi][byte] table); 0: encode_word_k1b
+#endif
+#if BIC_K1_PI && !BIC_K1_LC
+#error "BIC_K1_PI needs BIC_K1_LC"
+#endif
+constexpr uint32_t kK1Table = BIC_K1_PI ? 512u : 0u;  // the k = 1 rows' table in the u32 byte tables
 constexpr int kK1Batch = BIC_K1_BATCH;
 // the k = 1 list's entries i0, i0 + nw, ... (one wave, with its LDS row image and the byte table)
 template <int WPL>
@@ -2039,12 +2058,12 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
   auto place = [&](uint32_t k) {
     const uint64_t e = nrows + i0 + (uint64_t)k * nw;
     Row r;
-    const uint64_t e0 = a.cls[2 * e];
+    const uint64_t e0 = cls_ld(a, 2 * e);
     r.id = (uint32_t)e0;
     r.L = e0 >> 32;
     r.plane = r.id / g.rows;
     r.row = r.id % g.rows;
-    const uint64_t Gs = a.cls[2 * e + 1];
+    const uint64_t Gs = cls_ld(a, 2 * e + 1);
     r.G = a.off_g ? Gs - (uint64_t)r.plane * a.slot_g * 64 + a.gbase[r.plane] * 64 : Gs;
     return r;
   };
@@ -2062,6 +2081,71 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     uint64_t rr[WPL];
     eg_src_assemble_lc<WPL>(g, cur.row, v, rr);
     uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
+#if BIC_K1_PI
+    // the backward parity form (k1_pi): pi of each word's last column's right context (zeta) from the
+    // next word holding a 1 -- in this lane, or the nearest lane to the right holding one (one ballot,
+    // one bpermute); the row's first remainder bit from the first lane holding a 1
+    const uint32_t tail = g.cols & 63u;  // columns of the row's last word (0: a full word)
+    uint64_t xt[WPL], Zm[WPL];
+    bool any = false;
+    uint32_t lead = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)lane * WPL + t;
+      const uint64_t valid = w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
+      xt[t] = rr[t] | ((w == g.used - 1 && tail) ? (BIC_MSB >> tail) : 0ull);  // + the end-of-row 1
+      Zm[t] = ~xt[t] & valid;
+    }
+#pragma unroll
+    for (int t = WPL - 1; t >= 0; --t)
+      if (xt[t]) {
+        lead = (uint32_t)__builtin_clzll(xt[t]) & 1u;
+        any = true;
+      }
+    const uint64_t m1 = __ballot(any);
+    const uint64_t nm = m1 & ~((2ull << lane) - 1ull);  // the lanes right of this one holding a 1
+    const uint32_t ln = (uint32_t)__shfl((int)lead, nm ? (int)__builtin_ctzll(nm) : lane);
+    const uint32_t lf = (uint32_t)__shfl((int)lead, m1 ? (int)__builtin_ctzll(m1) : 0);
+    uint32_t zc = nm ? ln : 0u;  // (no 1 to the right: the end-of-row 1 follows the last word)
+    uint32_t zeta[WPL];
+#pragma unroll
+    for (int t = WPL - 1; t >= 0; --t) {
+      zeta[t] = zc;
+      if (xt[t]) zc = (uint32_t)__builtin_clzll(xt[t]) & 1u;
+    }
+    const uint32_t* T = s_lut;
+    uint64_t A[WPL], B[WPL];
+    uint32_t lw[WPL], lsum = 0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)lane * WPL + t;
+      const uint64_t Pi = k1_pi(xt[t], Zm[t], zeta[t]);
+      uint64_t hi = 0, lo = 0;
+      uint32_t L = 0;
+      if (w < g.used) {
+        if (w == g.used - 1 && tail) L = k1_word_last(rr[t], Pi, tail, hi, lo);
+        else L = k1_word_full(rr[t], Pi, T, hi, lo);
+      }
+      left128(hi, lo, L ? L : 128u, A[t], B[t]);
+      lw[t] = L;
+      lsum += L;
+    }
+    const uint32_t inc = wave_incl_sum_u32(lsum);
+    uint32_t off = 1u + inc - lsum;  // (bit 0: the first run's remainder)
+    const uint32_t tot = 1u + lane63_u32(inc) + (tail ? 0u : 1u);
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      place128_64(img, off, A[t], B[t], lw[t]);
+      off += lw[t];
+    }
+    if (lane == 0) {
+      if (lf && m1) lds_or64(img, 0, BIC_MSB);
+      if (!tail) lds_or64(img, (tot - 1) >> 6, BIC_MSB >> ((tot - 1) & 63));  // the end-of-row '1'
+      if (tot != cur.L) atomicOr(&a.flags[3], 1u);  // the closed-form length disagrees with the emission
+    }
+    write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, cur.L, cur.G, a.out_g, a.gfrag + 2 * (uint64_t)cur.id,
+                                                     a.sink);
+#else
     // the lane's words l WPL + t: their last 1s, the wave's exclusive max of the lanes' last 1
     int lastc[WPL], mxl = -1;
 #pragma unroll
@@ -2101,6 +2185,7 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     if (lane == 0 && loc != cur.L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
     write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, cur.L, cur.G, a.out_g, a.gfrag + 2 * (uint64_t)cur.id,
                                                      a.sink);
+#endif
   };
   auto load = [&](const Row& r, uint64_t (&v)[WPL + 1], uint64_t&) {
     eg_src_load_lc<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v);
@@ -2181,11 +2266,31 @@ __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
   // every wave writes the whole table itself (the same values as the others): its own reads then
   // follow its own writes, and the kernel needs no workgroup barrier
-  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
   const uint32_t nw = gridDim.x * 4;
   // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
   const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   k0_rows<WPL>(a, i0, nw);
+  k1_rows<WPL>(a, i0, nw, gimg, s_lut);
+}
+
+// The two classes as launches of their own (BIC_EMIT_SPLIT): the k = 0 copies one list entry per wave
+// (a grid over every row, the waves past the list's end exit: no persistence, few registers), the k = 1
+// rows persistent as in k_emit_k01.
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
+  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  k0_rows<WPL, 1>(a, i0, gridDim.x * 4);
+}
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
+  __shared__ uint32_t s_lut[512];
+  const int lane = lane_id();
+  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
+  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
+  const uint32_t nw = gridDim.x * 4;
+  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   k1_rows<WPL>(a, i0, nw, gimg, s_lut);
 }
 
@@ -2298,7 +2403,10 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
                                                const uint64_t* __restrict__ boff2, const uint64_t* __restrict__ len2,
                                                const uint64_t* __restrict__ frag2, uint64_t* __restrict__ out2,
                                                uint32_t rows, uint64_t nrows, uint32_t second,
-                                               const uint64_t* __restrict__ gbase = nullptr, uint64_t slot_bits = 0) {
+                                               const uint64_t* __restrict__ gbase = nullptr, uint64_t slot_bits = 0,
+                                               const uint64_t* __restrict__ efix = nullptr, uint64_t* eout = nullptr,
+                                               uint64_t eslot = 0, uint32_t enp = 0) {
+  eg_fix_bit(efix, eout, eslot, enp);  // (EG source: after every reader of the residual rows)
   // blocks [second, ...) serve the second stream (EG) when both streams are written
   if (blockIdx.x >= second) {
     boff = boff2;
@@ -2445,7 +2553,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
                                                         fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows,
                                                         dg && de ? fgrid : 0xffffffffu,
                                                         dg && mode == kEncStaged ? a.off_g ? fs.gbase : nullptr : nullptr,
-                                                        slot_g * 64);
+                                                        slot_g * 64, dg ? a.efix : nullptr, out_e, slot_e, g.nplanes);
     return;
   }
   const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
@@ -2508,11 +2616,39 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       if (wpl == 1) { BIC_EMIT1(1, false, true, false, true); } else if (wpl == 2) { BIC_EMIT1(2, false, true, false, true); }
       else { BIC_EMIT1(4, false, true, false, true); }
     } else if (es) {  // Golomb alone, the residual rows from the EG stream: one kernel per row class
+#ifndef BIC_DBG_NOREST
+#define BIC_DBG_NOREST 0
+#endif
+#ifndef BIC_DBG_JOIN_FIRST
+#define BIC_DBG_JOIN_FIRST 0
+#endif
+#ifndef BIC_EMIT_SPLIT
+#define BIC_EMIT_SPLIT 0
+#endif
 #define BIC_EMITC(W)                                                                                      \
   {                                                                                                    \
-    k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                    \
-    static const int o_ = occ_of(reinterpret_cast<const void*>(&k_emit_k01<W>));                      \
-    k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                     \
+    if (!BIC_DBG_NOREST) k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);               \
+    if (BIC_DBG_JOIN_FIRST && rs != s) {                                                               \
+      (void)hipEventRecord(fs.ev_join, rs);                                                            \
+      (void)hipStreamWaitEvent(s, fs.ev_join, 0);                                                      \
+    }                                                                                                  \
+    if (BIC_EMIT_SPLIT == 0) {                                                                         \
+      static const int o_ = occ_of(reinterpret_cast<const void*>(&k_emit_k01<W>));                    \
+      k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                   \
+    } else {                                                                                           \
+      static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1<W>));                    \
+      const uint32_t g0 = (uint32_t)((nrows + 3) / 4);                                                 \
+      if (BIC_EMIT_SPLIT == 1) {                                                                       \
+        k_emit_k0<W><<<g0, 256, 0, s>>>(a);                                                            \
+        k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                 \
+      } else if (BIC_EMIT_SPLIT == 2) {                                                                \
+        k_emit_k1<W><<<egrid_of(o1_), 256, 0, rs>>>(a);                                                \
+        k_emit_k0<W><<<g0, 256, 0, s>>>(a);                                                            \
+      } else {                                                                                         \
+        k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                 \
+        k_emit_k0<W><<<g0, 256, 0, s>>>(a);                                                            \
+      }                                                                                                \
+    }                                                                                                  \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
 #undef BIC_EMITC

@@ -13,6 +13,7 @@
 //   bitplanes (bitplane_tool.cpp:24-30)
 //   tile path (compress7_test.cpp:184-275 with R = 0)
 #include "bic_device.h"
+#include "bic_k1pi.h"
 #include "bic_kstat.h"
 
 namespace bic {
@@ -1931,6 +1932,7 @@ void build_byte_lut(uint64_t* lut) {
       else         // R up to 21 bits: R | lr << 21 | t << 26 | tz << 29
         lut32[(k - 1) * 256 + v] = (uint32_t)R | (lr << 21) | (t << 26) | (tz << 29);
     }
+  k1pi_build_table(lut32 + 512);  // k = 1 rows by the backward parity (bic_k1pi.h)
 }
 
 Geom make_geom(size_t rows, size_t cols, size_t wpr, int nplanes) {

@@ -1,0 +1,112 @@
+// k1pi_check.cpp -- TEST (CPU): the k = 1 rows' backward-parity encoder of bic_fused.hip k1_rows
+// (BIC_K1_PI), composed on the host exactly as the kernel composes it -- 64 lanes, lane l holding the
+// row's words l*WPL .. l*WPL + WPL - 1, the ballot / nearest-right-lane exchange for zeta, the wave scan
+// of the lanes' lengths, the words' 128-bit strings OR'd into a row image at their offsets -- over the
+// helpers of csrc/bic_k1pi.h that the kernel uses. Reads rows of residual words from stdin, writes each
+// row's bit string ('0'/'1' characters, one line per row): tests/test_k1pi_host.py compares them with
+// the oracle's Golomb rows whose codewords all have k = 1.
+//
+// stdin: cols nrows, then nrows * ceil(cols / 64) words (hex).
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#include "bic_k1pi.h"
+
+using namespace bic;
+
+constexpr uint64_t kMsb = 1ull << 63;
+
+static std::vector<int> encode_row(const std::vector<uint64_t>& row, uint32_t cols, const uint32_t* T) {
+  const uint32_t used = (cols + 63) / 64;
+  const int WPL = used <= 64 ? 1 : (used <= 128 ? 2 : 4);
+  const uint32_t tail = cols & 63u;
+  const uint64_t trail = ~0ull << (63 - (cols - 1) % 64);
+  // per lane state
+  std::vector<uint64_t> xt(64 * WPL), Zm(64 * WPL), rr(64 * WPL);
+  std::vector<uint32_t> lead(64, 0), anyl(64, 0);
+  for (int lane = 0; lane < 64; ++lane)
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)lane * WPL + t;
+      const uint64_t valid = w < used ? (w == used - 1 ? trail : ~0ull) : 0ull;
+      const uint64_t r = w < used ? row[w] & valid : 0ull;
+      rr[lane * WPL + t] = r;
+      xt[lane * WPL + t] = r | ((w == used - 1 && tail) ? (kMsb >> tail) : 0ull);
+      Zm[lane * WPL + t] = ~xt[lane * WPL + t] & valid;
+    }
+  for (int lane = 0; lane < 64; ++lane)
+    for (int t = WPL - 1; t >= 0; --t)
+      if (xt[lane * WPL + t]) {
+        lead[lane] = (uint32_t)__builtin_clzll(xt[lane * WPL + t]) & 1u;
+        anyl[lane] = 1;
+      }
+  uint64_t m1 = 0;
+  for (int lane = 0; lane < 64; ++lane) m1 |= (uint64_t)anyl[lane] << lane;
+  const uint32_t lf = m1 ? lead[__builtin_ctzll(m1)] : 0u;
+  std::vector<uint64_t> A(64 * WPL), B(64 * WPL);
+  std::vector<uint32_t> lw(64 * WPL), lsum(64, 0);
+  for (int lane = 0; lane < 64; ++lane) {
+    const uint64_t nm = m1 & ~((lane == 63 ? 0ull : (2ull << lane)) - 1ull);
+    uint32_t zc = nm ? lead[__builtin_ctzll(nm)] : 0u;
+    std::vector<uint32_t> zeta(WPL);
+    for (int t = WPL - 1; t >= 0; --t) {
+      zeta[t] = zc;
+      if (xt[lane * WPL + t]) zc = (uint32_t)__builtin_clzll(xt[lane * WPL + t]) & 1u;
+    }
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)lane * WPL + t;
+      const uint64_t Pi = k1_pi(xt[lane * WPL + t], Zm[lane * WPL + t], zeta[t]);
+      uint64_t hi = 0, lo = 0;
+      uint32_t L = 0;
+      if (w < used) {
+        if (w == used - 1 && tail) L = k1_word_last(rr[lane * WPL + t], Pi, tail, hi, lo);
+        else L = k1_word_full(rr[lane * WPL + t], Pi, T, hi, lo);
+      }
+      left128(hi, lo, L ? L : 128u, A[lane * WPL + t], B[lane * WPL + t]);
+      lw[lane * WPL + t] = L;
+      lsum[lane] += L;
+    }
+  }
+  uint32_t total = 1;
+  std::vector<uint32_t> lane_off(64);
+  for (int lane = 0; lane < 64; ++lane) {
+    lane_off[lane] = total;
+    total += lsum[lane];
+  }
+  if (!tail) ++total;
+  std::vector<int> bits(total, 0);
+  bits[0] = (int)(lf && m1);
+  for (int lane = 0; lane < 64; ++lane) {
+    uint32_t off = lane_off[lane];
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t L = lw[lane * WPL + t];
+      for (uint32_t i = 0; i < L; ++i) {
+        const uint64_t word = i < 64 ? A[lane * WPL + t] : B[lane * WPL + t];
+        bits[off + i] |= (int)((word >> (63 - (i & 63))) & 1u);
+      }
+      off += L;
+    }
+  }
+  if (!tail) bits[total - 1] = 1;
+  return bits;
+}
+
+int main() {
+  uint32_t T[512];
+  k1pi_build_table(T);
+  unsigned cols = 0, nrows = 0;
+  if (scanf("%u %u", &cols, &nrows) != 2) return 2;
+  const uint32_t used = (cols + 63) / 64;
+  std::vector<uint64_t> row(used);
+  for (unsigned r = 0; r < nrows; ++r) {
+    for (uint32_t w = 0; w < used; ++w) {
+      unsigned long long v = 0;
+      if (scanf("%llx", &v) != 1) return 3;
+      row[w] = v;
+    }
+    const std::vector<int> b = encode_row(row, cols, T);
+    for (int x : b) putchar('0' + x);
+    putchar('\n');
+  }
+  return 0;
+}

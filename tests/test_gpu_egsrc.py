@@ -64,6 +64,7 @@ def _check(ctx, oracle, g, img, nplanes, plane0, golomb, eg):
 @pytest.mark.parametrize("rows,cols,kind", [
     (70, 4096, "uniform"), (130, 4096, "smooth"), (66, 8192, "uniform"), (65, 12288, "smooth"),
     (64, 16384, "uniform"), (33, 16384, "smooth"), (90, 4096, "first_col0"), (40, 8192, "first_edge"),
+    (40, 16384, "first_edge"),
     (70, 4096, "constant"), (70, 8192, "sparse"), (1, 4096, "uniform"), (2, 16384, "smooth"),
 ])
 def test_eg_source(ctx, oracle, staged, rows, cols, kind):
@@ -72,6 +73,21 @@ def test_eg_source(ctx, oracle, staged, rows, cols, kind):
     for golomb, eg in ((True, True), (False, True), (True, False)):
         _check(ctx, oracle, g, img, 8, 0, golomb, eg)
     _check(ctx, oracle, g, img, 3, 4, True, True)
+
+
+@pytest.mark.parametrize("rows,cols", [(40, 16384), (24, 16384), (40, 12288)])
+def test_eg_source_first1_slow_row(ctx, oracle, staged, rows, cols):
+    """The row holding a plane's first residual 1 at column j1 > 0 whose Golomb image exceeds the LDS
+    window (a dense row after long zero runs: high k), so k_rows_global re-reads it from the EG slot.
+    The EG stream's one fixed bit per plane (at that row's layout bit of pixel j1 - 1) must be cleared
+    only after that read (it was cleared by k_rows_global's block 0 before its row loop).
+    One plane per call, so the first-1 row is the slow list's first entry, the one block 0's wave 0
+    takes."""
+    img = _img(oracle, rows * 7 + cols, rows, cols, "first_edge")
+    g = ctx.torch.from_numpy(img).to(ctx.dev)
+    for p in range(8):
+        _check(ctx, oracle, g, img, 1, p, True, True)
+    _check(ctx, oracle, g, img, 8, 0, True, True)
 
 
 def test_eg_source_matches_resid_path(ctx, oracle, staged):
