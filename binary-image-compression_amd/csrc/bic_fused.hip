@@ -2039,9 +2039,50 @@ __device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t 
 #error "BIC_K1_PI needs BIC_K1_LC"
 #endif
 constexpr uint32_t kK1Table = BIC_K1_PI ? 512u : 0u;  // the k = 1 rows' table in the u32 byte tables
+#ifndef BIC_CLASS_PLANES
+#define BIC_CLASS_PLANES 1
+#endif
+constexpr bool kClassPlanes = BIC_CLASS_PLANES != 0;  // class kernels for Golomb alone from planes (C4)
 constexpr int kK1Batch = BIC_K1_BATCH;
 // the k = 1 list's entries i0, i0 + nw, ... (one wave, with its LDS row image and the byte table)
+// residual words of a row from the planes (the med, pred.cpp:3-15) in the lane-consecutive layout of
+// eg_src_load_lc / eg_src_assemble_lc: lane l holds words l WPL .. l WPL + WPL - 1 (loads clamped into
+// the row, words past it zero)
 template <int WPL>
+__device__ __forceinline__ void row_load_lc(const uint64_t* planes, const Geom& g, uint32_t plane, uint32_t row,
+                                            uint64_t (&v)[2 * WPL]) {
+  const uint64_t* cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
+  const uint64_t* up = row ? cur - g.wpr : cur;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = (uint32_t)lane_id() * WPL + t;
+    const uint32_t wc = w < g.used ? w : g.used - 1;
+    v[t] = cur[wc];
+    v[WPL + t] = row ? up[wc] : 0ull;
+  }
+}
+template <int WPL>
+__device__ __forceinline__ void row_resid_lc(const Geom& g, uint32_t row, const uint64_t (&v)[2 * WPL],
+                                             uint64_t (&r)[WPL]) {
+  const int lane = lane_id();
+  uint64_t d[WPL];
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) d[t] = v[t] ^ v[WPL + t];
+  uint64_t dl = shfl_up_u64(d[WPL - 1], 1);  // the D word left of the lane's first (lane l - 1's last)
+  if (lane == 0) dl = 0;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = (uint32_t)lane * WPL + t;
+    uint64_t x = d[t] ^ ((d[t] >> 1) | ((t ? d[t - 1] : dl) << 63));
+    if (row == 0 && w == 0) x &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+    if (w == g.used - 1) x &= g.trail;
+    r[t] = w < g.used ? x : 0ull;
+  }
+}
+
+// PL: the residual rows formed from the planes (row_load_lc / row_resid_lc) instead of read back from
+// the EG stream
+template <int WPL, bool PL = false>
 __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_t nw, uint32_t* gimg,
                                         const uint32_t* s_lut) {
   const Geom& g = a.g;
@@ -2068,7 +2109,8 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     return r;
   };
 #if BIC_K1_LC
-  auto emit = [&](const Row& cur, const uint64_t (&v)[WPL + 1], uint64_t) {
+  constexpr int kV = PL ? 2 * WPL : WPL + 1;
+  auto emit = [&](const Row& cur, const uint64_t (&v)[kV], uint64_t) {
     if (cur.L > kCapBits) {  // k_rows_global writes the row
       if (lane == 0) {
         *reinterpret_cast<unsigned long long*>(a.gslow + cur.id) = a.row_o[cur.id] + cur.row + 1;
@@ -2079,7 +2121,8 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
     for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
     uint64_t rr[WPL];
-    eg_src_assemble_lc<WPL>(g, cur.row, v, rr);
+    if constexpr (PL) row_resid_lc<WPL>(g, cur.row, v, rr);
+    else eg_src_assemble_lc<WPL>(g, cur.row, v, rr);
     uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
 #if BIC_K1_PI
     // the backward parity form (k1_pi): pi of each word's last column's right context (zeta) from the
@@ -2187,10 +2230,10 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
                                                      a.sink);
 #endif
   };
-  auto load = [&](const Row& r, uint64_t (&v)[WPL + 1], uint64_t&) {
-    eg_src_load_lc<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v);
+  auto load = [&](const Row& r, uint64_t (&v)[kV], uint64_t&) {
+    if constexpr (PL) row_load_lc<WPL>(a.planes, g, r.plane, r.row, v);
+    else eg_src_load_lc<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v);
   };
-  constexpr int kV = WPL + 1;
 #else
   auto emit = [&](const Row& cur, const uint64_t (&v)[WPL], uint64_t last) {
     if (cur.L > kCapBits) {  // k_rows_global writes the row
@@ -2272,6 +2315,61 @@ __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   k0_rows<WPL>(a, i0, nw);
   k1_rows<WPL>(a, i0, nw, gimg, s_lut);
+}
+
+// The class kernels over residual rows formed from the planes (Golomb alone with prediction, the C4
+// path: bic_encode_planes*): k = 0 rows are the residual row R (the med of the plane rows, formed in
+// registers) then the end-of-row '1', placed at the row's Golomb offset -- one list entry per wave,
+// every lane owning the output words 64 k + lane (k <= WPL); k = 1 rows as k1_rows<WPL, true>.
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_k0p(FusedArgs a) {
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  const uint32_t e = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t n = __hip_atomic_load(a.counter + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (e >= n) return;
+  const uint32_t id = (uint32_t)cls_ld(a, 2 * (uint64_t)e);
+  const uint32_t plane = id / g.rows, row = id % g.rows;
+  const uint64_t Gs = cls_ld(a, 2 * (uint64_t)e + 1);
+  const uint64_t G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
+  uint64_t p[WPL], u[WPL], r[WPL];
+  row_load<WPL, true>(a.planes, g, plane, row, p, u);
+  row_resid<WPL, true>(g, row, p, u, r);
+  // the row's string S = R then '1' (the end-of-row codeword, column cols): words 64 k + lane
+  const uint32_t tail = g.cols & 63u, eolw = tail ? g.used - 1 : g.used;
+  uint64_t S[WPL + 1];
+#pragma unroll
+  for (int k = 0; k < WPL; ++k) S[k] = r[k];
+  S[WPL] = 0;
+#pragma unroll
+  for (int k = 0; k <= WPL; ++k)
+    if ((uint32_t)(64 * k + lane) == eolw) S[k] |= BIC_MSB >> tail;
+  const uint64_t L = (uint64_t)g.cols + 1;
+  const uint32_t gs = (uint32_t)(G & 63);
+  const uint64_t w0 = G >> 6, nwo = ((G + L - 1) >> 6) - w0 + 1;
+  const bool tail_whole = ((G + L) & 63) == 0;
+#pragma unroll
+  for (int k = 0; k <= WPL; ++k) {
+    const uint32_t t = 64 * k + lane;
+    uint64_t prev = shfl_up_u64(S[k], 1);
+    if (lane == 0) prev = k ? rl64(S[k ? k - 1 : 0], 63) : 0ull;
+    const uint64_t x = gs ? (prev << (64 - gs)) | (S[k] >> gs) : S[k];
+    const bool in = t < nwo;
+    const bool whole = in && (t != 0 || gs == 0) && (t != nwo - 1 || tail_whole);
+    uint64_t* dst = whole ? a.out_g + w0 + t : (in ? a.gfrag + 2 * (uint64_t)id + (t == 0 ? 0 : 1) : a.sink + lane);
+    class_store(dst, whole ? bswap64(x) : x);
+  }
+}
+template <int WPL>
+__global__ __launch_bounds__(256) void k_emit_k1p(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
+  __shared__ uint32_t s_lut[512];
+  const int lane = lane_id();
+  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
+  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
+  const uint32_t nw = gridDim.x * 4;
+  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  k1_rows<WPL, true>(a, i0, nw, gimg, s_lut);
 }
 
 // The two classes as launches of their own (BIC_EMIT_SPLIT): the k = 0 copies one list entry per wave
@@ -2530,7 +2628,10 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   const bool es = mode == kEncStaged && fs.eg_src && out_e && !a.off_e && !predict;
   a.esrc = es ? out_e : nullptr;
   a.efix = es ? fs.efix : nullptr;
-  a.cls = es && out_g && !fs.eg_src_one ? fs.cls : nullptr;
+  // the class kernels (the LEN scan lists the k = 0 and the k = 1 rows): the EG source; and Golomb alone
+  // from planes with prediction (BIC_CLASS_PLANES: k_emit_k0p / k_emit_k1p instead of k_emit_known)
+  const bool cpl = kClassPlanes && mode == kEncStaged && predict && out_g && !out_e && planes && !fs.eg_src_one;
+  a.cls = (es && out_g && !fs.eg_src_one) || cpl ? fs.cls : nullptr;
   a.sink = fs.sink;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
@@ -2610,7 +2711,18 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   }
 #define BIC_EMIT(W, P)                                                                                \
   if (dg && de) BIC_EMIT1(W, P, true, true, false) else if (dg) BIC_EMIT1(W, P, true, false, false) else BIC_EMIT1(W, P, false, true, false)
-    if (predict) {
+    if (cpl) {  // Golomb alone from planes: one kernel per row class (k_emit_rest takes the mixed rows)
+      const uint32_t g0 = (uint32_t)((nrows + 3) / 4);
+#define BIC_EMITP(W)                                                                                      \
+  {                                                                                                    \
+    k_emit_rest<true, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                     \
+    static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1p<W>));                     \
+    k_emit_k0p<W><<<g0, 256, 0, s>>>(a);                                                               \
+    k_emit_k1p<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                    \
+  }
+      if (wpl == 1) { BIC_EMITP(1); } else if (wpl == 2) { BIC_EMITP(2); } else { BIC_EMITP(4); }
+#undef BIC_EMITP
+    } else if (predict) {
       if (wpl == 1) { BIC_EMIT(1, true); } else if (wpl == 2) { BIC_EMIT(2, true); } else { BIC_EMIT(4, true); }
     } else if (es && !a.cls) {  // Golomb alone, the residual rows from the EG stream, one kernel
       if (wpl == 1) { BIC_EMIT1(1, false, true, false, true); } else if (wpl == 2) { BIC_EMIT1(2, false, true, false, true); }

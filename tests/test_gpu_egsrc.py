@@ -131,16 +131,45 @@ sys.exit(1 if bad else 0)
 """
 
 
+_FRESH_C3 = r"""
+import sys
+sys.path.insert(0, {pkg!r}); sys.path.insert(0, {tests!r})
+import numpy as np
+import pybic
+from oracle_lib import Oracle
+o = Oracle()
+rows = cols = 16384
+ctx = pybic.Context(0)
+t = ctx.torch
+gen = t.Generator(device=ctx.dev)
+gen.manual_seed(0x5EED0000)
+g = t.randint(0, 256, (rows, cols), dtype=t.uint8, device=ctx.dev, generator=gen)  # (bench.py's C3 input)
+_, (og, bg), (oe, be) = ctx.encode_gray(g, store_planes=False)  # the process's first encode: the bench's C3 call
+ctx.sync()
+P = o.bitplanes_par(g.cpu().numpy(), 8)
+exp = o.encode_planes_par(P, cols, 1)
+bad = []
+for k in range(8):
+    for coder, out, bits in ((0, og, bg), (1, oe, be)):
+        eb, est = exp[(k, coder)]
+        if int(pybic.as_u64(bits)[k]) != eb or pybic.stream_bytes(out[k], eb) != est.tobytes():
+            bad.append((k, coder))
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
 def test_first_encode_of_a_process():
-    """The first encode of a fresh process: with device-scope fork / join events on the second
-    stream it read stale prefix data (class-kernel rows wrong in 15 of 16 fresh processes on the
-    pool's boxes). Two fresh processes, each checked against the oracle."""
+    """The first encode of a fresh process: in round 4 (kernels of commit 67ba6e6, device-scope fork /
+    join events) class-kernel rows came out wrong in 15 of 16 fresh processes on the pool's boxes
+    (DESIGN.md §3). Two fresh processes at 70 x 4096, and one running exactly the bench's default C3 call
+    (16384^2 gray, planes not returned) as its first encode, each checked against the oracle."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = _FRESH.format(pkg=os.path.join(root, "binary-image-compression_amd"), tests=os.path.join(root, "tests"))
-    for _ in range(2):
+    kw = dict(pkg=os.path.join(root, "binary-image-compression_amd"), tests=os.path.join(root, "tests"))
+    for code in (_FRESH.format(**kw), _FRESH.format(**kw), _FRESH_C3.format(**kw)):
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 

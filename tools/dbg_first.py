@@ -62,9 +62,11 @@ for rep in range(reps):
                 continue
             # absolute stream words touched by the differences, and which of them still hold 0xaa
             words = sorted(set(((a + d) // 64).tolist()))
+            extra = int(np.sum(got[a:b] & ~ex[a:b] & 1))  # 1s the output has and the oracle's row has not
+            missing = int(np.sum(ex[a:b] & ~got[a:b] & 1))
             fill = [w for w in words if np.array_equal(got[w * 64:w * 64 + 64], pat)] if words else []
             bad.append(dict(plane=k, row=r, cls=cls[k][r], start=a, len=b - a, diffs=int(len(d)),
-                            first=int(d[0]), nwords=len(words), fill_words=len(fill),
+                            first=int(d[0]), nwords=len(words), fill_words=len(fill), extra=extra, missing=missing,
                             rel_words=[w - a // 64 for w in words][:12]))
     print(json.dumps(dict(lib=os.path.basename(pybic.LIB_PATH), rep=rep, rc=rc, classes=counts,
                           nbad=len(bad), bad_classes={c: sum(1 for x in bad if x["cls"] == c) for c in counts},
