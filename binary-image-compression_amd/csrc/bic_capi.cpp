@@ -132,12 +132,13 @@ void set_aux(bic_ctx* ctx, bic::FusedScratch& fs) {
     hipStream_t st = nullptr;
     hipEvent_t a = nullptr, b = nullptr;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
-    // the fork / join events keep HIP's default (system-scope) fences: with device-scope events
-    // (hipEventDisableSystemFence) the first encode of a process read stale prefix data on the
-    // second stream (rows of the class kernels came out wrong; tools/dbg_egsrc8.py, 15 of 16 first
-    // encodes), with the default fences none did
+    // device-scope fork / join events: they order two streams of this device, and a system-scope
+    // release would write back L2 at every fork (emission 167-170 vs 172-174 us, same box). Round 4 had
+    // switched them to system scope over a first-encode failure that the scope did not cause: that
+    // build's k_emit_k1 lost bits of k = 1 rows with either scope (6 of 6 fresh processes each), and
+    // only its LDS image zeroing decided it; these kernels measured 0 of 8 with either.
 #ifndef BIC_FORK_EVENT_FLAGS
-#define BIC_FORK_EVENT_FLAGS hipEventDisableTiming
+#define BIC_FORK_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
 #endif
     const unsigned fl = BIC_FORK_EVENT_FLAGS;
     if (hipEventCreateWithFlags(&a, fl) != hipSuccess || hipEventCreateWithFlags(&b, fl) != hipSuccess) {

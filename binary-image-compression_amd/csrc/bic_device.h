@@ -564,6 +564,18 @@ __device__ __forceinline__ uint64_t funnel64(uint64_t hi, uint64_t lo, uint32_t 
   return ((uint64_t)r1 << 32) | r0;
 }
 
+// Zero a wave's 32-bit LDS row image (n16 16-byte units) before codewords are OR'd into it with 4-byte
+// LDS atomics: the 16-byte zero stores are drained (s_waitcnt lgkmcnt(0)) before the first atomic issues.
+// Round 4's k_emit_k1 zeroed its image with 16-byte stores and OR'd 8-byte atomics into it with no such
+// wait; on the first encode of a process, with k_emit_rest's workgroups sharing the CUs, its k = 1 rows
+// lost about a quarter of their 1 bits. The 64-bit images now zero with 8-byte stores of
+// the atomics' own type (k1_rows, emit_known_row), the form that measured clean.
+__device__ __forceinline__ void lds_image_zero32(uint32_t* img, uint32_t n16) {
+  uint4* z = reinterpret_cast<uint4*>(img);
+  for (uint32_t i = lane_id(); i < n16; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // A row image of 64-bit LDS words (bit 64 i + b at significance 63 - b of word i), OR'd with
 // ds_or_b64: a lane's string (<= 128 bits at any offset) lands in at most three words.
 __device__ __forceinline__ void lds_or64(uint64_t* img, uint32_t i, uint64_t v) {

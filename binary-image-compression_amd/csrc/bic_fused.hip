@@ -49,6 +49,16 @@ constexpr int kGImg = 684;    // u32 words of Golomb row image per wave (21760 b
                               // the k = 1, 2 byte tables 4 workgroups (32 waves) fit one CU's LDS)
 constexpr int kEImg = 520;    // u32 words of EG row image per wave (cols <= 16384)
 constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads ahead)
+#ifndef BIC_K1_LC
+#define BIC_K1_LC 1  // lane l holds the row's words l WPL .. (one wave scan per row, not per word group)
+#endif
+#ifndef BIC_K1_PI
+#define BIC_K1_PI 1  // k = 1 rows by the backward parity (k1_pi, the [pi][byte] table); 0: encode_word_k1b
+#endif
+#if BIC_K1_PI && !BIC_K1_LC
+#error "BIC_K1_PI needs BIC_K1_LC"
+#endif
+constexpr uint32_t kK1Table = BIC_K1_PI ? 512u : 0u;  // the k = 1 rows' table in the u32 byte tables
 // One lane's codewords for one residual word.
 struct LaneEnc {
   uint32_t head, k0, z;  // first codeword: k0-bit binary part, then z unary zeros
@@ -901,10 +911,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   uint32_t ones = 0;
   int fcol = INT_MAX;
   if (valid) {
-    if constexpr (DO_G) {  // zero the Golomb image while the row loads are in flight
-      uint4* z = reinterpret_cast<uint4*>(gimg);
-      for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
-    }
+    if constexpr (DO_G) lds_image_zero32(gimg, kGImg / 4);  // the Golomb image (row loads in flight)
     uint64_t rr[WPL];
     resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
 #pragma unroll
@@ -1273,10 +1280,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
   const bool do_g = DO_G && a.glen[id] != 0 && a.gslow[id] == 0;
   const bool do_e = DO_E && a.elen[id] != 0;
   if (!do_g && !do_e) return;
-  if (do_g) {
-    uint4* z = reinterpret_cast<uint4*>(win);
-    for (int i = lane; i < kWin / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
-  }
+  if (do_g) lds_image_zero32(win, kWin / 4);
   uint64_t rr[WPL];
   resid_row<WPL, PREDICT>(a.planes, g, plane, row, rr);
   const uint32_t O = a.row_o[id];
@@ -1310,8 +1314,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       if (do_g) {
-        uint4* z = reinterpret_cast<uint4*>(win);
-        for (int i = lane; i < kWin / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+        lds_image_zero32(win, kWin / 4);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
       }
@@ -1710,9 +1713,9 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
   const uint64_t L = Lf & kLenMask;
   const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0, fits = L <= kCapBits;
   const bool gk1 = DO_G && L && k1 && fits;  // Golomb row through the LDS image (k = 1 byte tables)
-  if (gk1) {  // zero the Golomb image
-    uint4* z = reinterpret_cast<uint4*>(gimg);
-    for (int i = lane; i < kGImg / 4; i += 64) z[i] = make_uint4(0, 0, 0, 0);
+  if (gk1) {  // zero the Golomb image: 8-byte stores of its atomics' type (see lds_image_zero32)
+    unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
+    for (int i = lane; i < kGImg / 2; i += 64) z[i] = 0ull;
   }
   bool f_here = false;  // the plane's first 1 is in this row (k_emit_rest writes its EG row)
   if (DO_E && O == 0) {
@@ -1749,6 +1752,57 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
       eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.gfrag + 2 * id);
     } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
       uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
+#if BIC_K1_PI
+      // the backward parity (k1_pi) over words t * 64 + lane: zeta of a word from the next word of the
+      // row holding a 1 -- in its group t to the right (ballot, bpermute), else the first such word of a
+      // later group (uniform)
+      const uint32_t tail = g.cols & 63u;
+      uint64_t xt[WPL], Zm[WPL];
+      uint32_t lead[WPL];
+      uint64_t m1[WPL];
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        const uint32_t w = t * 64 + lane;
+        const uint64_t valid = w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
+        xt[t] = rr[t] | ((w == g.used - 1 && tail) ? (BIC_MSB >> tail) : 0ull);
+        Zm[t] = ~xt[t] & valid;
+        lead[t] = xt[t] ? (uint32_t)__builtin_clzll(xt[t]) & 1u : 0u;
+        m1[t] = __ballot(xt[t] != 0);
+      }
+      uint32_t carry = 0, first_r = 0;  // lead of the first word holding a 1 in the groups after t
+      uint32_t zeta[WPL];
+#pragma unroll
+      for (int t = WPL - 1; t >= 0; --t) {
+        const uint64_t nm = m1[t] & ~((2ull << lane) - 1ull);
+        const uint32_t ln = (uint32_t)__shfl((int)lead[t], nm ? (int)__builtin_ctzll(nm) : lane);
+        zeta[t] = nm ? ln : carry;
+        if (m1[t]) carry = (uint32_t)__builtin_amdgcn_readlane((int)lead[t], (int)__builtin_ctzll(m1[t]));
+      }
+      first_r = carry;  // (the lead of the row's first word holding a 1; 0: none)
+      const uint32_t* T = s_lut;
+      uint32_t loc = 1;  // bit 0: the first run's remainder
+#pragma unroll
+      for (int t = 0; t < WPL; ++t) {
+        if (t * 64 >= (int)g.used) break;
+        const uint32_t w = t * 64 + lane;
+        const uint64_t Pi = k1_pi(xt[t], Zm[t], zeta[t]);
+        uint64_t hi = 0, lo = 0, A, B;
+        uint32_t Lw = 0;
+        if (w < g.used) {
+          if (w == g.used - 1 && tail) Lw = k1_word_last(rr[t], Pi, tail, hi, lo);
+          else Lw = k1_word_full(rr[t], Pi, T, hi, lo);
+        }
+        left128(hi, lo, Lw ? Lw : 128u, A, B);
+        const uint32_t inc = wave_incl_sum_u32(Lw);
+        place128_64(img, loc + inc - Lw, A, B, Lw);
+        loc += lane63_u32(inc);
+      }
+      if (!tail) ++loc;  // the end-of-row '1' after the last word
+      if (lane == 0) {
+        if (first_r) lds_or64(img, 0, BIC_MSB);
+        if (!tail) lds_or64(img, (loc - 1) >> 6, BIC_MSB >> ((loc - 1) & 63));
+      }
+#else
       int jpc = -1;
       uint32_t loc = 0;
 #pragma unroll
@@ -1771,6 +1825,7 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
           ls.flush();
         }
       }
+#endif
       if (lane == 0 && loc != L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1800,7 +1855,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   const int wave = threadIdx.x >> 6;
   uint32_t* gimg = lds + wave * kGImg;
   if (DO_G)
-    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
   __syncthreads();  // the only workgroup barrier
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   // persistent waves: rows id, id + stride, ...
@@ -1895,13 +1950,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
 }
 
-#ifndef BIC_DBG_CLS_VLOAD
-#define BIC_DBG_CLS_VLOAD 0
-#endif
-__device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) {
-  if constexpr (BIC_DBG_CLS_VLOAD) return __hip_atomic_load(a.cls + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return a.cls[i];
-}
+__device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) { return a.cls[i]; }
 
 // k = 0: the row's Golomb bits are R then the end-of-row '1' (GolombCoder.cpp:13-34 with k = 0: each
 // sample's zeros and its '1'), i.e. the EG row ~R '1' (eg.cpp:20-37) with its first cols bits inverted.
@@ -1911,6 +1960,9 @@ __device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) {
 #define BIC_K0_BATCH 4
 #endif
 constexpr int kK0Batch = BIC_K0_BATCH;
+#ifndef BIC_K0_PLACE_AHEAD
+#define BIC_K0_PLACE_AHEAD 0
+#endif
 // the k = 0 list's entries i0, i0 + nw, ... (one wave; i0 and nw wave-uniform)
 template <int WPL, int BATCH = kK0Batch>
 __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_t nw) {
@@ -1986,6 +2038,27 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
   };
   // rows in batches of BATCH: every row's loads issued before the first row's stores, so a wave
   // waits for its previous stores once per batch
+#if BIC_K0_PLACE_AHEAD
+  // the next batch's list entries (scalar loads) are read while this batch is emitted, so a batch's
+  // source loads never wait behind its own list entries
+  Row rn[BATCH];
+#pragma unroll
+  for (int u = 0; u < BATCH; ++u) rn[u] = place((uint32_t)u < R ? (uint32_t)u : 0u);
+  for (uint32_t k = 0; k < R; k += BATCH) {
+    Row r[BATCH];
+    uint64_t v[BATCH][WPL + 1];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      r[u] = rn[u];
+      load(r[u], v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) rn[u] = place(k + BATCH + u < R ? k + BATCH + u : k);
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u)
+      if (k + u < R) emit(r[u], v[u]);
+  }
+#else
   for (uint32_t k = 0; k < R; k += BATCH) {
     Row r[BATCH];
     uint64_t v[BATCH][WPL + 1];
@@ -1998,6 +2071,7 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
     for (int u = 0; u < BATCH; ++u)
       if (k + u < R) emit(r[u], v[u]);
   }
+#endif
 }
 
 // write_row64 with a fixed number of store instructions (MAXT per lane, the idle lanes' to a.sink)
@@ -2029,60 +2103,9 @@ __device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t 
 #ifndef BIC_K1_BATCH
 #define BIC_K1_BATCH 3
 #endif
-#ifndef BIC_K1_LC
-#define BIC_K1_LC 1  // lane l holds the row's words l WPL .. (one wave scan per row, not per word group)
-#endif
-#ifndef BIC_K1_PI
-#define BIC_K1_PI 1  // k = 1 rows by the backward parity (k1_pi, the [pi][byte] table); 0: encode_word_k1b
-#endif
-#if BIC_K1_PI && !BIC_K1_LC
-#error "BIC_K1_PI needs BIC_K1_LC"
-#endif
-constexpr uint32_t kK1Table = BIC_K1_PI ? 512u : 0u;  // the k = 1 rows' table in the u32 byte tables
-#ifndef BIC_CLASS_PLANES
-#define BIC_CLASS_PLANES 1
-#endif
-constexpr bool kClassPlanes = BIC_CLASS_PLANES != 0;  // class kernels for Golomb alone from planes (C4)
 constexpr int kK1Batch = BIC_K1_BATCH;
 // the k = 1 list's entries i0, i0 + nw, ... (one wave, with its LDS row image and the byte table)
-// residual words of a row from the planes (the med, pred.cpp:3-15) in the lane-consecutive layout of
-// eg_src_load_lc / eg_src_assemble_lc: lane l holds words l WPL .. l WPL + WPL - 1 (loads clamped into
-// the row, words past it zero)
 template <int WPL>
-__device__ __forceinline__ void row_load_lc(const uint64_t* planes, const Geom& g, uint32_t plane, uint32_t row,
-                                            uint64_t (&v)[2 * WPL]) {
-  const uint64_t* cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
-  const uint64_t* up = row ? cur - g.wpr : cur;
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) {
-    const uint32_t w = (uint32_t)lane_id() * WPL + t;
-    const uint32_t wc = w < g.used ? w : g.used - 1;
-    v[t] = cur[wc];
-    v[WPL + t] = row ? up[wc] : 0ull;
-  }
-}
-template <int WPL>
-__device__ __forceinline__ void row_resid_lc(const Geom& g, uint32_t row, const uint64_t (&v)[2 * WPL],
-                                             uint64_t (&r)[WPL]) {
-  const int lane = lane_id();
-  uint64_t d[WPL];
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) d[t] = v[t] ^ v[WPL + t];
-  uint64_t dl = shfl_up_u64(d[WPL - 1], 1);  // the D word left of the lane's first (lane l - 1's last)
-  if (lane == 0) dl = 0;
-#pragma unroll
-  for (int t = 0; t < WPL; ++t) {
-    const uint32_t w = (uint32_t)lane * WPL + t;
-    uint64_t x = d[t] ^ ((d[t] >> 1) | ((t ? d[t - 1] : dl) << 63));
-    if (row == 0 && w == 0) x &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
-    if (w == g.used - 1) x &= g.trail;
-    r[t] = w < g.used ? x : 0ull;
-  }
-}
-
-// PL: the residual rows formed from the planes (row_load_lc / row_resid_lc) instead of read back from
-// the EG stream
-template <int WPL, bool PL = false>
 __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_t nw, uint32_t* gimg,
                                         const uint32_t* s_lut) {
   const Geom& g = a.g;
@@ -2109,7 +2132,7 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     return r;
   };
 #if BIC_K1_LC
-  constexpr int kV = PL ? 2 * WPL : WPL + 1;
+  constexpr int kV = WPL + 1;
   auto emit = [&](const Row& cur, const uint64_t (&v)[kV], uint64_t) {
     if (cur.L > kCapBits) {  // k_rows_global writes the row
       if (lane == 0) {
@@ -2121,8 +2144,7 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
     for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
     uint64_t rr[WPL];
-    if constexpr (PL) row_resid_lc<WPL>(g, cur.row, v, rr);
-    else eg_src_assemble_lc<WPL>(g, cur.row, v, rr);
+    eg_src_assemble_lc<WPL>(g, cur.row, v, rr);
     uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
 #if BIC_K1_PI
     // the backward parity form (k1_pi): pi of each word's last column's right context (zeta) from the
@@ -2231,8 +2253,7 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
 #endif
   };
   auto load = [&](const Row& r, uint64_t (&v)[kV], uint64_t&) {
-    if constexpr (PL) row_load_lc<WPL>(a.planes, g, r.plane, r.row, v);
-    else eg_src_load_lc<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v);
+    eg_src_load_lc<WPL>(a.esrc + (uint64_t)r.plane * a.slot_e, g, r.row, v);
   };
 #else
   auto emit = [&](const Row& cur, const uint64_t (&v)[WPL], uint64_t last) {
@@ -2314,81 +2335,6 @@ __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
   const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   k0_rows<WPL>(a, i0, nw);
-  k1_rows<WPL>(a, i0, nw, gimg, s_lut);
-}
-
-// The class kernels over residual rows formed from the planes (Golomb alone with prediction, the C4
-// path: bic_encode_planes*): k = 0 rows are the residual row R (the med of the plane rows, formed in
-// registers) then the end-of-row '1', placed at the row's Golomb offset -- one list entry per wave,
-// every lane owning the output words 64 k + lane (k <= WPL); k = 1 rows as k1_rows<WPL, true>.
-template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_k0p(FusedArgs a) {
-  const Geom& g = a.g;
-  const int lane = lane_id();
-  const uint32_t e = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t n = __hip_atomic_load(a.counter + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (e >= n) return;
-  const uint32_t id = (uint32_t)cls_ld(a, 2 * (uint64_t)e);
-  const uint32_t plane = id / g.rows, row = id % g.rows;
-  const uint64_t Gs = cls_ld(a, 2 * (uint64_t)e + 1);
-  const uint64_t G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
-  uint64_t p[WPL], u[WPL], r[WPL];
-  row_load<WPL, true>(a.planes, g, plane, row, p, u);
-  row_resid<WPL, true>(g, row, p, u, r);
-  // the row's string S = R then '1' (the end-of-row codeword, column cols): words 64 k + lane
-  const uint32_t tail = g.cols & 63u, eolw = tail ? g.used - 1 : g.used;
-  uint64_t S[WPL + 1];
-#pragma unroll
-  for (int k = 0; k < WPL; ++k) S[k] = r[k];
-  S[WPL] = 0;
-#pragma unroll
-  for (int k = 0; k <= WPL; ++k)
-    if ((uint32_t)(64 * k + lane) == eolw) S[k] |= BIC_MSB >> tail;
-  const uint64_t L = (uint64_t)g.cols + 1;
-  const uint32_t gs = (uint32_t)(G & 63);
-  const uint64_t w0 = G >> 6, nwo = ((G + L - 1) >> 6) - w0 + 1;
-  const bool tail_whole = ((G + L) & 63) == 0;
-#pragma unroll
-  for (int k = 0; k <= WPL; ++k) {
-    const uint32_t t = 64 * k + lane;
-    uint64_t prev = shfl_up_u64(S[k], 1);
-    if (lane == 0) prev = k ? rl64(S[k ? k - 1 : 0], 63) : 0ull;
-    const uint64_t x = gs ? (prev << (64 - gs)) | (S[k] >> gs) : S[k];
-    const bool in = t < nwo;
-    const bool whole = in && (t != 0 || gs == 0) && (t != nwo - 1 || tail_whole);
-    uint64_t* dst = whole ? a.out_g + w0 + t : (in ? a.gfrag + 2 * (uint64_t)id + (t == 0 ? 0 : 1) : a.sink + lane);
-    class_store(dst, whole ? bswap64(x) : x);
-  }
-}
-template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_k1p(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
-  __shared__ uint32_t s_lut[512];
-  const int lane = lane_id();
-  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
-  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
-  const uint32_t nw = gridDim.x * 4;
-  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  k1_rows<WPL, true>(a, i0, nw, gimg, s_lut);
-}
-
-// The two classes as launches of their own (BIC_EMIT_SPLIT): the k = 0 copies one list entry per wave
-// (a grid over every row, the waves past the list's end exit: no persistence, few registers), the k = 1
-// rows persistent as in k_emit_k01.
-template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_k0(FusedArgs a) {
-  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  k0_rows<WPL, 1>(a, i0, gridDim.x * 4);
-}
-template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_k1(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
-  __shared__ uint32_t s_lut[512];
-  const int lane = lane_id();
-  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
-  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
-  const uint32_t nw = gridDim.x * 4;
-  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   k1_rows<WPL>(a, i0, nw, gimg, s_lut);
 }
 
@@ -2628,10 +2574,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   const bool es = mode == kEncStaged && fs.eg_src && out_e && !a.off_e && !predict;
   a.esrc = es ? out_e : nullptr;
   a.efix = es ? fs.efix : nullptr;
-  // the class kernels (the LEN scan lists the k = 0 and the k = 1 rows): the EG source; and Golomb alone
-  // from planes with prediction (BIC_CLASS_PLANES: k_emit_k0p / k_emit_k1p instead of k_emit_known)
-  const bool cpl = kClassPlanes && mode == kEncStaged && predict && out_g && !out_e && planes && !fs.eg_src_one;
-  a.cls = (es && out_g && !fs.eg_src_one) || cpl ? fs.cls : nullptr;
+  a.cls = es && out_g && !fs.eg_src_one ? fs.cls : nullptr;
   a.sink = fs.sink;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
@@ -2711,56 +2654,17 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   }
 #define BIC_EMIT(W, P)                                                                                \
   if (dg && de) BIC_EMIT1(W, P, true, true, false) else if (dg) BIC_EMIT1(W, P, true, false, false) else BIC_EMIT1(W, P, false, true, false)
-    if (cpl) {  // Golomb alone from planes: one kernel per row class (k_emit_rest takes the mixed rows)
-      const uint32_t g0 = (uint32_t)((nrows + 3) / 4);
-#define BIC_EMITP(W)                                                                                      \
-  {                                                                                                    \
-    k_emit_rest<true, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                     \
-    static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1p<W>));                     \
-    k_emit_k0p<W><<<g0, 256, 0, s>>>(a);                                                               \
-    k_emit_k1p<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                    \
-  }
-      if (wpl == 1) { BIC_EMITP(1); } else if (wpl == 2) { BIC_EMITP(2); } else { BIC_EMITP(4); }
-#undef BIC_EMITP
-    } else if (predict) {
+    if (predict) {
       if (wpl == 1) { BIC_EMIT(1, true); } else if (wpl == 2) { BIC_EMIT(2, true); } else { BIC_EMIT(4, true); }
     } else if (es && !a.cls) {  // Golomb alone, the residual rows from the EG stream, one kernel
       if (wpl == 1) { BIC_EMIT1(1, false, true, false, true); } else if (wpl == 2) { BIC_EMIT1(2, false, true, false, true); }
       else { BIC_EMIT1(4, false, true, false, true); }
     } else if (es) {  // Golomb alone, the residual rows from the EG stream: one kernel per row class
-#ifndef BIC_DBG_NOREST
-#define BIC_DBG_NOREST 0
-#endif
-#ifndef BIC_DBG_JOIN_FIRST
-#define BIC_DBG_JOIN_FIRST 0
-#endif
-#ifndef BIC_EMIT_SPLIT
-#define BIC_EMIT_SPLIT 0
-#endif
 #define BIC_EMITC(W)                                                                                      \
   {                                                                                                    \
-    if (!BIC_DBG_NOREST) k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);               \
-    if (BIC_DBG_JOIN_FIRST && rs != s) {                                                               \
-      (void)hipEventRecord(fs.ev_join, rs);                                                            \
-      (void)hipStreamWaitEvent(s, fs.ev_join, 0);                                                      \
-    }                                                                                                  \
-    if (BIC_EMIT_SPLIT == 0) {                                                                         \
-      static const int o_ = occ_of(reinterpret_cast<const void*>(&k_emit_k01<W>));                    \
-      k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                   \
-    } else {                                                                                           \
-      static const int o1_ = occ_of(reinterpret_cast<const void*>(&k_emit_k1<W>));                    \
-      const uint32_t g0 = (uint32_t)((nrows + 3) / 4);                                                 \
-      if (BIC_EMIT_SPLIT == 1) {                                                                       \
-        k_emit_k0<W><<<g0, 256, 0, s>>>(a);                                                            \
-        k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                 \
-      } else if (BIC_EMIT_SPLIT == 2) {                                                                \
-        k_emit_k1<W><<<egrid_of(o1_), 256, 0, rs>>>(a);                                                \
-        k_emit_k0<W><<<g0, 256, 0, s>>>(a);                                                            \
-      } else {                                                                                         \
-        k_emit_k1<W><<<egrid_of(o1_), 256, 0, s>>>(a);                                                 \
-        k_emit_k0<W><<<g0, 256, 0, s>>>(a);                                                            \
-      }                                                                                                \
-    }                                                                                                  \
+    k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                    \
+    static const int o_ = occ_of(reinterpret_cast<const void*>(&k_emit_k01<W>));                      \
+    k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                     \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
 #undef BIC_EMITC

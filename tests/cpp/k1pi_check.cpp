@@ -17,6 +17,53 @@ using namespace bic;
 
 constexpr uint64_t kMsb = 1ull << 63;
 
+// the strided layout of k_emit_known (emit_known_row): lane l holds words t * 64 + l
+static std::vector<int> encode_row_strided(const std::vector<uint64_t>& row, uint32_t cols, const uint32_t* T) {
+  const uint32_t used = (cols + 63) / 64;
+  const int WPL = used <= 64 ? 1 : (used <= 128 ? 2 : 4);
+  const uint32_t tail = cols & 63u;
+  const uint64_t trail = ~0ull << (63 - (cols - 1) % 64);
+  std::vector<uint64_t> xt(64 * WPL), Zm(64 * WPL), rr(64 * WPL);
+  std::vector<uint32_t> lead(64 * WPL, 0);
+  std::vector<uint64_t> m1(WPL, 0);
+  for (int t = 0; t < WPL; ++t)
+    for (int lane = 0; lane < 64; ++lane) {
+      const uint32_t w = t * 64 + lane;
+      const uint64_t valid = w < used ? (w == used - 1 ? trail : ~0ull) : 0ull;
+      const uint64_t r = w < used ? row[w] & valid : 0ull;
+      const int i = t * 64 + lane;
+      rr[i] = r;
+      xt[i] = r | ((w == used - 1 && tail) ? (kMsb >> tail) : 0ull);
+      Zm[i] = ~xt[i] & valid;
+      lead[i] = xt[i] ? (uint32_t)__builtin_clzll(xt[i]) & 1u : 0u;
+      if (xt[i]) m1[t] |= 1ull << lane;
+    }
+  std::vector<uint32_t> zeta(64 * WPL);
+  uint32_t carry = 0;
+  for (int t = WPL - 1; t >= 0; --t) {
+    for (int lane = 0; lane < 64; ++lane) {
+      const uint64_t nm = m1[t] & ~((lane == 63 ? 0ull : (2ull << lane)) - 1ull);
+      zeta[t * 64 + lane] = nm ? lead[t * 64 + __builtin_ctzll(nm)] : carry;
+    }
+    if (m1[t]) carry = lead[t * 64 + __builtin_ctzll(m1[t])];
+  }
+  const uint32_t first_r = carry;
+  std::vector<int> bits(1, (int)first_r);
+  for (int t = 0; t < WPL; ++t)
+    for (int lane = 0; lane < 64; ++lane) {
+      const uint32_t w = t * 64 + lane;
+      if (w >= used) continue;
+      const int i = t * 64 + lane;
+      const uint64_t Pi = k1_pi(xt[i], Zm[i], zeta[i]);
+      uint64_t hi = 0, lo = 0, A, B;
+      const uint32_t L = (w == used - 1 && tail) ? k1_word_last(rr[i], Pi, tail, hi, lo) : k1_word_full(rr[i], Pi, T, hi, lo);
+      left128(hi, lo, L ? L : 128u, A, B);
+      for (uint32_t b = 0; b < L; ++b) bits.push_back((int)(((b < 64 ? A : B) >> (63 - (b & 63))) & 1u));
+    }
+  if (!tail) bits.push_back(1);
+  return bits;
+}
+
 static std::vector<int> encode_row(const std::vector<uint64_t>& row, uint32_t cols, const uint32_t* T) {
   const uint32_t used = (cols + 63) / 64;
   const int WPL = used <= 64 ? 1 : (used <= 128 ? 2 : 4);
@@ -91,7 +138,8 @@ static std::vector<int> encode_row(const std::vector<uint64_t>& row, uint32_t co
   return bits;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool strided = argc > 1 && argv[1][0] == 's';
   uint32_t T[512];
   k1pi_build_table(T);
   unsigned cols = 0, nrows = 0;
@@ -104,7 +152,7 @@ int main() {
       if (scanf("%llx", &v) != 1) return 3;
       row[w] = v;
     }
-    const std::vector<int> b = encode_row(row, cols, T);
+    const std::vector<int> b = strided ? encode_row_strided(row, cols, T) : encode_row(row, cols, T);
     for (int x : b) putchar('0' + x);
     putchar('\n');
   }

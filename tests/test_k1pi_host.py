@@ -31,8 +31,11 @@ def _plane(rng, rows, cols, p):
     return np.packbits(bits, axis=1).view(">u8").astype(np.uint64).reshape(rows, wpr)
 
 
+@pytest.mark.parametrize("layout", ["lanes", "strided"])
 @pytest.mark.parametrize("cols", [4096, 16384, 8192, 4000, 1000, 130, 70, 64, 16383])
-def test_k1_rows_match_oracle(prog, cols):
+def test_k1_rows_match_oracle(prog, cols, layout):
+    """layout "lanes": k1_rows (lane l holds words l WPL ..); "strided": k_emit_known's emit_known_row
+    (lane l holds words t * 64 + l)"""
     o = Oracle()
     rng = np.random.default_rng(cols)
     rows = 240 if cols <= 8192 else 96
@@ -52,7 +55,7 @@ def test_k1_rows_match_oracle(prog, cols):
     k1 = [r for r in range(rows) if kmin[r] == 1 and kmax[r] == 1]
     assert k1, "the input has no all-k = 1 row"
     inp = f"{cols} {len(k1)}\n" + "\n".join(" ".join(f"{int(w):x}" for w in R[r]) for r in k1) + "\n"
-    p = subprocess.run([prog], input=inp, capture_output=True, text=True, check=True)
+    p = subprocess.run([prog, layout[0]], input=inp, capture_output=True, text=True, check=True)
     got = p.stdout.split("\n")
     for i, r in enumerate(k1):
         exp = "".join(map(str, bits[offs[r]:offs[r + 1]]))

@@ -35,6 +35,8 @@ for k in range(8):
     cls.append(c)
 ctx = pybic.Context(0)
 ctx.set_encoder("staged")
+if os.environ.get("DBG_ONE_STREAM") == "1":  # the class kernels and k_emit_rest one after the other on one stream
+    ctx.set_one_stream(True)
 g = ctx.torch.from_numpy(img).to(ctx.dev)
 slot = ctx.slot_words(rows, cols, pybic.CODER_GOLOMB)
 og = ctx.empty_i64(8, slot)

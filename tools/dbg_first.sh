@@ -1,10 +1,10 @@
 #!/bin/bash
 # tools/dbg_first.sh N VAR...: N fresh processes per variant library lib/var_VAR.so ("default" =
 # lib/libbic.so), each one first encode through tools/dbg_first.py; one JSON line per encode into
-# gpurun_out/dbg_first.jsonl
+# gpurun_out/dbg_first$DBG_TAG.jsonl (DBG_ONE_STREAM=1: one stream)
 set -o pipefail
 N=$1; shift
-out=gpurun_out/dbg_first.jsonl
+out=gpurun_out/dbg_first${DBG_TAG}.jsonl
 : > $out
 for v in "$@"; do
   lib=binary-image-compression_amd/lib/var_$v.so
