@@ -38,9 +38,20 @@ __device__ unsigned long long g_known[2][1 << 17];
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
     if (lane == 0 && (uint64_t)id * 8 + (slot) < (1u << 21)) g_stamps[(uint64_t)id * 8 + (slot)] = t_; \
   } while (0)
+// k_row_walk's phases (slots 4-7 of the row: entry, residual word loaded, length walked, stored), on
+// the 100 MHz clock every XCD shares (s_memrealtime), waiting for the phase's loads first
+#define WSTAMP(slot)                                                                               \
+  do {                                                                                             \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
+    if (threadIdx.x == 0 && (uint64_t)id * 8 + (slot) < (1u << 21)) g_stamps[(uint64_t)id * 8 + (slot)] = t_; \
+  } while (0)
 #else
 #define STAMP(slot) \
   do {              \
+  } while (0)
+#define WSTAMP(slot) \
+  do {               \
   } while (0)
 #endif
 
@@ -59,6 +70,16 @@ constexpr int kPad = 4;       // zeroed words after an image's end (get64 reads 
 #error "BIC_K1_PI needs BIC_K1_LC"
 #endif
 constexpr uint32_t kK1Table = BIC_K1_PI ? 512u : 0u;  // the k = 1 rows' table in the u32 byte tables
+#ifndef BIC_KNOWN_PI
+// k_emit_known's k = 1 rows (C4, C2, predict): 1 the backward parity, 0 encode_word_k1b (C4 0.268 ms
+// against 0.283 with the parity's strided lanes)
+#define BIC_KNOWN_PI 0
+#endif
+constexpr uint32_t kKnownTable = BIC_KNOWN_PI ? 512u : 0u;
+#ifndef BIC_SLOW_REST
+#define BIC_SLOW_REST 1  // class kernels' path: the slow rows by k_emit_rest (listed by the LEN scan), no k_rows_global
+#endif
+constexpr bool kSlowRest = BIC_SLOW_REST != 0;
 // One lane's codewords for one residual word.
 struct LaneEnc {
   uint32_t head, k0, z;  // first codeword: k0-bit binary part, then z unary zeros
@@ -858,9 +879,9 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
 // EG source: after every reader of the residual rows, the one bit per plane in which the uniform
 // layout differs from the EG stream (eg_src_junctions' ONES scan found it: the first 1's bit, or the
 // layout's bit past the end of a plane without 1s) is cleared. The readers are the Golomb emission
-// (k_emit_k01 / k_emit_known, k_emit_rest) and k_rows_global's slow rows, so with the Golomb stream
-// requested the clear is k_fixup's (block 0, launched after k_rows_global); without it nothing reads
-// the rows and k_rows_global's one block does it.
+// (k_emit_k01 / k_emit_known, k_emit_rest) and the slow rows (k_rows_global, or k_emit_rest's own
+// loop on the class kernels' path), so with the Golomb stream requested the clear is k_fixup's (block
+// 0, launched after both); without it nothing reads the rows and k_rows_global's one block does it.
 __device__ __forceinline__ void eg_fix_bit(const uint64_t* efix, uint64_t* out_e, uint64_t slot_e, uint32_t nplanes) {
   if (!efix || blockIdx.x != 0 || threadIdx.x >= nplanes) return;
   const uint64_t P = efix[threadIdx.x];
@@ -1455,13 +1476,22 @@ __device__ __forceinline__ void plane_bases(const FusedArgs& a, uint64_t* tmp) {
 // bits_g[] the plane's total; rows past the slot's end get glen = 0 and raise the overflow flag
 // (a later chunk may then sum a zeroed length: its offsets stay inside the slot, and the call
 // reports BIC_ENOSPC with the stream undefined).
+#ifndef BIC_LEN_REV
+#define BIC_LEN_REV 0
+#endif
+constexpr bool kLenRev = BIC_LEN_REV != 0;
 constexpr uint32_t kScanPer = 1, kScanChunk = 1024 * kScanPer;  // (1024-row chunks: twice the workgroups of 2048, C3 prefix 51 -> 42 us)
 template <bool ONES, bool CLASSIFY>
 __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
   __shared__ uint64_t tmp[17];
   const Geom& g = a.g;
   const uint32_t nb = (g.rows + kScanChunk - 1) / kScanChunk;
-  const uint32_t plane = blockIdx.x / nb, b = blockIdx.x % nb;
+  // (BIC_LEN_REV, the LEN scan: chunks dealt bottom row chunk first, planes interleaved, so the class
+  // lists -- appended in about this order -- lead with the rows the count pass wrote last, the part of
+  // the EG stream the Infinity Cache may still hold when the emission reads it)
+  const bool rev = kLenRev && !ONES;
+  const uint32_t plane = rev ? blockIdx.x % g.nplanes : blockIdx.x / nb;
+  const uint32_t b = rev ? nb - 1 - blockIdx.x / g.nplanes : blockIdx.x % nb;
   const uint64_t base = (uint64_t)plane * g.rows;
   auto val = [&](uint32_t r) -> uint64_t {
     if constexpr (ONES) {
@@ -1564,10 +1594,12 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       const uint32_t r = r0;
       const uint64_t f = r < g.rows ? a.glen[base + r] : 0;
       const bool ok = pre + v[0] <= cap && v[0] != 0;  // (an overflowing row is written by nobody)
-      const uint32_t c0 = ok && (f & kK0Row) ? 1u : 0u, c1 = ok && (f & kK1Row) ? 1u : 0u;
-      // a mixed row too long for k_emit_rest's LDS image goes to k_rows_global (k_emit_k1 lists its own)
+      // a k = 1 or mixed row too long for an LDS row image is written by k_emit_rest's slow-row loop
+      // (row_global; k = 0 rows are shifted copies, no image): the list is complete before the emission
       constexpr uint32_t kCapBitsRest = (kGImg - kPad) * 32;
-      if (ok && !(f & (kK0Row | kK1Row)) && v[0] > kCapBitsRest) {
+      const bool big = v[0] > kCapBitsRest;
+      const uint32_t c0 = ok && (f & kK0Row) ? 1u : 0u, c1 = ok && (f & kK1Row) && (!big || !kSlowRest) ? 1u : 0u;
+      if (ok && !(f & kK0Row) && big && (kSlowRest || !(f & kK1Row))) {
         a.gslow[base + r] = a.row_o[base + r] + r + 1;
         a.slow_ids[atomicAdd(a.slow_n, 1u)] = base + r;
       }
@@ -1657,15 +1689,18 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
   const uint32_t nlist = __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
     const uint64_t id = a.walk_ids[i];
+    WSTAMP(4);
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     const uint32_t O = a.row_o[id];
     uint64_t rr[1];
     if (!PREDICT && a.esrc) rr[0] = eg_src_word(a.esrc + (uint64_t)plane * a.slot_e, g, row, w);
     else resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
+    WSTAMP(5);
     const WideRow p = wide_prefix(rr[0], w, O + row, sh);
     uint32_t kor = 0;
     uint32_t ll = word_len(rr[0], w, p.n, p.jp, row * (g.cols + 1), w == g.used - 1, g.cols, kor);
     ll = wave_sum_u32(ll);
+    WSTAMP(6);
     const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);  // some k != 0 / some k != 1
     if (lane == 0) {
       sl[v] = ll;
@@ -1683,6 +1718,7 @@ __global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
       // would serialise this kernel)
       a.glen[id] = L | (!(kk & 1u) ? kK0Row : (!(kk & 2u) ? kK1Row : 0));
     }
+    WSTAMP(7);
     __syncthreads();
   }
 }
@@ -1752,7 +1788,7 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
       eg_row_regs<WPL, false>(rr, g, Gb, L, a.out_g, a.gfrag + 2 * id);
     } else if (gk1) {  // every codeword k = 1: branch-free byte-table words into a 64-bit LDS image
       uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
-#if BIC_K1_PI
+#if BIC_KNOWN_PI
       // the backward parity (k1_pi) over words t * 64 + lane: zeta of a word from the next word of the
       // row holding a 1 -- in its group t to the right (ballot, bpermute), else the first such word of a
       // later group (uniform)
@@ -1855,7 +1891,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   const int wave = threadIdx.x >> 6;
   uint32_t* gimg = lds + wave * kGImg;
   if (DO_G)
-    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kKnownTable + i];
   __syncthreads();  // the only workgroup barrier
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   // persistent waves: rows id, id + stride, ...
@@ -2134,10 +2170,14 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
 #if BIC_K1_LC
   constexpr int kV = WPL + 1;
   auto emit = [&](const Row& cur, const uint64_t (&v)[kV], uint64_t) {
-    if (cur.L > kCapBits) {  // k_rows_global writes the row
+    if (cur.L > kCapBits) {  // (the LEN scan lists such rows as slow, never here: a length disagreement)
       if (lane == 0) {
-        *reinterpret_cast<unsigned long long*>(a.gslow + cur.id) = a.row_o[cur.id] + cur.row + 1;
-        *reinterpret_cast<unsigned long long*>(a.slow_ids + atomicAdd(a.slow_n, 1u)) = cur.id;
+        if (kSlowRest) {
+          atomicOr(&a.flags[3], 1u);
+        } else {
+          *reinterpret_cast<unsigned long long*>(a.gslow + cur.id) = a.row_o[cur.id] + cur.row + 1;
+          *reinterpret_cast<unsigned long long*>(a.slow_ids + atomicAdd(a.slow_n, 1u)) = cur.id;
+        }
       }
       return;
     }
@@ -2257,10 +2297,14 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
   };
 #else
   auto emit = [&](const Row& cur, const uint64_t (&v)[WPL], uint64_t last) {
-    if (cur.L > kCapBits) {  // k_rows_global writes the row
+    if (cur.L > kCapBits) {  // (the LEN scan lists such rows as slow, never here: a length disagreement)
       if (lane == 0) {
-        *reinterpret_cast<unsigned long long*>(a.gslow + cur.id) = a.row_o[cur.id] + cur.row + 1;
-        *reinterpret_cast<unsigned long long*>(a.slow_ids + atomicAdd(a.slow_n, 1u)) = cur.id;
+        if (kSlowRest) {
+          atomicOr(&a.flags[3], 1u);
+        } else {
+          *reinterpret_cast<unsigned long long*>(a.gslow + cur.id) = a.row_o[cur.id] + cur.row + 1;
+          *reinterpret_cast<unsigned long long*>(a.slow_ids + atomicAdd(a.slow_n, 1u)) = cur.id;
+        }
       }
       return;
     }
@@ -2433,6 +2477,12 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
     }
     __syncthreads();  // the images and sh are reused by the next row
   }
+  // the class kernels' path (a.cls): the LEN scan listed every row too long for an LDS image, so the
+  // slow rows are written here, one wave per row, overlapping the class kernels (no k_rows_global)
+  if (DO_G && !PREDICT && kSlowRest && a.cls) {
+    const uint32_t nslow = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t li = blockIdx.x * nw + v; li < nslow; li += gridDim.x * nw) row_global<false>(a, a.slow_ids[li], lane);
+  }
 }
 
 __global__ __launch_bounds__(1024) void k_plane_bases(FusedArgs a) {
@@ -2587,7 +2637,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   if (stage == kFusedFinish) {
     // a fixed small grid walks the list of LDS-overflow rows (usually empty); block 0 also clears
     // the EG source's one bit per plane (eg_fix_bit)
-    if (dg || es) {
+    if ((dg && (!a.cls || !kSlowRest)) || (!dg && es)) {  // (a.cls: k_emit_rest wrote the slow rows)
       if (predict) k_rows_global<true><<<dg ? 256 : 1, 256, 0, s>>>(a);
       else k_rows_global<false><<<dg ? 256 : 1, 256, 0, s>>>(a);
     }

@@ -1,0 +1,46 @@
+"""Phase clocks of k_row_walk (diagnostic build lib/libbic_stamps.so, make stamps): one C3 encode_gray
+(the bench's default call), then per walked row its entry, residual-word, walked and stored times on
+the shared 100 MHz clock (slots 4-7 of bic_fused.hip WSTAMP). Prints the walk's span, the rows'
+phase durations and how the rows' start times spread over the span."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["BIC_LIB_PATH"] = os.path.join(ROOT, "binary-image-compression_amd", "lib", "libbic_stamps.so")
+sys.path.insert(0, os.path.join(ROOT, "binary-image-compression_amd"))
+import pybic  # noqa: E402
+
+rows = cols = 16384
+ctx = pybic.Context(0)
+t = ctx.torch
+g = t.Generator(device=ctx.dev)
+g.manual_seed(0x5EED0000)
+gray = t.randint(0, 256, (rows, cols), dtype=t.uint8, device=ctx.dev, generator=g)
+lib = pybic.load()
+lib.bic_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
+n = rows * 8 * 8
+out = {}
+for rep in range(3):
+    ctx.encode_gray(gray, store_planes=False)
+    ctx.sync()
+    buf = np.zeros(n, np.uint64)
+    assert lib.bic_debug_stamps(buf.ctypes.data, n) == 0
+    S = buf.reshape(-1, 8).astype(np.int64)[:, 4:8]
+    ok = (S[:, 0] > 0) & (S[:, 3] >= S[:, 0])
+    if rep == 0:
+        first = S[:, 0].copy()
+    else:  # rows stamped by this call only (the array keeps older values)
+        ok &= S[:, 0] != first
+        first = S[:, 0].copy()
+    W = S[ok]
+    t0 = W[:, 0].min()
+    d = lambda a: np.percentile(a, [10, 50, 90, 100]).round(2).tolist()  # noqa: E731
+    out = dict(rep=rep, rows=int(ok.sum()), span_us=float((W[:, 3].max() - t0) / 100),
+               load_us=d((W[:, 1] - W[:, 0]) / 100), walk_us=d((W[:, 2] - W[:, 1]) / 100),
+               store_us=d((W[:, 3] - W[:, 2]) / 100), start_us=d((W[:, 0] - t0) / 100),
+               end_us=d((W[:, 3] - t0) / 100), planes=np.bincount(np.nonzero(ok)[0] // rows, minlength=8).tolist())
+    print(json.dumps(out), flush=True)
