@@ -32,6 +32,10 @@ struct bic_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // bytes at the arena's start left zero by the last call (the single / two-pass encoder's k_fixup
+  // clears its counter and look-back records for the next call); ensure_scratch hands the value to
+  // its caller (scratch_zero_prev) and resets it, since any other user may dirty the arena
+  size_t scratch_zero = 0, scratch_zero_prev = 0;
   uint64_t* lut = nullptr;        // device [3][256] byte table of the fused encoder
   uint32_t* flags = nullptr;      // device [4]: overflow, domain, look-back timeout, internal length check
   uint64_t* lentab = nullptr;     // device copy of the tile length table
@@ -106,7 +110,10 @@ int bind(bic_ctx* ctx) {
 }
 
 int ensure_scratch(bic_ctx* ctx, size_t bytes) {
+  ctx->scratch_zero_prev = ctx->scratch_zero;
+  ctx->scratch_zero = 0;
   if (bytes <= ctx->scratch_bytes) return BIC_OK;
+  ctx->scratch_zero_prev = 0;
   BIC_HIP(hipStreamSynchronize(ctx->cur));  // earlier calls may still use the old arena
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   ctx->scratch = nullptr;
@@ -216,8 +223,9 @@ int bic_ctx_create(int device, bic_ctx** out) {
   }
   ctx->cur = ctx->own;
   {
-    uint64_t host_lut[3 * 256];
+    uint64_t host_lut[bic::kLutWords];
     bic::build_byte_lut(host_lut);
+    bic::egad_build_nib(host_lut + bic::kLutEgadNib);
     if (hipMalloc(&ctx->lut, sizeof(host_lut)) != hipSuccess ||
         hipMemcpy(ctx->lut, host_lut, sizeof(host_lut), hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipStreamDestroy(ctx->own);
@@ -483,6 +491,13 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     fs.off_g = off_golomb;
     fs.off_e = off_eg;
     fs.index = row_index;
+    // (BIC_ZERO_READY: skip the zeroing when the previous call's k_fixup left the counters and records
+    // zero -- measured C2 0.042 -> 0.032 ms with the slow rows inline, but a two-pass call after
+    // single-kernel calls came out wrong in 1 of 30 repetitions (tools/dbg_twopass.py), 0 of 30
+    // with the memset; off until that is understood)
+#ifdef BIC_ZERO_READY
+    fs.zero_ready = mode != bic::kEncStaged && ctx->scratch_zero_prev >= fs.zero_bytes;
+#endif
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -495,6 +510,7 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
           [&] { stage(bic::kFusedRows); });
     timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
     BIC_HIP(hipGetLastError());
+    if (mode != bic::kEncStaged) ctx->scratch_zero = fs.zero_bytes;  // (k_fixup cleared them)
     return BIC_OK;
   }
   // rows wider than 16384 columns: multi-pass chunk kernels (bic_kernels.hip)
@@ -718,7 +734,8 @@ int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t 
     if ((rc = ensure_scratch(ctx, bic::egad_scratch_bytes((uint64_t)rows * nplanes)))) return rc;
     timed(ctx, "encode_eg_adaptive", [&] {
       bic::launch_egad(ctx->cur, planes, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, (uint32_t)nplanes,
-                       predict ? 1 : 0, out, slot_words, plane_bits, ctx->scratch, ctx->flags);
+                       predict ? 1 : 0, out, slot_words, plane_bits, ctx->scratch, ctx->flags, nullptr,
+                       ctx->lut + bic::kLutEgadNib);
     });
     BIC_HIP(hipGetLastError());
     return BIC_OK;
@@ -741,7 +758,7 @@ int bic_egad_row_index(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t
   uint64_t* bits = reinterpret_cast<uint64_t*>(static_cast<char*>(ctx->scratch) + sb);
   timed(ctx, "egad_row_index", [&] {
     bic::launch_egad(ctx->cur, planes, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, (uint32_t)nplanes,
-                     predict ? 1 : 0, nullptr, slot, bits, ctx->scratch, ctx->flags, index);
+                     predict ? 1 : 0, nullptr, slot, bits, ctx->scratch, ctx->flags, index, ctx->lut + bic::kLutEgadNib);
   });
   BIC_HIP(hipGetLastError());
   return BIC_OK;

@@ -53,6 +53,7 @@ struct EgadArgs {
   uint32_t* lane_bits;
   uint32_t* slow_n;
   uint32_t* slow_ids;
+  const uint64_t* nib;  // egad_build_nib's table (kNibTable entries)
 };
 
 // One run from state i: bits of its codeword, the new state. (eg.cpp:20-37 with incBlockSize.)
@@ -359,20 +360,143 @@ __device__ __forceinline__ void eg_lane_runs(const EgLane<WPL>& L, uint32_t cols
   if (L.eol) f((uint32_t)((int)cols - 1 - prev), true);
 }
 
-template <int WPL>
-__device__ __forceinline__ uint32_t eg_lane_walk(const EgLane<WPL>& L, uint32_t cols, uint32_t s) {
-  eg_lane_runs(L, cols, [&](uint32_t len, bool eol) {
-    uint32_t nb, m, g, rem;
-    s = eg_run(s, len, eol, nb, m, g, rem);
-  });
-  return s;
+
+// ---- Nibble form of a lane's runs (the wave-per-row kernels) -------------------------------------
+// The coder read pixel by pixel: a state (i, c) -- the EGLUT index and the zeros of the open block --
+// where a zero completes the block when c + 1 = 2^J(i) ('1', incBlockSize) and a 1 emits '0' and c in
+// J(i) bits (decBlockSize); the fresh coder (kFresh) has block size 1 and g = 1. For i <= 15 (block
+// sizes 1..8) and the fresh coder there are 61 states (i, c), and a 4-pixel nibble maps each to a new
+// state and <= 20 output bits: one entry of a 61 x 16 table (egad_build_nib, host; staged in LDS)
+// replaces up to four run steps. Zero stretches (a word's leading zeros, whole zero words, the
+// end-of-row run) advance block by block, and states above 15 (sparse rows) go pixel by pixel.
+constexpr uint32_t kNibStates = 61, kNibTable = kNibStates * 16;  // u64 entries
+static_assert(kNibTable == kLutWords - kLutEgadNib, "the context's table buffer holds the nibble table");
+__host__ __device__ __forceinline__ uint32_t nib_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
+__host__ __device__ __forceinline__ uint32_t nib_idx(uint32_t i, uint32_t c) {
+  return i == kFresh ? 60u : (i < 4 ? i : (i < 8 ? 4 + (i - 4) * 2 + c : (i < 12 ? 12 + (i - 8) * 4 + c : 28 + (i - 12) * 8 + c)));
+}
+// entry: bits (right-aligned, <= 20) | count << 24 | i' << 32 | c' << 40
+void egad_build_nib(uint64_t* T) {
+  for (uint32_t i0 = 0; i0 <= kFresh; ++i0) {
+    if (i0 >= 16 && i0 != kFresh) continue;
+    const uint32_t nc = i0 == kFresh ? 1u : 1u << nib_j(i0);
+    for (uint32_t c0 = 0; c0 < nc; ++c0)
+      for (uint32_t nib = 0; nib < 16; ++nib) {
+        uint32_t i = i0, c = c0, n = 0;
+        uint64_t bits = 0;
+        for (int b = 3; b >= 0; --b) {
+          const uint32_t bs = i == kFresh ? 1u : 1u << nib_j(i), g = i == kFresh ? 1u : nib_j(i);
+          if ((nib >> b) & 1u) {  // a 1: '0' then c in g bits, decBlockSize
+            bits = (bits << (1 + g)) | c;
+            n += 1 + g;
+            i = (i == kFresh || i == 0) ? 0u : i - 1;
+            c = 0;
+          } else if (++c == bs) {  // a full block: '1', incBlockSize
+            bits = (bits << 1) | 1u;
+            n += 1;
+            i = i == kFresh ? 1u : (i < 31 ? i + 1 : 31u);
+            c = 0;
+          }
+        }
+        T[nib_idx(i0, c0) * 16 + nib] = bits | ((uint64_t)n << 24) | ((uint64_t)i << 32) | ((uint64_t)c << 40);
+      }
+  }
+}
+
+// One coder (i, c) walking a lane; out(v, n) takes n (<= 32) right-aligned bits
+struct NibCoder {
+  uint32_t i, c;
+  // z zeros: whole blocks ('1' each) then the open block's count
+  template <typename OUT>
+  __device__ __forceinline__ void zeros(uint32_t z, OUT&& out) {
+    uint32_t m = 0;
+    while (z) {
+      if (i == kFresh) {
+        --z;
+        ++m;
+        i = 1;
+        continue;
+      }
+      const uint32_t bs = 1u << nib_j(i), need = bs - c;
+      if (z < need) {
+        c += z;
+        break;
+      }
+      z -= need;
+      ++m;
+      c = 0;
+      if (i < 31) ++i;
+    }
+    while (m >= 32) {
+      out(0xFFFFFFFFu, 32);
+      m -= 32;
+    }
+    if (m) out((1u << m) - 1u, m);
+  }
+  // the n (1..4) pixels at the top of the nibble, one at a time
+  template <typename OUT>
+  __device__ __forceinline__ void pixels(uint32_t nib, uint32_t n, OUT&& out) {
+    for (uint32_t b = 0; b < n; ++b) {
+      const uint32_t bs = i == kFresh ? 1u : 1u << nib_j(i), g = i == kFresh ? 1u : nib_j(i);
+      if ((nib >> (3 - b)) & 1u) {
+        out(c, 1 + g);
+        i = (i == kFresh || i == 0) ? 0u : i - 1;
+        c = 0;
+      } else if (++c == bs) {
+        out(1u, 1);
+        i = i == kFresh ? 1u : (i < 31 ? i + 1 : 31u);
+        c = 0;
+      }
+    }
+  }
+  template <typename OUT>
+  __device__ __forceinline__ void nibble(uint32_t nib, uint32_t n, const uint64_t* T, OUT&& out) {
+    if (n == 4 && (i < 16 || i == kFresh)) {
+      const uint64_t e = T[nib_idx(i, c) * 16 + nib];
+      const uint32_t cnt = (uint32_t)(e >> 24) & 31u;
+      if (cnt) out((uint32_t)e & 0xFFFFFFu, cnt);
+      i = (uint32_t)(e >> 32) & 63u;
+      c = (uint32_t)(e >> 40);
+    } else {
+      pixels(nib, n, out);
+    }
+  }
+};
+
+// The lane's runs from state s (its first run's start, column jp + 1, has an empty block): every
+// column from there through the lane's last 1 (and, on the row's last lane, through the row's end
+// and the end-of-row '1'). Returns the state after them.
+template <int WPL, typename OUT>
+__device__ __forceinline__ uint32_t eg_lane_nib(const EgLane<WPL>& L, uint32_t used, uint32_t cols, uint32_t s,
+                                                const uint64_t* T, OUT&& out) {
+  NibCoder k{s, 0};
+  uint32_t col = (uint32_t)(L.jp + 1);  // the next column to code
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = L.w0 + t;
+    const uint64_t x = L.R[t];
+    if (w >= used || !x) continue;  // (zeros: coded by the next stretch)
+    const uint32_t f1 = w * 64 + (uint32_t)__builtin_clzll(x), l1 = w * 64 + 63 - (uint32_t)__builtin_ctzll(x);
+    const uint32_t a = f1 & ~3u;  // the nibble holding the word's first 1
+    if (a > col) k.zeros(a - col, out);  // (a >= col: col follows a 1 of an earlier word, or the row start)
+    for (uint32_t nb = a; nb <= l1; nb += 4) {
+      const uint32_t nib = (uint32_t)(x >> (60 - (nb - w * 64))) & 15u;
+      k.nibble(nib, nb + 3 <= l1 ? 4u : l1 - nb + 1, T, out);
+    }
+    col = l1 + 1;
+  }
+  if (L.eol) {
+    k.zeros(cols - col, out);
+    out(1u, 1);  // end of row (eg.cpp:30-32: no decBlockSize)
+  }
+  return k.i;
 }
 
 // Every lane's start state for the row start s0 (lane 0 starts at s0): constant maps are known at
 // once; a round hands each known end to the next lane. Returns the lane's start; *end = its end.
 template <int WPL>
-__device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t cols, uint32_t lo, uint32_t hi,
-                                                  uint32_t s0, uint32_t* end) {
+__device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t used, uint32_t cols, uint32_t lo,
+                                                  uint32_t hi, uint32_t s0, const uint64_t* T, uint32_t* end) {
   const int lane = lane_id();
   const bool ident = lo == kIdent;
   bool done = !ident && lo == hi;
@@ -383,7 +507,7 @@ __device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t
       if (ident) sout = sin;
       else if (sin == 0 || sin == kFresh) sout = lo;  // (a fresh coder steps like index 0)
       else if (sin == 31) sout = hi;
-      else sout = eg_lane_walk(L, cols, sin);
+      else sout = eg_lane_nib(L, used, cols, sin, T, [](uint32_t, uint32_t) {});
       done = true;
     }
     const uint32_t prev = (uint32_t)dpp_or<0x138>((int)kUnk, (int)(done ? sout : kUnk));
@@ -394,29 +518,35 @@ __device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t
   return sin;
 }
 
+// the nibble table into the workgroup's LDS (before any wave leaves)
+__device__ __forceinline__ void nib_stage(const EgadArgs& a, uint64_t* sT) {
+  for (uint32_t i = threadIdx.x; i < kNibTable; i += blockDim.x) sT[i] = a.nib[i];
+  __syncthreads();
+}
+
 // The lanes' maps and the row's map F_r(0), F_r(31) (lane 63 carries the row's end).
 template <int WPL>
 __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
+  __shared__ uint64_t sT[kNibTable];
+  nib_stage(a, sT);
   const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (id >= (uint64_t)a.rows * a.nplanes) return;  // whole wave
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
-  uint32_t lo = 0, hi = 31;
-  bool any = false;
-  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
-    uint32_t nb, m, g, rem;
-    any = true;
-    const bool same = hi == lo;  // met: one trajectory from here on (a branch: the wave skips the
-    lo = eg_run(lo, len, eol, nb, m, g, rem);  // second walk once every lane's two have met)
-    if (same) hi = lo;
-    else hi = eg_run(hi, len, eol, nb, m, g, rem);
-  });
-  if (!any) lo = hi = kIdent;
+  bool any = L.eol;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) any |= L.R[t] != 0;
+  uint32_t lo = kIdent, hi = kIdent;
+  if (any) {
+    auto none = [](uint32_t, uint32_t) {};
+    lo = eg_lane_nib(L, a.used, a.cols, 0, sT, none);
+    hi = eg_lane_nib(L, a.used, a.cols, 31, sT, none);
+  }
   a.lane_lo[id * 64 + lane_id()] = (uint8_t)lo;
   a.lane_hi[id * 64 + lane_id()] = (uint8_t)hi;
   uint32_t e0, e31;
-  (void)eg_lane_chain(L, a.cols, lo, hi, 0, &e0);
-  (void)eg_lane_chain(L, a.cols, lo, hi, 31, &e31);
+  (void)eg_lane_chain(L, a.used, a.cols, lo, hi, 0, sT, &e0);
+  (void)eg_lane_chain(L, a.used, a.cols, lo, hi, 31, sT, &e31);
   if (lane_id() == 63) {
     a.lo_end[id] = (uint8_t)e0;
     a.hi_end[id] = (uint8_t)e31;
@@ -426,19 +556,17 @@ __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
 // The row's bits from its start state: per lane its start and bits, the row's total.
 template <int WPL>
 __global__ __launch_bounds__(256) void k_egad_llen(EgadArgs a) {
+  __shared__ uint64_t sT[kNibTable];
+  nib_stage(a, sT);
   const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
   const uint32_t lo = a.lane_lo[id * 64 + lane_id()], hi = a.lane_hi[id * 64 + lane_id()];
   uint32_t end;
-  const uint32_t s = eg_lane_chain(L, a.cols, lo, hi, a.start[id], &end);
-  uint32_t bits = 0, t = s;
-  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
-    uint32_t nb, m, g, rem;
-    t = eg_run(t, len, eol, nb, m, g, rem);
-    bits += nb;
-  });
+  const uint32_t s = eg_lane_chain(L, a.used, a.cols, lo, hi, a.start[id], sT, &end);
+  uint32_t bits = 0;
+  if (lo != kIdent) (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t, uint32_t n) { bits += n; });
   a.lane_st[id * 64 + lane_id()] = (uint8_t)s;
   a.lane_bits[id * 64 + lane_id()] = bits;
   const uint64_t tot = wave_sum_u64(bits);
@@ -477,6 +605,8 @@ struct EgImgSink {
 template <int WPL>
 __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t imgs[4][kEgImg];
+  __shared__ uint64_t sT[kNibTable];
+  nib_stage(a, sT);
   const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint64_t Ltot = a.len[id];
@@ -497,26 +627,11 @@ __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   uint32_t pos = wave_incl_sum_u32(bits) - bits;  // the lane's first bit in the row
   uint32_t s = a.lane_st[id * 64 + lane_id()];
   EgImgSink k{img, 0, 0};
-  eg_lane_runs(L, a.cols, [&](uint32_t len, bool eol) {
-    uint32_t nb, m, g, rem;
-    s = eg_run(s, len, eol, nb, m, g, rem);
-    while (m >= 64) {  // a '1' per full block
-      k.put(pos, ~0ull, 64);
-      pos += 64;
-      m -= 64;
-    }
-    if (m) {
-      k.put(pos, ~0ull, m);
-      pos += m;
-    }
-    if (eol) {
-      k.put(pos, 1ull, 1);  // end of row
-      pos += 1;
-    } else {
-      k.put(pos, (uint64_t)rem, 1 + g);  // '0' and the g-bit remainder
-      pos += 1 + g;
-    }
-  });
+  if (a.lane_lo[id * 64 + lane_id()] != kIdent)
+    (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t v, uint32_t n) {
+      k.put(pos, v, n);
+      pos += n;
+    });
   k.flush();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -550,8 +665,9 @@ size_t egad_scratch_bytes(uint64_t nrows) { return nrows * (3 + 8 * 4) + nrows *
 
 void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t nplanes,
                  int predict, uint64_t* out, uint64_t slot, uint64_t* bits, void* scratch, uint32_t* flags,
-                 uint64_t* index) {
+                 uint64_t* index, const uint64_t* nib) {
   EgadArgs a;
+  a.nib = nib;
   a.rows = rows;
   a.cols = cols;
   a.wpr = wpr;

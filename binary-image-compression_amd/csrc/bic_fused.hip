@@ -46,11 +46,21 @@ __device__ unsigned long long g_known[2][1 << 17];
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
     if (threadIdx.x == 0 && (uint64_t)id * 8 + (slot) < (1u << 21)) g_stamps[(uint64_t)id * 8 + (slot)] = t_; \
   } while (0)
+// k_scan_rows' phases per workgroup (slots of g_stamps from 1 << 20: ONES scan, then LEN scan)
+#define SSTAMP(slot)                                                                              \
+  do {                                                                                            \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                   \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                               \
+    if (threadIdx.x == 0) g_stamps[(1u << 20) + (ONES ? 0u : 8192u) + blockIdx.x * 8u + (slot)] = t_; \
+  } while (0)
 #else
 #define STAMP(slot) \
   do {              \
   } while (0)
 #define WSTAMP(slot) \
+  do {               \
+  } while (0)
+#define SSTAMP(slot) \
   do {               \
   } while (0)
 #endif
@@ -80,6 +90,9 @@ constexpr uint32_t kKnownTable = BIC_KNOWN_PI ? 512u : 0u;
 #define BIC_SLOW_REST 1  // class kernels' path: the slow rows by k_emit_rest (listed by the LEN scan), no k_rows_global
 #endif
 constexpr bool kSlowRest = BIC_SLOW_REST != 0;
+#ifndef BIC_K01_MIX
+#define BIC_K01_MIX 0
+#endif
 // One lane's codewords for one residual word.
 struct LaneEnc {
   uint32_t head, k0, z;  // first codeword: k0-bit binary part, then z unary zeros
@@ -208,42 +221,57 @@ __device__ __forceinline__ LaneEnc encode_word(uint64_t x, uint32_t w, uint32_t 
       return e;
     }
   }
-  bool first = true;
+  // k changes inside the word (or n = 0, the plane's first sample): one codeword at a time, the
+  // word's first one (binary part and unary zeros cut off: head, z) peeled off the loop, and
+  // A = arow + jp + 1 - n carried (A' = A + s as n' = n + 1). (Byte by byte with per-byte k bounds
+  // measured slower.)
 #ifdef BIC_STAMPS
   e.path = 3;
 #endif
-  for (;;) {
-    int j;
+  uint32_t A = arow + (uint32_t)(jp + 1) - n;
+  {
     uint32_t s;
+    int j;
     if (x) {
       const int cz = __builtin_clzll(x);
       x ^= BIC_MSB >> cz;
       j = (int)(w * 64) + cz;
       s = (uint32_t)(j - jp - 1);
-    } else if (eol) {
+    } else {  // (eol: the row's end-of-row codeword alone)
       j = (int)cols;
       s = cols - 1 - (uint32_t)jp;
       eol = false;
-    } else {
-      break;
     }
-    const uint32_t k = golomb_k_state(n, arow + (uint32_t)(jp + 1) - n);
+    const uint32_t k = golomb_k_state(n, A);
     const uint32_t q = s >> k;
-    const uint32_t bin = s & ((1u << k) - 1u);
     if constexpr (STR) {
-      if (first) {
-        e.head = bin;
-        e.k0 = k;
-        e.z = q;
-        tail_put(e, 1, 1);
-        first = false;
-      } else {
-        tail_put(e, ((uint64_t)bin << (q + 1)) | 1ull, k + q + 1);  // s <= 63 here: k + q + 1 <= 64
-      }
+      e.head = s & ((1u << k) - 1u);
+      e.k0 = k;
+      e.z = q;
+      tail_put(e, 1, 1);
     }
     e.len += k + q + 1;
+    A += s;
     ++n;
     jp = j;
+  }
+  while (x) {  // (n >= 1 from here; s <= 62: k + q + 1 <= 64)
+    const int cz = __builtin_clzll(x);
+    x ^= BIC_MSB >> cz;
+    const int j = (int)(w * 64) + cz;
+    const uint32_t s = (uint32_t)(j - jp - 1);
+    const uint32_t k = golomb_k(n, A), q = s >> k;
+    if constexpr (STR) tail_put(e, ((uint64_t)(s & ((1u << k) - 1u)) << (q + 1)) | 1ull, k + q + 1);
+    e.len += k + q + 1;
+    A += s;
+    ++n;
+    jp = j;
+  }
+  if (eol) {
+    const uint32_t s = cols - 1 - (uint32_t)jp;
+    const uint32_t k = golomb_k(n, A), q = s >> k;
+    if constexpr (STR) tail_put(e, ((uint64_t)(s & ((1u << k) - 1u)) << (q + 1)) | 1ull, k + q + 1);
+    e.len += k + q + 1;
   }
   return e;
 }
@@ -674,6 +702,7 @@ struct FusedArgs {
                   // pairs; the class kernels store as unsigned long long, a type apart, so the compiler
                   // keeps these loads on the scalar cache: no wait on the vector memory counter)
   uint64_t* sink;     // FusedScratch::sink
+  uint32_t* walk_o;   // FusedScratch::walk_o (the walked rows' row_o)
 #ifdef BIC_STAMPS
   int known;
 #endif
@@ -830,12 +859,11 @@ __device__ __forceinline__ uint64_t img_resid(const uint32_t* eimg, const Geom& 
 // grid walking that list, one wave per row) recomputes each and writes it straight to global
 // memory -- its inner words are zeroed and OR'd, the bits landing in its first/last (shared) word
 // go to the fragment table.
+// (row_global_at: the row's absolute offset G, length L and slow = its samples before + 1 given)
 template <bool PREDICT>
-__device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int lane) {
+__device__ __forceinline__ void row_global_at(const FusedArgs& a, uint64_t id, uint32_t plane, uint32_t row,
+                                              uint64_t G, uint64_t L, uint64_t slow, int lane) {
   const Geom& g = a.g;
-  const uint64_t slow = a.gslow[id];
-  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
-  const uint64_t G = gb_abs(a, id, plane), L = a.glen[id] & kLenMask;
   uint64_t* frag = a.gfrag + 2 * id;
   const uint64_t wh = G >> 6, wt = (G + L - 1) >> 6;
   const bool hpart = !word_complete(wh, G, L);
@@ -874,6 +902,12 @@ __device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int 
     if (hpart) put_shared(a.out_g, wh, frag, 0, h | (wh == wt ? tl : 0));
     if (tpart && wt != wh) put_shared(a.out_g, wt, frag, 1, tl);
   }
+}
+template <bool PREDICT>
+__device__ __forceinline__ void row_global(const FusedArgs& a, uint64_t id, int lane) {
+  const Geom& g = a.g;
+  const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
+  row_global_at<PREDICT>(a, id, plane, row, gb_abs(a, id, plane), a.glen[id] & kLenMask, a.gslow[id], lane);
 }
 
 // EG source: after every reader of the residual rows, the one bit per plane in which the uniform
@@ -1051,7 +1085,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   }
 
   STAMP(3);
-  // ---- Golomb codewords into the row image (rows longer than the LDS window: k_rows_global) ----
+  // ---- Golomb codewords into the row image (rows longer than the LDS window: row_global_at below) ----
   if constexpr (DO_G) {
     constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
     const bool fits = L <= kCapBits;
@@ -1111,9 +1145,11 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
         if (lane == 0) {
           a.gboff[id] = G;
           a.glen[id] = L;
-          a.gslow[id] = fits ? 0 : O + row + 1;  // k_rows_global writes the row
-          if (!fits) a.slow_ids[atomicAdd(a.slow_n, 1u)] = id;
+          a.gslow[id] = 0;
         }
+        // a row longer than the LDS window: written here, straight to global memory (no list, no
+        // k_rows_global launch)
+        if (!fits) row_global_at<PREDICT>(a, id, plane, row, G, L, O + row + 1, lane);
       } else if (lane == 0) {
         a.gboff[id] = G;
         a.glen[id] = 0;
@@ -1418,10 +1454,9 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
 // statistics (bic_kstat.h) prove every codeword k = 0 (length cols + 1: the residual row and its
 // end-of-row '1') or k = 1 (2n + (zeros - odd runs) / 2) get their length without being read;
 // returns true for the others (k_row_walk walks them).
-__device__ __forceinline__ bool row_class(const FusedArgs& a, uint64_t id, uint32_t row, uint32_t O) {
+__device__ __forceinline__ bool row_class(const FusedArgs& a, uint64_t id, uint32_t row, uint32_t O, const RowK& rk) {
   const Geom& g = a.g;
   if (row == 0) return true;  // (the plane's first sample has k = 1 from the fresh state, Golomb.h:18)
-  const RowK rk = row_kstats(a.krec + id * a.ns, a.kpos + id * a.ns, a.ns, g.cols);
   const int64_t N0 = (int64_t)O + row, A0 = (int64_t)row * g.cols - O;
   if (A0 - N0 + rk.q0 <= 0) {
     a.glen[id] = kK0Row | (g.cols + 1);
@@ -1502,6 +1537,7 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       return a.glen[base + r] & kLenMask;
     }
   };
+  SSTAMP(0);
   const uint32_t r0 = b * kScanChunk + threadIdx.x * kScanPer;
   uint64_t v[kScanPer], sum = 0;
 #pragma unroll
@@ -1509,6 +1545,16 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
     v[i] = r0 + i < g.rows ? val(r0 + i) : 0;
     sum += v[i];
   }
+  // (ONES + CLASSIFY: the rows' k statistics loaded now, their latency under the scans below)
+  RowKRaw rks[kScanPer];
+  if constexpr (ONES && CLASSIFY) {
+#pragma unroll
+    for (uint32_t i = 0; i < kScanPer; ++i) {
+      const uint64_t id = base + (r0 + i < g.rows ? r0 + i : 0);
+      rks[i] = row_kstats_load(a.krec + id * a.ns, a.kpos + id * a.ns, a.ns);
+    }
+  }
+  SSTAMP(1);
   uint64_t before = 0;  // this thread's share of the plane's rows before the chunk
   const uint32_t lim = b * kScanChunk;
   if constexpr (ONES) {  // the records of those rows are one contiguous range
@@ -1529,17 +1575,20 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
 #pragma unroll 8
     for (uint32_t r = threadIdx.x; r < lim; r += 1024) before += val(r);
   }
+  SSTAMP(2);
   uint64_t tot, btot;
   uint64_t pre = block_excl_scan<uint64_t>(sum, tmp, tot);
   (void)block_excl_scan<uint64_t>(before, tmp, btot);
   pre += btot;
+  SSTAMP(3);
   if constexpr (ONES) {
     bool walks[kScanPer];  // classify every row of the thread first: their record loads overlap
     uint64_t p = pre;
 #pragma unroll
     for (uint32_t i = 0; i < kScanPer; ++i) {
       const uint32_t r = r0 + i;
-      walks[i] = CLASSIFY && r < g.rows && row_class(a, base + r, r, (uint32_t)p);
+      if constexpr (CLASSIFY) walks[i] = r < g.rows && row_class(a, base + r, r, (uint32_t)p, row_kstats_combine(rks[i], g.cols));
+      else walks[i] = false;
       p += v[i];
     }
 #pragma unroll
@@ -1555,7 +1604,11 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
           const int leader = __builtin_ctzll(m);
           if (lane_id() == leader) wb = atomicAdd(a.counter + 2, (uint32_t)__popcll(m));
           wb = (uint32_t)__shfl((int)wb, leader);
-          if (walk) a.walk_ids[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)(base + r);
+          if (walk) {
+            const uint32_t wi = wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+            a.walk_ids[wi] = (uint32_t)(base + r);
+            a.walk_o[wi] = (uint32_t)pre;
+          }
         }
       }
       const bool first1 = in && pre == 0 && v[i] > 0;  // the row holding the plane's first 1
@@ -1641,6 +1694,7 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
     }
     if (b == nb - 1 && threadIdx.x == 0) a.bits_g[plane] = btot + tot;
   }
+  SSTAMP(4);
 }
 
 // One row across a workgroup of blockDim.x / 64 (<= 4) waves, lane = word 64 v + lane of wave v:
@@ -1658,7 +1712,7 @@ __device__ __forceinline__ WideRow wide_prefix(uint64_t x, uint32_t w, uint32_t 
   const int mx = wave_incl_max(x ? (int)(w * 64 + 63 - __builtin_ctzll(x)) : -1);
   if (lane == 63) {
     sh[v] = inc;
-    sh[4 + v] = (uint32_t)mx;
+    sh[8 + v] = (uint32_t)mx;
   }
   __syncthreads();
   uint32_t nb = nbase, tot = 0;
@@ -1667,7 +1721,7 @@ __device__ __forceinline__ WideRow wide_prefix(uint64_t x, uint32_t w, uint32_t 
     const uint32_t c = sh[u];
     if (u < v) {
       nb += c;
-      jb = max(jb, (int)sh[4 + u]);
+      jb = max(jb, (int)sh[8 + u]);
     }
     tot += c;
   }
@@ -1675,30 +1729,59 @@ __device__ __forceinline__ WideRow wide_prefix(uint64_t x, uint32_t w, uint32_t 
   return WideRow{nb + inc - pc, max(jb, dpp_or<0x138>(-1, mx)), tot};
 }
 
-// The listed rows' Golomb lengths (codeword walk, word_len), one workgroup per row and one word
-// per lane, so a row's serial codeword chain is one word long; a fixed grid strides over the
-// list, whose length k_scan_rows left in counter[2]. k_emit_rest takes the rows with mixed k, and
-// the row holding the plane's first 1, from this same list.
+// The listed rows' Golomb lengths (codeword walk, word_len), one workgroup per row and one HALF word
+// per lane (lanes 2w and 2w + 1 share residual word w, each counting the codewords whose '1' lies in
+// its 32 columns), so a row's serial codeword chain is at most 32 columns long; a fixed grid strides
+// over the list, whose length k_scan_rows left in counter[2]. k_emit_rest takes the rows with mixed k,
+// and the row holding the plane's first 1, from this same list. (One word per lane: C3 walk 17.4 us.)
 constexpr uint32_t kWalkWaves = 8192;  // the walk grid in waves (32 per CU), whatever the row width
+#ifndef BIC_WALK_SPLIT
+#define BIC_WALK_SPLIT 2
+#endif
+constexpr uint32_t kWalkSplit = BIC_WALK_SPLIT;  // lanes per residual word (1 or 2)
+// residual word w of a row on its own (the word left of it loaded too): no cross-lane exchange, so
+// any lane layout can call it
 template <bool PREDICT>
-__global__ __launch_bounds__(256) void k_row_walk(FusedArgs a) {
-  __shared__ uint32_t sh[8], sl[4], sk[4];
+__device__ __forceinline__ uint64_t resid_word_at(const uint64_t* planes, const Geom& g, uint32_t plane, uint32_t row,
+                                                  uint32_t w) {
+  if (w >= g.used) return 0;
+  const uint64_t* cur = planes + (uint64_t)plane * g.plane_words + (uint64_t)row * g.wpr;
+  uint64_t d = cur[w];
+  if constexpr (PREDICT) {
+    const uint64_t* up = cur - g.wpr;
+    if (row) d ^= up[w];
+    const uint64_t dl = w ? cur[w - 1] ^ (row ? up[w - 1] : 0ull) : 0ull;
+    d ^= (d >> 1) | (dl << 63);
+    if (row == 0 && w == 0) d &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+  }
+  return w == g.used - 1 ? d & g.trail : d;
+}
+template <bool PREDICT>
+__global__ __launch_bounds__(512) void k_row_walk(FusedArgs a) {
+  __shared__ uint32_t sh[16], sl[8], sk[8];
   const Geom& g = a.g;
   const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint32_t w = 64 * v + lane;
+  const uint32_t w = (64 * v + lane) / kWalkSplit, h = kWalkSplit == 1 ? 1u : (uint32_t)lane & 1u;
+  const uint64_t hmask = kWalkSplit == 1 ? ~0ull : (h ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull);
   const uint32_t nlist = __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (the list entry -- row id and its row_o, side by side -- of the workgroup's next row is loaded
+  // while this row is walked)
+  uint32_t nid = blockIdx.x < nlist ? a.walk_ids[blockIdx.x] : 0u, nO = blockIdx.x < nlist ? a.walk_o[blockIdx.x] : 0u;
   for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
-    const uint64_t id = a.walk_ids[i];
+    const uint64_t id = nid;
+    const uint32_t O = nO;
+    if (i + gridDim.x < nlist) {
+      nid = a.walk_ids[i + gridDim.x];
+      nO = a.walk_o[i + gridDim.x];
+    }
     WSTAMP(4);
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
-    const uint32_t O = a.row_o[id];
-    uint64_t rr[1];
-    if (!PREDICT && a.esrc) rr[0] = eg_src_word(a.esrc + (uint64_t)plane * a.slot_e, g, row, w);
-    else resid_row<1, PREDICT>(a.planes, g, plane, row, rr, 64 * v);
+    const uint64_t x = ((!PREDICT && a.esrc) ? eg_src_word(a.esrc + (uint64_t)plane * a.slot_e, g, row, w)
+                                             : resid_word_at<PREDICT>(a.planes, g, plane, row, w)) & hmask;
     WSTAMP(5);
-    const WideRow p = wide_prefix(rr[0], w, O + row, sh);
+    const WideRow p = wide_prefix(x, w, O + row, sh);
     uint32_t kor = 0;
-    uint32_t ll = word_len(rr[0], w, p.n, p.jp, row * (g.cols + 1), w == g.used - 1, g.cols, kor);
+    uint32_t ll = word_len(x, w, p.n, p.jp, row * (g.cols + 1), w == g.used - 1 && h == 1, g.cols, kor);
     ll = wave_sum_u32(ll);
     WSTAMP(6);
     const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);  // some k != 0 / some k != 1
@@ -2378,6 +2461,15 @@ __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   const uint32_t nw = gridDim.x * 4;
   // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
   const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#if BIC_K01_MIX
+  // half of the waves take their k = 1 rows first: LDS- and issue-heavy rows beside the copies'
+  // memory traffic, instead of every wave in the same phase at once
+  if (i0 & 1) {
+    k1_rows<WPL>(a, i0, nw, gimg, s_lut);
+    k0_rows<WPL>(a, i0, nw);
+    return;
+  }
+#endif
   k0_rows<WPL>(a, i0, nw);
   k1_rows<WPL>(a, i0, nw, gimg, s_lut);
 }
@@ -2391,7 +2483,7 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t gimg[kGImg];
   __shared__ __attribute__((aligned(16))) uint32_t eimg[kEImg];
   __shared__ uint32_t s_lut[512];
-  __shared__ uint32_t sh[8];
+  __shared__ uint32_t sh[16];  // (wide_prefix: up to 8 waves)
   __shared__ int sf[4];
   const Geom& g = a.g;
   const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -2499,8 +2591,17 @@ __global__ __launch_bounds__(256) void k_fixup(const uint64_t* __restrict__ boff
                                                uint32_t rows, uint64_t nrows, uint32_t second,
                                                const uint64_t* __restrict__ gbase = nullptr, uint64_t slot_bits = 0,
                                                const uint64_t* __restrict__ efix = nullptr, uint64_t* eout = nullptr,
-                                               uint64_t eslot = 0, uint32_t enp = 0) {
+                                               uint64_t eslot = 0, uint32_t enp = 0, uint32_t* zc = nullptr,
+                                               uint64_t* zr = nullptr, uint64_t zn = 0) {
   eg_fix_bit(efix, eout, eslot, enp);  // (EG source: after every reader of the residual rows)
+  if (zr) {  // single / two-pass encoder: its counters and 2 zn look-back records cleared for the next call
+    const uint64_t zi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (zi < zn) {
+      zr[zi] = 0;
+      zr[zn + zi] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 64) zc[threadIdx.x] = 0;
+  }
   // blocks [second, ...) serve the second stream (EG) when both streams are written
   if (blockIdx.x >= second) {
     boff = boff2;
@@ -2548,7 +2649,7 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
 // ------------------------------------------------------------------------------------
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
-  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 3 + 1024 + (size_t)g.nplanes * 8 * 4 + 64 +
+  return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 4 + 1024 + (size_t)g.nplanes * 8 * 4 + 64 +
          n * 16 * 2 + 64 + 512;  // (cls, sink)
 }
 
@@ -2575,8 +2676,9 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
   fs.row_o = fs.sones + n * kMaxStrips;
   fs.walk_ids = fs.row_o + n;
   fs.rest_ids = fs.walk_ids + n;
+  fs.walk_o = fs.rest_ids + n;
   {
-    uintptr_t e = reinterpret_cast<uintptr_t>(fs.rest_ids + n);
+    uintptr_t e = reinterpret_cast<uintptr_t>(fs.walk_o + n);
     e = (e + 7) & ~(uintptr_t)7;
     fs.pones = reinterpret_cast<uint64_t*>(e);
     fs.gbase = fs.pones + g.nplanes;
@@ -2606,7 +2708,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   if (stage == kFusedPrep) {
     // the staged encoder's count pass zeroes its counters itself (kZeroWords, launch_row_ones /
     // launch_gray_rows)
-    if (mode != kEncStaged) (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
+    // (single / two-pass: not when the previous call's k_fixup left them zero)
+    if (mode != kEncStaged && !fs.zero_ready) (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
     return;
   }
   const bool single_pass = mode == kEncSingle;
@@ -2614,6 +2717,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
               fs.eboff, fs.elen, fs.efrag, fs.row_o, fs.sones, fs.krec, fs.kpos, fs.counted ? fs.ns : 1u, fs.walk_ids, fs.rest_ids, fs.slow_n, fs.slow_ids, out_g, slot_g, bits_g, out_e, slot_e,
               bits_e, flags};
   a.pones = fs.pones;
+  a.walk_o = fs.walk_o;
   a.gbase = fs.gbase;
   a.off_g = out_g ? fs.off_g : nullptr;
   a.off_e = out_e ? fs.off_e : nullptr;
@@ -2637,7 +2741,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   if (stage == kFusedFinish) {
     // a fixed small grid walks the list of LDS-overflow rows (usually empty); block 0 also clears
     // the EG source's one bit per plane (eg_fix_bit)
-    if ((dg && (!a.cls || !kSlowRest)) || (!dg && es)) {  // (a.cls: k_emit_rest wrote the slow rows)
+    // (a.cls: k_emit_rest wrote the slow rows; single pass: k_encode_rows did)
+    if ((dg && !single_pass && (!a.cls || !kSlowRest)) || (!dg && es)) {
       if (predict) k_rows_global<true><<<dg ? 256 : 1, 256, 0, s>>>(a);
       else k_rows_global<false><<<dg ? 256 : 1, 256, 0, s>>>(a);
     }
@@ -2647,7 +2752,8 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
                                                         fs.eboff, fs.elen, fs.efrag, out_e, g.rows, nrows,
                                                         dg && de ? fgrid : 0xffffffffu,
                                                         dg && mode == kEncStaged ? a.off_g ? fs.gbase : nullptr : nullptr,
-                                                        slot_g * 64, dg ? a.efix : nullptr, out_e, slot_e, g.nplanes);
+                                                        slot_g * 64, dg ? a.efix : nullptr, out_e, slot_e, g.nplanes,
+                                                        fs.counter, mode != kEncStaged ? fs.ones_rec : nullptr, nrows);
     return;
   }
   const int wpl = g.used <= 64 ? 1 : (g.used <= 128 ? 2 : 4);
@@ -2658,9 +2764,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
       if (dg) k_scan_rows<true, true><<<sgrid, 1024, 0, s>>>(a);
       else k_scan_rows<true, false><<<sgrid, 1024, 0, s>>>(a);
       if (dg) {
-        const uint32_t nwv = (g.used + 63) / 64;  // one workgroup per row, one word per lane
-        if (predict) k_row_walk<true><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
-        else k_row_walk<false><<<kWalkWaves / nwv, 64 * nwv, 0, s>>>(a);
+        const uint32_t wwv = (kWalkSplit * g.used + 63) / 64;  // k_row_walk: waves per row (<= 8)
+        if (predict) k_row_walk<true><<<kWalkWaves / wwv, 64 * wwv, 0, s>>>(a);
+        else k_row_walk<false><<<kWalkWaves / wwv, 64 * wwv, 0, s>>>(a);
         k_scan_rows<false, false><<<sgrid, 1024, 0, s>>>(a);  // (+ the row index)
       }
       // packed output: the planes' start words (the rows' Golomb offsets stay slot-relative: gb_abs)

@@ -55,9 +55,14 @@ bool med_rows_supported(const Geom& g, const void* planes, const void* resid);
 size_t egad_scratch_bytes(uint64_t nrows);
 // out null: no emission (index only); index (nullable): per row its first bit in the plane's stream and
 // the coder state there (bic_egad_row_index)
+// nib: egad_build_nib's table in device memory (the context's byte-table buffer, kLutEgadNib)
 void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t nplanes,
                  int predict, uint64_t* out, uint64_t slot, uint64_t* bits, void* scratch, uint32_t* flags,
-                 uint64_t* index = nullptr);
+                 uint64_t* index, const uint64_t* nib);
+// the adaptive EG coder's nibble table (976 u64 entries), built on the host
+void egad_build_nib(uint64_t* T);
+constexpr size_t kLutEgadNib = 3 * 256;        // its offset in the context's byte-table buffer (u64 words)
+constexpr size_t kLutWords = kLutEgadNib + 976;  // the whole buffer
 // f1 decoders (bic_decode.hip)
 bool decode_supported(uint32_t cols);
 size_t decode_scratch_bytes(uint32_t rows, uint32_t wpr, uint32_t nplanes);
@@ -111,6 +116,7 @@ struct FusedScratch {
   uint32_t* counter;
   uint64_t *ones_rec, *bits_rec;
   size_t zero_bytes;  // counter + records, zeroed per launch
+  bool zero_ready = false;  // (single / two-pass) already zero: the previous call's k_fixup cleared them
   uint64_t *gboff, *glen, *gfrag, *gslow, *eboff, *elen, *efrag;
   uint32_t* row_o;   // ones of the plane before each row (two-pass / staged encoders)
   // staged encoder's count pass: per (plane, row, strip) the residual 1-count and the Golomb k
@@ -120,6 +126,7 @@ struct FusedScratch {
   uint32_t* kpos;
   uint32_t ns;
   uint32_t* walk_ids;  // rows whose Golomb length is walked (k_row_walk)
+  uint32_t* walk_o;    // their ones before (row_o), beside the id: the walk loads both at once
   uint32_t* rest_ids;  // rows the REST emit launch writes (mixed k, the plane's first 1; counter[3])
   // optional second stream for the REST launch (it then runs beside the main emit launch) and
   // the fork / join events; null: one stream

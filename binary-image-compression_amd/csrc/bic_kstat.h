@@ -204,14 +204,24 @@ struct RowK {
   int32_t q0, qh, ql;
   uint32_t ones, chg;
 };
-__device__ __forceinline__ RowK row_kstats(const int4* rec, const uint32_t* pos, uint32_t ns, uint32_t cols) {
+// (in two halves -- the strips' records loaded, then combined -- so a caller can keep the loads in
+// flight across other work)
+struct RowKRaw {
   int4 v[kMaxStrips];
   uint32_t pp[kMaxStrips];
+};
+__device__ __forceinline__ RowKRaw row_kstats_load(const int4* rec, const uint32_t* pos, uint32_t ns) {
+  RowKRaw q;
 #pragma unroll
   for (uint32_t s = 0; s < kMaxStrips; ++s) {
-    v[s] = s < ns ? rec[s] : make_int4(0, 0, 0, 0);
-    pp[s] = s < ns ? pos[s] : 0u;
+    q.v[s] = s < ns ? rec[s] : make_int4(0, 0, 0, 0);
+    q.pp[s] = s < ns ? pos[s] : 0u;
   }
+  return q;
+}
+__device__ __forceinline__ RowK row_kstats_combine(const RowKRaw& q, uint32_t cols) {
+  const int4* v = q.v;
+  const uint32_t* pp = q.pp;
   RowK r{0, 0, 0, 0, 0};
   int32_t last = -1;
 #pragma unroll
@@ -227,6 +237,9 @@ __device__ __forceinline__ RowK row_kstats(const int4* rec, const uint32_t* pos,
   }
   r.chg += (uint32_t)((last ^ (int32_t)cols) & 1);  // the end-of-row sample at column cols
   return r;
+}
+__device__ __forceinline__ RowK row_kstats(const int4* rec, const uint32_t* pos, uint32_t ns, uint32_t cols) {
+  return row_kstats_combine(row_kstats_load(rec, pos, ns), cols);
 }
 
 }  // namespace bic

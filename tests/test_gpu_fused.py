@@ -439,3 +439,20 @@ def test_narrow_rows_pitched(ctx, oracle, rows, cols, wpr, p):
             nb = int(as_u64(bits)[k])
             assert nb == eb, (k, coder)
             assert stream_bytes(out[k], nb) == est.tobytes(), (k, coder)
+
+
+def test_look_back_records_left_zero(ctx, oracle):
+    """The single-kernel and two-pass encoders skip zeroing their counters and look-back records when
+    the previous call's k_fixup left them zero (bic_capi.cpp scratch_zero): calls of growing and
+    shrinking row counts, with other users of the context's scratch (the staged encoder, the
+    multi-pass kernels) in between, each checked against the oracle"""
+    seq = [("single-kernel", 40, 1000), ("single-kernel", 12, 1000), ("single-kernel", 90, 1000),
+           ("two-pass", 90, 1000), ("single-kernel", 90, 1000), ("staged", 60, 4096),
+           ("single-kernel", 60, 4096), ("multipass", 30, 2000), ("two-pass", 30, 2000), ("single-kernel", 30, 2000)]
+    try:
+        for i, (mode, rows, cols) in enumerate(seq):
+            ctx.set_encoder(mode)
+            P = np.stack([oracle.gen_plane(0xAB + 7 * i + k, (0.5, 0.1)[k], rows, cols) for k in range(2)])
+            check(ctx, oracle, P, cols, i & 1)
+    finally:
+        ctx.set_encoder("auto")

@@ -1,7 +1,8 @@
-"""Phase clocks of k_row_walk (diagnostic build lib/libbic_stamps.so, make stamps): one C3 encode_gray
-(the bench's default call), then per walked row its entry, residual-word, walked and stored times on
-the shared 100 MHz clock (slots 4-7 of bic_fused.hip WSTAMP). Prints the walk's span, the rows'
-phase durations and how the rows' start times spread over the span."""
+"""Phase clocks of the staged prefix (diagnostic build lib/libbic_stamps.so, make stamps): one C3
+encode_gray (the bench's default call), then per walked row of k_row_walk its entry, residual-word,
+walked and stored times on the shared 100 MHz clock (slots 4-7 of bic_fused.hip WSTAMP), and per
+workgroup of the two k_scan_rows launches (SSTAMP) its entry, own rows loaded, earlier rows summed,
+block scans done and end. Prints spans, phase durations and how the start times spread."""
 import ctypes as C
 import json
 import os
@@ -22,14 +23,14 @@ g.manual_seed(0x5EED0000)
 gray = t.randint(0, 256, (rows, cols), dtype=t.uint8, device=ctx.dev, generator=g)
 lib = pybic.load()
 lib.bic_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
-n = rows * 8 * 8
+n = (1 << 20) + 16384
 out = {}
 for rep in range(3):
     ctx.encode_gray(gray, store_planes=False)
     ctx.sync()
     buf = np.zeros(n, np.uint64)
     assert lib.bic_debug_stamps(buf.ctypes.data, n) == 0
-    S = buf.reshape(-1, 8).astype(np.int64)[:, 4:8]
+    S = buf[:rows * 8 * 8].reshape(-1, 8).astype(np.int64)[:, 4:8]
     ok = (S[:, 0] > 0) & (S[:, 3] >= S[:, 0])
     if rep == 0:
         first = S[:, 0].copy()
@@ -44,3 +45,11 @@ for rep in range(3):
                store_us=d((W[:, 3] - W[:, 2]) / 100), start_us=d((W[:, 0] - t0) / 100),
                end_us=d((W[:, 3] - t0) / 100), planes=np.bincount(np.nonzero(ok)[0] // rows, minlength=8).tolist())
     print(json.dumps(out), flush=True)
+    for name, off in (("ones_scan", 0), ("len_scan", 8192)):
+        T = buf[(1 << 20) + off:(1 << 20) + off + 8192].reshape(-1, 8).astype(np.int64)[:, :5]
+        T = T[T[:, 0] > 0][:128]
+        t0 = T[:, 0].min()
+        print(json.dumps(dict(rep=rep, kernel=name, wgs=len(T), span_us=float((T[:, 4].max() - t0) / 100),
+                              own_us=d((T[:, 1] - T[:, 0]) / 100), before_us=d((T[:, 2] - T[:, 1]) / 100),
+                              scans_us=d((T[:, 3] - T[:, 2]) / 100), tail_us=d((T[:, 4] - T[:, 3]) / 100),
+                              start_us=d((T[:, 0] - t0) / 100), end_us=d((T[:, 4] - t0) / 100))), flush=True)
