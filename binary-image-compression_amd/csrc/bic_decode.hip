@@ -42,6 +42,7 @@ struct DecArgs {
   // unmed's column chunk totals (k_col_chunks' output), formed by the Golomb row kernel itself when
   // a wave's 64 rows are one column chunk of one plane (rows % kColChunk == 0); null otherwise
   uint64_t* ctot;
+  const uint64_t* egnib;  // egad_build_dec_nib's table (the adaptive EG decoder)
 };
 
 __device__ __forceinline__ const uint64_t* plane_stream(const DecArgs& a, uint32_t plane) {
@@ -230,8 +231,75 @@ __global__ __launch_bounds__(256) void k_dec_golomb_lanes(DecArgs a) {
 // independently from the egad row index (bic_egad_row_index: per row its first bit and the state
 // there; 32 = a fresh coder: index 0 but g = 1, eg.h:9). One lane per row; the leading 1s of the
 // next 64 stream bits are counted at once (the blocks), the remainder read as one field.
-__device__ __forceinline__ uint32_t egad_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
+__host__ __device__ __forceinline__ uint32_t egad_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
+// Nibble steps: while the index is <= 15 (blocks of <= 8 columns, remainders of <= 3 bits) and the row's
+// end is more than 40 columns away, 4 stream bits at a time through a table over the decoder's state
+// (i, phase: in a run's '1's (U) or its remainder (R) after k of its g bits, value v) -- 17 U and 45 R
+// states: the columns they advance (<= 36), the 1s they place there and the state after. Other bits
+// (higher indices, the row's last columns and its end-of-row '1') one at a time, checked.
+constexpr uint32_t kFreshD = 32;
+__host__ __device__ __forceinline__ uint32_t egad_dsidx(uint32_t i, uint32_t ph, uint32_t k, uint32_t v) {
+  if (!ph) return i == kFreshD ? 16u : i;
+  if (i == kFreshD) return 17u;
+  if (i < 8) return 18u + (i - 4);
+  if (i < 12) return 22u + (i - 8) * 3 + (k ? 1 + v : 0u);
+  return 34u + (i - 12) * 7 + (k == 0 ? 0u : (k == 1 ? 1 + v : 3 + v));
+}
+// entry: the 1s (bit 39 - p: column col + p) | P << 40 | i << 46 | ph << 52 | k << 53 | v << 55; bit 63: escape
+void egad_build_dec_nib(uint64_t* T) {
+  for (uint32_t n = 0; n < 62 * 16; ++n) T[n] = 1ull << 63;
+  auto fill = [&](uint32_t i0, uint32_t ph0, uint32_t k0, uint32_t v0) {
+    for (uint32_t nib = 0; nib < 16; ++nib) {
+      uint32_t i = i0, ph = ph0, k = k0, v = v0, P = 0;
+      uint64_t m = 0;
+      bool esc = false;
+      for (int b = 3; b >= 0 && !esc; --b) {
+        const uint32_t bit = (nib >> b) & 1u;
+        const uint32_t g = i == kFreshD ? 1u : egad_j(i);
+        if (!ph) {
+          if (bit) {  // a full block of zeros, incBlockSize
+            P += i == kFreshD ? 1u : 1u << g;
+            i = i == kFreshD ? 1u : i + 1;
+          } else if (g == 0) {  // '0' with no remainder: the run's 1
+            m |= 1ull << (39 - P);
+            ++P;
+            i = (i == kFreshD || i == 0) ? 0u : i - 1;
+          } else {
+            ph = 1;
+            k = 0;
+            v = 0;
+          }
+        } else {
+          v = 2 * v + bit;
+          if (++k == g) {  // the remainder read: its zeros, then the run's 1
+            P += v;
+            m |= 1ull << (39 - P);
+            ++P;
+            i = (i == kFreshD || i == 0) ? 0u : i - 1;
+            ph = 0;
+            k = v = 0;
+          }
+        }
+        esc = i != kFreshD && i >= 16;
+      }
+      if (!esc)
+        T[egad_dsidx(i0, ph0, k0, v0) * 16 + nib] = m | ((uint64_t)P << 40) | ((uint64_t)i << 46) |
+                                                     ((uint64_t)ph << 52) | ((uint64_t)k << 53) | ((uint64_t)v << 55);
+    }
+  };
+  for (uint32_t i = 0; i < 16; ++i) fill(i, 0, 0, 0);
+  fill(kFreshD, 0, 0, 0);
+  fill(kFreshD, 1, 0, 0);
+  for (uint32_t i = 4; i < 16; ++i) {
+    const uint32_t g = egad_j(i);
+    for (uint32_t k = 0; k < g; ++k)
+      for (uint32_t v = 0; v < (1u << k); ++v) fill(i, 1, k, v);
+  }
+}
 __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
+  __shared__ uint64_t sT[62 * 16];
+  for (uint32_t q = threadIdx.x; q < 62 * 16; q += 256) sT[q] = a.egnib[q];
+  __syncthreads();
   const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
@@ -298,48 +366,76 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
     ++ow;
     acc = 0;
   };
-  uint32_t idx = S0 == 32 ? 0u : (uint32_t)S0, g = S0 == 32 ? 1u : egad_j(idx);
-  uint64_t bs = S0 == 32 ? 1ull : 1ull << g;  // (a fresh coder's block is 1 with g = 1: eg.h:9)
-  uint32_t j = 0;  // the row's next column
+  // the coder state: index i (kFreshD: a fresh coder, index 0 with g = 1, eg.h:9), phase ph (0: a
+  // run's '1's, 1: its remainder after k of its g bits, value v); col: the row's next column
+  uint32_t i = S0 == 32 ? kFreshD : (uint32_t)S0, ph = 0, k = 0, v = 0, col = 0;
+  auto one = [&](uint32_t c) {  // the run's 1 at column c
+    while ((c >> 6) > ow) flush();
+    acc |= BIC_MSB >> (c & 63);
+  };
   while (!bad) {
-    const uint64_t maxlen = (uint64_t)(a.cols - j);
-    uint64_t L = 0;
-    bool eol = false;
-    for (;;) {  // the run's '1's: full blocks, or the one that passes the row's end
-      const uint64_t y = peek();
-      const uint32_t c = y == ~0ull ? 64u : (uint32_t)__builtin_clzll(~y);
-      uint32_t t = 0;
-      while (t < c) {
-        L += bs;
-        ++t;
-        if (L > maxlen) {
-          eol = true;
-          break;
-        }
-        if (idx < 31) ++idx;
-        g = egad_j(idx);
-        bs = 1ull << g;
-      }
-      if (t) advance(t);
-      if (eol || c < 64 || used_bits > len) break;
-    }
-    if (used_bits > len) bad = true;
-    if (eol || bad) break;
-    advance(1);  // the '0'
-    const uint64_t rem = g ? peek() >> (64 - g) : 0ull;
-    advance(g);
-    L += rem;
-    if (idx > 0) --idx;
-    g = egad_j(idx);
-    bs = 1ull << g;
-    if (L >= maxlen || used_bits > len) {
+    if (used_bits > len) {
       bad = true;
       break;
     }
-    const uint32_t c = j + (uint32_t)L;  // the run's 1
-    while ((c >> 6) > ow) flush();
-    acc |= BIC_MSB >> (c & 63);
-    j = c + 1;
+    if ((i < 16 || i == kFreshD) && col + 40 <= a.cols && used_bits + 4 <= len) {
+      const uint64_t e = sT[egad_dsidx(i, ph, k, v) * 16 + (uint32_t)(peek() >> 60)];
+      if (!(e >> 63)) {
+        advance(4);
+        const uint32_t P = (uint32_t)(e >> 40) & 63u;
+        const uint64_t m = (e & 0xFFFFFFFFFFull) << 24;  // MSB-first: bit 63 is column col
+        if (m) {
+          while ((col >> 6) > ow) flush();
+          const uint32_t o = col & 63u;
+          acc |= m >> o;
+          if (o + P > 64) {
+            const uint64_t spill = m << (64 - o);
+            flush();
+            acc |= spill;
+          }
+        }
+        col += P;
+        i = (uint32_t)(e >> 46) & 63u;
+        ph = (uint32_t)(e >> 52) & 1u;
+        k = (uint32_t)(e >> 53) & 3u;
+        v = (uint32_t)(e >> 55) & 7u;
+        continue;
+      }
+    }
+    const uint32_t bit = (uint32_t)(peek() >> 63);
+    advance(1);
+    const uint32_t g = i == kFreshD ? 1u : egad_j(i);
+    if (!ph) {
+      if (bit) {  // a full block -- or, passing the row's end, its end-of-row '1'
+        const uint32_t z = i == kFreshD ? 1u : 1u << g;
+        if ((uint64_t)col + z > a.cols) break;
+        col += z;
+        i = i == kFreshD ? 1u : (i < 31 ? i + 1 : 31u);
+      } else if (g == 0) {
+        if (col >= a.cols) {
+          bad = true;
+          break;
+        }
+        one(col++);
+        i = i == 0 ? 0u : i - 1;
+      } else {
+        ph = 1;
+        k = 0;
+        v = 0;
+      }
+    } else {
+      v = 2 * v + bit;
+      if (++k == g) {
+        col += v;
+        if (col >= a.cols) {
+          bad = true;
+          break;
+        }
+        one(col++);
+        i = (i == kFreshD || i == 0) ? 0u : i - 1;
+        ph = 0;
+      }
+    }
   }
   if (used_bits != len) bad = true;
   while (ow < a.used) flush();
@@ -858,8 +954,9 @@ size_t decode_scratch_bytes(uint32_t rows, uint32_t wpr, uint32_t nplanes) {
 void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t slot, const uint64_t* word_off,
                    const uint64_t* plane_bits, const uint64_t* index, const uint8_t* p00, uint32_t rows,
                    uint32_t cols, uint32_t wpr, uint32_t nplanes, int predict, uint64_t* out, void* scratch,
-                   uint32_t* flags) {
+                   uint32_t* flags, const uint64_t* egnib) {
   DecArgs a;
+  a.egnib = egnib;
   a.rows = rows;
   a.cols = cols;
   a.wpr = wpr;

@@ -370,7 +370,7 @@ __device__ __forceinline__ void eg_lane_runs(const EgLane<WPL>& L, uint32_t cols
 // replaces up to four run steps. Zero stretches (a word's leading zeros, whole zero words, the
 // end-of-row run) advance block by block, and states above 15 (sparse rows) go pixel by pixel.
 constexpr uint32_t kNibStates = 61, kNibTable = kNibStates * 16;  // u64 entries
-static_assert(kNibTable == kLutWords - kLutEgadNib, "the context's table buffer holds the nibble table");
+static_assert(kNibTable == kLutEgadDec - kLutEgadNib, "the context's table buffer holds the nibble table");
 __host__ __device__ __forceinline__ uint32_t nib_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
 __host__ __device__ __forceinline__ uint32_t nib_idx(uint32_t i, uint32_t c) {
   return i == kFresh ? 60u : (i < 4 ? i : (i < 8 ? 4 + (i - 4) * 2 + c : (i < 12 ? 12 + (i - 8) * 4 + c : 28 + (i - 12) * 8 + c)));
@@ -492,6 +492,46 @@ __device__ __forceinline__ uint32_t eg_lane_nib(const EgLane<WPL>& L, uint32_t u
   return k.i;
 }
 
+// eg_lane_nib from 0 and from 31 at once (the lane's map ends, k_egad_lmap): the two coders step
+// together until they hold the same (i, c), after which the second is a copy of the first -- in a
+// dense row they meet within a few nibbles
+template <int WPL>
+__device__ __forceinline__ void eg_lane_nib2(const EgLane<WPL>& L, uint32_t used, uint32_t cols, const uint64_t* T,
+                                             uint32_t& lo, uint32_t& hi) {
+  NibCoder k0{0, 0}, k1{31, 0};
+  bool met = false;
+  auto none = [](uint32_t, uint32_t) {};
+  uint32_t col = (uint32_t)(L.jp + 1);
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = L.w0 + t;
+    const uint64_t x = L.R[t];
+    if (w >= used || !x) continue;
+    const uint32_t f1 = w * 64 + (uint32_t)__builtin_clzll(x), l1 = w * 64 + 63 - (uint32_t)__builtin_ctzll(x);
+    const uint32_t a = f1 & ~3u;
+    if (a > col) {
+      k0.zeros(a - col, none);
+      if (!met) k1.zeros(a - col, none);
+      met = met || (k0.i == k1.i && k0.c == k1.c);
+    }
+    for (uint32_t nb = a; nb <= l1; nb += 4) {
+      const uint32_t nib = (uint32_t)(x >> (60 - (nb - w * 64))) & 15u, n = nb + 3 <= l1 ? 4u : l1 - nb + 1;
+      k0.nibble(nib, n, T, none);
+      if (!met) {
+        k1.nibble(nib, n, T, none);
+        met = k0.i == k1.i && k0.c == k1.c;
+      }
+    }
+    col = l1 + 1;
+  }
+  if (L.eol) {
+    k0.zeros(cols - col, none);
+    if (!met) k1.zeros(cols - col, none);
+  }
+  lo = k0.i;
+  hi = met ? k0.i : k1.i;
+}
+
 // Every lane's start state for the row start s0 (lane 0 starts at s0): constant maps are known at
 // once; a round hands each known end to the next lane. Returns the lane's start; *end = its end.
 template <int WPL>
@@ -538,9 +578,7 @@ __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
   for (int t = 0; t < WPL; ++t) any |= L.R[t] != 0;
   uint32_t lo = kIdent, hi = kIdent;
   if (any) {
-    auto none = [](uint32_t, uint32_t) {};
-    lo = eg_lane_nib(L, a.used, a.cols, 0, sT, none);
-    hi = eg_lane_nib(L, a.used, a.cols, 31, sT, none);
+    eg_lane_nib2(L, a.used, a.cols, sT, lo, hi);
   }
   a.lane_lo[id * 64 + lane_id()] = (uint8_t)lo;
   a.lane_hi[id * 64 + lane_id()] = (uint8_t)hi;

@@ -90,9 +90,7 @@ constexpr uint32_t kKnownTable = BIC_KNOWN_PI ? 512u : 0u;
 #define BIC_SLOW_REST 1  // class kernels' path: the slow rows by k_emit_rest (listed by the LEN scan), no k_rows_global
 #endif
 constexpr bool kSlowRest = BIC_SLOW_REST != 0;
-#ifndef BIC_K01_MIX
-#define BIC_K01_MIX 0
-#endif
+
 // One lane's codewords for one residual word.
 struct LaneEnc {
   uint32_t head, k0, z;  // first codeword: k0-bit binary part, then z unary zeros
@@ -1176,7 +1174,10 @@ constexpr uint32_t kIterCap = (kWin - 8) * 32 - 128;  // bits one 64-word step m
 
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
-  __shared__ uint64_t sh_cnt[kTileRows], sh_pre[2];
+  // (sh_len apart from sh_cnt: a wave that finishes its length early must not overwrite the 1-counts
+  // a slower wave is still summing for its O -- one array for both raced: a wrong O, a wrong length,
+  // about 1 in 15 two-pass calls, tools/dbg_twopass.py)
+  __shared__ uint64_t sh_cnt[kTileRows], sh_len[kTileRows], sh_pre[2];
   __shared__ uint32_t sh_tile;
   __shared__ uint32_t s_lut[512];
   const Geom& g = a.g;
@@ -1254,11 +1255,11 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
         step_max = max(step_max, tot);
       }
     }
-    if (lane == 0) sh_cnt[wave] = L;
+    if (lane == 0) sh_len[wave] = L;
     __syncthreads();
     if (wave == 0) {
       uint64_t tile_bits = 0;
-      for (int q = 0; q < kTileRows; ++q) tile_bits += sh_cnt[q];
+      for (int q = 0; q < kTileRows; ++q) tile_bits += sh_len[q];
       uint64_t Gt = 0;
       if (trow == 0) {
         if (lane == 0) rec_store(&a.bits_rec[rid], kInc | tile_bits);
@@ -1272,7 +1273,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
     __syncthreads();
     if (valid && lane == 0) {
       uint64_t Grel = sh_pre[1];
-      for (int q = 0; q < wave; ++q) Grel += sh_cnt[q];
+      for (int q = 0; q < wave; ++q) Grel += sh_len[q];
       const uint64_t cap = a.slot_g * 64;
       a.gboff[id] = (uint64_t)plane * cap + Grel;
       if (row == g.rows - 1) a.bits_g[plane] = Grel + L;
@@ -2461,15 +2462,6 @@ __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   const uint32_t nw = gridDim.x * 4;
   // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
   const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-#if BIC_K01_MIX
-  // half of the waves take their k = 1 rows first: LDS- and issue-heavy rows beside the copies'
-  // memory traffic, instead of every wave in the same phase at once
-  if (i0 & 1) {
-    k1_rows<WPL>(a, i0, nw, gimg, s_lut);
-    k0_rows<WPL>(a, i0, nw);
-    return;
-  }
-#endif
   k0_rows<WPL>(a, i0, nw);
   k1_rows<WPL>(a, i0, nw, gimg, s_lut);
 }

@@ -61,15 +61,19 @@ void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t 
                  uint64_t* index, const uint64_t* nib);
 // the adaptive EG coder's nibble table (976 u64 entries), built on the host
 void egad_build_nib(uint64_t* T);
-constexpr size_t kLutEgadNib = 3 * 256;        // its offset in the context's byte-table buffer (u64 words)
-constexpr size_t kLutWords = kLutEgadNib + 976;  // the whole buffer
+constexpr size_t kLutEgadNib = 3 * 256;         // its offset in the context's byte-table buffer (u64 words)
+constexpr size_t kLutEgadDec = kLutEgadNib + 976;  // the decoder's table (992 u64 words)
+constexpr size_t kLutWords = kLutEgadDec + 992;    // the whole buffer
 // f1 decoders (bic_decode.hip)
 bool decode_supported(uint32_t cols);
 size_t decode_scratch_bytes(uint32_t rows, uint32_t wpr, uint32_t nplanes);
+// egnib: egad_build_dec_nib's table in device memory (the context's byte-table buffer, kLutEgadDec)
 void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t slot, const uint64_t* word_off,
                    const uint64_t* plane_bits, const uint64_t* index, const uint8_t* p00, uint32_t rows,
                    uint32_t cols, uint32_t wpr, uint32_t nplanes, int predict, uint64_t* out, void* scratch,
-                   uint32_t* flags);
+                   uint32_t* flags, const uint64_t* egnib);
+// the adaptive EG decoder's nibble table (62 states x 16 nibbles, u64), built on the host
+void egad_build_dec_nib(uint64_t* T);
 void launch_med_rows(hipStream_t s, const Geom& g, const uint64_t* planes, int predict, uint64_t* resid,
                      uint32_t* part, uint64_t* weight_out);
 void launch_golomb_bits(hipStream_t s, const Geom& g, const uint64_t* planes, int predict,
