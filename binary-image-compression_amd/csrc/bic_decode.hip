@@ -245,7 +245,8 @@ __host__ __device__ __forceinline__ uint32_t egad_dsidx(uint32_t i, uint32_t ph,
   if (i < 12) return 22u + (i - 8) * 3 + (k ? 1 + v : 0u);
   return 34u + (i - 12) * 7 + (k == 0 ? 0u : (k == 1 ? 1 + v : 3 + v));
 }
-// entry: the 1s (bit 39 - p: column col + p) | P << 40 | i << 46 | ph << 52 | k << 53 | v << 55; bit 63: escape
+// entry: the 1s (bit 39 - p: column col + p) | P << 40 | i << 46 (5 bits, 16: fresh) | ph << 51 | k << 52 |
+// v << 54 | the state's own table row << 57; bit 63: escape
 void egad_build_dec_nib(uint64_t* T) {
   for (uint32_t n = 0; n < 62 * 16; ++n) T[n] = 1ull << 63;
   auto fill = [&](uint32_t i0, uint32_t ph0, uint32_t k0, uint32_t v0) {
@@ -283,8 +284,9 @@ void egad_build_dec_nib(uint64_t* T) {
         esc = i != kFreshD && i >= 16;
       }
       if (!esc)
-        T[egad_dsidx(i0, ph0, k0, v0) * 16 + nib] = m | ((uint64_t)P << 40) | ((uint64_t)i << 46) |
-                                                     ((uint64_t)ph << 52) | ((uint64_t)k << 53) | ((uint64_t)v << 55);
+        T[egad_dsidx(i0, ph0, k0, v0) * 16 + nib] =
+            m | ((uint64_t)P << 40) | ((uint64_t)(i == kFreshD ? 16u : i) << 46) | ((uint64_t)ph << 51) |
+            ((uint64_t)k << 52) | ((uint64_t)v << 54) | ((uint64_t)egad_dsidx(i, ph, k, v) << 57);
     }
   };
   for (uint32_t i = 0; i < 16; ++i) fill(i, 0, 0, 0);
@@ -369,6 +371,7 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
   // the coder state: index i (kFreshD: a fresh coder, index 0 with g = 1, eg.h:9), phase ph (0: a
   // run's '1's, 1: its remainder after k of its g bits, value v); col: the row's next column
   uint32_t i = S0 == 32 ? kFreshD : (uint32_t)S0, ph = 0, k = 0, v = 0, col = 0;
+  uint32_t sid = (i < 16 || i == kFreshD) ? egad_dsidx(i, 0, 0, 0) : 64u;  // the state's table row (64: none)
   auto one = [&](uint32_t c) {  // the run's 1 at column c
     while ((c >> 6) > ow) flush();
     acc |= BIC_MSB >> (c & 63);
@@ -378,8 +381,8 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
       bad = true;
       break;
     }
-    if ((i < 16 || i == kFreshD) && col + 40 <= a.cols && used_bits + 4 <= len) {
-      const uint64_t e = sT[egad_dsidx(i, ph, k, v) * 16 + (uint32_t)(peek() >> 60)];
+    if (sid < 64 && col + 40 <= a.cols && used_bits + 4 <= len) {
+      const uint64_t e = sT[sid * 16 + (uint32_t)(peek() >> 60)];
       if (!(e >> 63)) {
         advance(4);
         const uint32_t P = (uint32_t)(e >> 40) & 63u;
@@ -395,10 +398,12 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
           }
         }
         col += P;
-        i = (uint32_t)(e >> 46) & 63u;
-        ph = (uint32_t)(e >> 52) & 1u;
-        k = (uint32_t)(e >> 53) & 3u;
-        v = (uint32_t)(e >> 55) & 7u;
+        i = (uint32_t)(e >> 46) & 31u;
+        i = i == 16 ? kFreshD : i;
+        ph = (uint32_t)(e >> 51) & 1u;
+        k = (uint32_t)(e >> 52) & 3u;
+        v = (uint32_t)(e >> 54) & 7u;
+        sid = (uint32_t)(e >> 57) & 63u;
         continue;
       }
     }
@@ -436,6 +441,7 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
         ph = 0;
       }
     }
+    sid = (i < 16 || i == kFreshD) ? egad_dsidx(i, ph, k, v) : 64u;
   }
   if (used_bits != len) bad = true;
   while (ow < a.used) flush();

@@ -19,6 +19,8 @@
 //            shared with neighbouring rows kept as fragments for the fixup kernel)
 #include "bic_device.h"
 
+#include <algorithm>
+
 namespace bic {
 
 // EGLUT = J[] (eg.cpp:2-10: 0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,5,5,6,6,7,7,8,9,...,15) in closed
@@ -54,6 +56,8 @@ struct EgadArgs {
   uint32_t* slow_n;
   uint32_t* slow_ids;
   const uint64_t* nib;  // egad_build_nib's table (kNibTable entries)
+  uint32_t* map_n;      // rows whose map k_egad_rmap could not prove constant (k_egad_lmap walks them)
+  uint32_t* map_ids;
 };
 
 // One run from state i: bits of its codeword, the new state. (eg.cpp:20-37 with incBlockSize.)
@@ -466,9 +470,11 @@ struct NibCoder {
 // The lane's runs from state s (its first run's start, column jp + 1, has an empty block): every
 // column from there through the lane's last 1 (and, on the row's last lane, through the row's end
 // and the end-of-row '1'). Returns the state after them.
+// (stop: return after the step that ends at that column -- a step boundary of this lane's walk, whose
+// boundaries do not depend on the state: eg_lane_nib2c's meeting point)
 template <int WPL, typename OUT>
 __device__ __forceinline__ uint32_t eg_lane_nib(const EgLane<WPL>& L, uint32_t used, uint32_t cols, uint32_t s,
-                                                const uint64_t* T, OUT&& out) {
+                                                const uint64_t* T, OUT&& out, uint32_t stop = 0xFFFFFFFFu) {
   NibCoder k{s, 0};
   uint32_t col = (uint32_t)(L.jp + 1);  // the next column to code
 #pragma unroll
@@ -478,15 +484,20 @@ __device__ __forceinline__ uint32_t eg_lane_nib(const EgLane<WPL>& L, uint32_t u
     if (w >= used || !x) continue;  // (zeros: coded by the next stretch)
     const uint32_t f1 = w * 64 + (uint32_t)__builtin_clzll(x), l1 = w * 64 + 63 - (uint32_t)__builtin_ctzll(x);
     const uint32_t a = f1 & ~3u;  // the nibble holding the word's first 1
-    if (a > col) k.zeros(a - col, out);  // (a >= col: col follows a 1 of an earlier word, or the row start)
+    if (a > col) {  // (a >= col: col follows a 1 of an earlier word, or the row start)
+      k.zeros(a - col, out);
+      if (a >= stop) return k.i;
+    }
     for (uint32_t nb = a; nb <= l1; nb += 4) {
-      const uint32_t nib = (uint32_t)(x >> (60 - (nb - w * 64))) & 15u;
-      k.nibble(nib, nb + 3 <= l1 ? 4u : l1 - nb + 1, T, out);
+      const uint32_t n = nb + 3 <= l1 ? 4u : l1 - nb + 1;
+      k.nibble((uint32_t)(x >> (60 - (nb - w * 64))) & 15u, n, T, out);
+      if (nb + n >= stop) return k.i;
     }
     col = l1 + 1;
   }
   if (L.eol) {
     k.zeros(cols - col, out);
+    if (cols >= stop) return k.i;
     out(1u, 1);  // end of row (eg.cpp:30-32: no decBlockSize)
   }
   return k.i;
@@ -495,12 +506,28 @@ __device__ __forceinline__ uint32_t eg_lane_nib(const EgLane<WPL>& L, uint32_t u
 // eg_lane_nib from 0 and from 31 at once (the lane's map ends, k_egad_lmap): the two coders step
 // together until they hold the same (i, c), after which the second is a copy of the first -- in a
 // dense row they meet within a few nibbles
-template <int WPL>
+// (COUNT: also the bits of the walk from 0 -- btot in all, bat of them before the meeting point X, the
+// column after the step where the two walks first hold the same state; X = ~0: they never meet. A walk
+// from any start lies between the two (each step is monotone in (i, c) ordered by i, then c), so it
+// has met them by X too, and its bits after X are btot - bat.)
+template <int WPL, bool COUNT = false>
 __device__ __forceinline__ void eg_lane_nib2(const EgLane<WPL>& L, uint32_t used, uint32_t cols, const uint64_t* T,
-                                             uint32_t& lo, uint32_t& hi) {
+                                             uint32_t& lo, uint32_t& hi, uint32_t* X = nullptr, uint32_t* btot = nullptr,
+                                             uint32_t* bat = nullptr) {
   NibCoder k0{0, 0}, k1{31, 0};
   bool met = false;
+  uint32_t nb0 = 0, mX = 0xFFFFFFFFu, mb = 0;
+  auto cnt = [&](uint32_t, uint32_t n) {
+    if constexpr (COUNT) nb0 += n;
+  };
   auto none = [](uint32_t, uint32_t) {};
+  auto check = [&](uint32_t pos) {
+    if (!met && k0.i == k1.i && k0.c == k1.c) {
+      met = true;
+      mX = pos;
+      mb = nb0;
+    }
+  };
   uint32_t col = (uint32_t)(L.jp + 1);
 #pragma unroll
   for (int t = 0; t < WPL; ++t) {
@@ -510,26 +537,33 @@ __device__ __forceinline__ void eg_lane_nib2(const EgLane<WPL>& L, uint32_t used
     const uint32_t f1 = w * 64 + (uint32_t)__builtin_clzll(x), l1 = w * 64 + 63 - (uint32_t)__builtin_ctzll(x);
     const uint32_t a = f1 & ~3u;
     if (a > col) {
-      k0.zeros(a - col, none);
+      k0.zeros(a - col, cnt);
       if (!met) k1.zeros(a - col, none);
-      met = met || (k0.i == k1.i && k0.c == k1.c);
+      check(a);
     }
     for (uint32_t nb = a; nb <= l1; nb += 4) {
       const uint32_t nib = (uint32_t)(x >> (60 - (nb - w * 64))) & 15u, n = nb + 3 <= l1 ? 4u : l1 - nb + 1;
-      k0.nibble(nib, n, T, none);
+      k0.nibble(nib, n, T, cnt);
       if (!met) {
         k1.nibble(nib, n, T, none);
-        met = k0.i == k1.i && k0.c == k1.c;
+        check(nb + n);
       }
     }
     col = l1 + 1;
   }
   if (L.eol) {
-    k0.zeros(cols - col, none);
+    k0.zeros(cols - col, cnt);
     if (!met) k1.zeros(cols - col, none);
+    check(cols);
+    cnt(1u, 1);
   }
   lo = k0.i;
   hi = met ? k0.i : k1.i;
+  if constexpr (COUNT) {
+    *X = mX;
+    *btot = nb0;
+    *bat = mb;
+  }
 }
 
 // Every lane's start state for the row start s0 (lane 0 starts at s0): constant maps are known at
@@ -566,11 +600,7 @@ __device__ __forceinline__ void nib_stage(const EgadArgs& a, uint64_t* sT) {
 
 // The lanes' maps and the row's map F_r(0), F_r(31) (lane 63 carries the row's end).
 template <int WPL>
-__global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
-  __shared__ uint64_t sT[kNibTable];
-  nib_stage(a, sT);
-  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (id >= (uint64_t)a.rows * a.nplanes) return;  // whole wave
+__device__ __forceinline__ void egad_lmap_row(const EgadArgs& a, uint64_t id, const uint64_t* sT) {
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
   bool any = L.eol;
@@ -580,8 +610,6 @@ __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
   if (any) {
     eg_lane_nib2(L, a.used, a.cols, sT, lo, hi);
   }
-  a.lane_lo[id * 64 + lane_id()] = (uint8_t)lo;
-  a.lane_hi[id * 64 + lane_id()] = (uint8_t)hi;
   uint32_t e0, e31;
   (void)eg_lane_chain(L, a.used, a.cols, lo, hi, 0, sT, &e0);
   (void)eg_lane_chain(L, a.used, a.cols, lo, hi, 31, sT, &e31);
@@ -589,6 +617,75 @@ __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
     a.lo_end[id] = (uint8_t)e0;
     a.hi_end[id] = (uint8_t)e31;
   }
+}
+
+// The row's map from a window at its end (k_egad_rmap, thread per row): the walks from 0 and 31 begin
+// after the first 1 of the row's last four words -- any state there lies between them -- and go to the
+// row's end; if they meet, F_r is constant and that is its value. A row of <= 4 words is walked whole
+// from its start (F_r(0) and F_r(31) exactly). Other rows (no 1 in the window, or the walks not met)
+// are listed for k_egad_lmap, which walks every lane of the row.
+__device__ __forceinline__ uint64_t egad_resid(const EgadArgs& a, uint32_t plane, uint32_t row, uint32_t w) {
+  if (w >= a.used) return 0;
+  const uint64_t* cur = a.planes + (uint64_t)plane * a.plane_words + (uint64_t)row * a.wpr;
+  uint64_t x = cur[w];
+  if (a.predict) {
+    const uint64_t* up = cur - a.wpr;
+    const uint64_t d = x ^ (row ? up[w] : 0ull);
+    const uint64_t dl = w ? cur[w - 1] ^ (row ? up[w - 1] : 0ull) : 0ull;
+    x = d ^ ((d >> 1) | (dl << 63));
+    if (row == 0 && w == 0) x &= ~BIC_MSB;  // pred.cpp never writes pP(0,0)
+  }
+  return w == a.used - 1 ? x & a.trail : x;
+}
+__global__ __launch_bounds__(256) void k_egad_rmap(EgadArgs a) {
+  __shared__ uint64_t sT[kNibTable];
+  nib_stage(a, sT);
+  const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (uint64_t)a.rows * a.nplanes) return;
+  const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
+  constexpr int K = 4;
+  EgLane<K> L;
+  L.w0 = a.used > K ? a.used - K : 0u;
+  L.eol = true;
+  L.jp = -1;
+#pragma unroll
+  for (int t = 0; t < K; ++t) L.R[t] = egad_resid(a, plane, row, L.w0 + t);
+  if (L.w0) {  // start after the window's first 1
+    bool found = false;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      if (!found && L.R[t]) {
+        const uint32_t b = (uint32_t)__builtin_clzll(L.R[t]);
+        L.jp = (int)((L.w0 + t) * 64 + b);
+        L.R[t] &= b == 63 ? 0ull : ~0ull >> (b + 1);
+        found = true;
+      } else if (!found) {
+        L.R[t] = 0;
+      }
+    }
+    if (!found) {
+      a.map_ids[atomicAdd(a.map_n, 1u)] = (uint32_t)id;
+      return;
+    }
+  }
+  uint32_t lo, hi;
+  eg_lane_nib2(L, a.used, a.cols, sT, lo, hi);
+  if (!L.w0 || lo == hi) {
+    a.lo_end[id] = (uint8_t)lo;
+    a.hi_end[id] = (uint8_t)hi;
+  } else {
+    a.map_ids[atomicAdd(a.map_n, 1u)] = (uint32_t)id;
+  }
+}
+
+// (the rows k_egad_rmap listed, a wave each)
+template <int WPL>
+__global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
+  __shared__ uint64_t sT[kNibTable];
+  nib_stage(a, sT);
+  const uint32_t nl = __hip_atomic_load(a.map_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t li = blockIdx.x * 4 + (threadIdx.x >> 6); li < nl; li += gridDim.x * 4)
+    egad_lmap_row<WPL>(a, a.map_ids[li], sT);
 }
 
 // The row's bits from its start state: per lane its start and bits, the row's total.
@@ -600,11 +697,21 @@ __global__ __launch_bounds__(256) void k_egad_llen(EgadArgs a) {
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
-  const uint32_t lo = a.lane_lo[id * 64 + lane_id()], hi = a.lane_hi[id * 64 + lane_id()];
+  // the lane's map ends (walks from 0 and 31 together, the one from 0 counted), its start from the
+  // row's, then its bits: a walk from the start up to the meeting point and the rest from the count
+  bool any = L.eol;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) any |= L.R[t] != 0;
+  uint32_t lo = kIdent, hi = kIdent, X = 0xFFFFFFFFu, btot = 0, bat = 0;
+  if (any) eg_lane_nib2<WPL, true>(L, a.used, a.cols, sT, lo, hi, &X, &btot, &bat);
+  a.lane_lo[id * 64 + lane_id()] = (uint8_t)lo;
   uint32_t end;
   const uint32_t s = eg_lane_chain(L, a.used, a.cols, lo, hi, a.start[id], sT, &end);
   uint32_t bits = 0;
-  if (lo != kIdent) (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t, uint32_t n) { bits += n; });
+  if (lo != kIdent) {
+    (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t, uint32_t n) { bits += n; }, X);
+    if (X != 0xFFFFFFFFu) bits += btot - bat;
+  }
   a.lane_st[id * 64 + lane_id()] = (uint8_t)s;
   a.lane_bits[id * 64 + lane_id()] = bits;
   const uint64_t tot = wave_sum_u64(bits);
@@ -699,7 +806,7 @@ __global__ __launch_bounds__(256) void k_egad_index(EgadArgs a, uint64_t* index)
 
 // len, boff, frag[2] (u64), lo_end, hi_end, start (u8); per (row, lane): lane_lo, lane_hi, lane_st
 // (u8), lane_bits (u32); the slow-row list and its count
-size_t egad_scratch_bytes(uint64_t nrows) { return nrows * (3 + 8 * 4) + nrows * 64 * 7 + nrows * 4 + 512; }
+size_t egad_scratch_bytes(uint64_t nrows) { return nrows * (3 + 8 * 4) + nrows * 64 * 7 + nrows * 4 * 2 + 512; }
 
 void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t cols, uint32_t wpr, uint32_t nplanes,
                  int predict, uint64_t* out, uint64_t slot, uint64_t* bits, void* scratch, uint32_t* flags,
@@ -731,6 +838,8 @@ void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t 
   a.lane_bits = reinterpret_cast<uint32_t*>(u);
   a.slow_ids = a.lane_bits + n * 64;
   a.slow_n = a.slow_ids + n;
+  a.map_n = a.slow_n + 1;  // (zeroed with slow_n)
+  a.map_ids = a.slow_n + 2;
   a.out = out;
   a.slot = slot;
   a.bits = bits;
@@ -745,9 +854,12 @@ void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t 
     if (out) k_egad_emit<<<grid, 256, 0, s>>>(a);
   } else {  // wave per row (4 rows per workgroup)
     const uint32_t wgrid = (uint32_t)((n + 3) / 4);
-    (void)hipMemsetAsync(a.slow_n, 0, 4, s);
+    (void)hipMemsetAsync(a.slow_n, 0, 8, s);
+    // row maps from windows (thread per row), the rows they cannot settle by their lanes (a wave each)
+    const uint32_t lgrid = (uint32_t)std::min<uint64_t>(wgrid, 2048);
 #define BIC_EGAD(W)                                   \
-  k_egad_lmap<W><<<wgrid, 256, 0, s>>>(a);            \
+  k_egad_rmap<<<grid, 256, 0, s>>>(a);                \
+  k_egad_lmap<W><<<lgrid, 256, 0, s>>>(a);            \
   k_egad_resolve<<<nplanes, 64, 0, s>>>(a);           \
   k_egad_llen<W><<<wgrid, 256, 0, s>>>(a);            \
   k_egad_scan<<<nplanes, 1024, 0, s>>>(a);            \

@@ -2080,6 +2080,9 @@ __device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) { ret
 #define BIC_K0_BATCH 4
 #endif
 constexpr int kK0Batch = BIC_K0_BATCH;
+#ifndef BIC_DIAG_K0
+#define BIC_DIAG_K0 0
+#endif
 #ifndef BIC_K0_PLACE_AHEAD
 #define BIC_K0_PLACE_AHEAD 0
 #endif
@@ -2121,7 +2124,12 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
     for (int k = 0; k <= WPL; ++k) {
       const int64_t j = r.si + 64 * k + lane;
       const int64_t jc = j > jend ? jend : j;
+#if BIC_DIAG_K0 == 2  // diagnostic build only (wrong output): the copies' loads from one cached line
+      v[k] = S[lane + (r.id & 1)];
+      (void)jc;
+#else
       v[k] = S[jc < 0 ? 0 : jc];
+#endif
     }
   };
   auto emit = [&](const Row& cur, uint64_t (&v)[WPL + 1]) {
@@ -2152,6 +2160,9 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
       const bool in = t < nwo;
       const bool whole = in && (t != 0 || gs == 0) && (t != nwo - 1 || ((cur.G + L) & 63) == 0);
       uint64_t* dst = whole ? a.out_g + w0 + t : (in ? a.gfrag + 2 * (uint64_t)cur.id + (t == 0 ? 0 : 1) : a.sink + lane);
+#if BIC_DIAG_K0 == 1  // diagnostic build only (wrong output): the copies' stores all to the sink
+      dst = a.sink + lane;
+#endif
       // (unsigned long long: a type apart from the u64 loads, so no load is taken to depend on it)
       class_store(dst, whole ? bswap64(x) : x);
     }

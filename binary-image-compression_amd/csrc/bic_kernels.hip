@@ -532,6 +532,9 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
 }
 
 // NP8: every plane of the image (no plane-count tests in the row loop)
+#ifndef BIC_DIAG_GS
+#define BIC_DIAG_GS 0
+#endif
 #ifndef BIC_GRAY_PREFETCH
 #define BIC_GRAY_PREFETCH 1
 #endif
@@ -730,6 +733,9 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
         uint64_t N = ~__builtin_bitreverse64(__ballot((gn >> b) & 1u));
         if (lastS) N = BIC_MSB | (rn < g.rows ? N >> 1 : 0ull);
         uint64_t* eb = eo + (uint64_t)b * eg_stride;
+#if BIC_DIAG_GS == 1  // diagnostic build only (wrong output): every wave's EG words to one 1 KB block
+        eb = out_e + (uint64_t)b * 128 + lane;
+#endif
         if (esh == 0) {
           eb[0] = bswap64(E);
           if (lastS && lane == 63) eb[1] = bswap64(N);  // the word the '1' opens (the next row's first)
