@@ -381,9 +381,10 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
       bad = true;
       break;
     }
-    if (sid < 64 && col + 40 <= a.cols && used_bits + 4 <= len) {
+    while (sid < 64 && col + 40 <= a.cols && used_bits + 4 <= len) {  // table steps while they apply
       const uint64_t e = sT[sid * 16 + (uint32_t)(peek() >> 60)];
-      if (!(e >> 63)) {
+      if (e >> 63) break;  // (escape: this nibble bit by bit)
+      {
         advance(4);
         const uint32_t P = (uint32_t)(e >> 40) & 63u;
         const uint64_t m = (e & 0xFFFFFFFFFFull) << 24;  // MSB-first: bit 63 is column col
@@ -404,8 +405,11 @@ __global__ __launch_bounds__(256) void k_dec_egad(DecArgs a) {
         k = (uint32_t)(e >> 52) & 3u;
         v = (uint32_t)(e >> 54) & 7u;
         sid = (uint32_t)(e >> 57) & 63u;
-        continue;
       }
+    }
+    if (used_bits > len) {
+      bad = true;
+      break;
     }
     const uint32_t bit = (uint32_t)(peek() >> 63);
     advance(1);

@@ -376,8 +376,10 @@ __device__ __forceinline__ void eg_lane_runs(const EgLane<WPL>& L, uint32_t cols
 constexpr uint32_t kNibStates = 61, kNibTable = kNibStates * 16;  // u64 entries
 static_assert(kNibTable == kLutEgadDec - kLutEgadNib, "the context's table buffer holds the nibble table");
 __host__ __device__ __forceinline__ uint32_t nib_j(uint32_t i) { return i < 16 ? i >> 2 : (i < 24 ? (i >> 1) - 4 : i - 16); }
+// (row of state (i, c), i <= 15: the band J = i / 4 starts at row 4 (2^J - 1) and holds 2^J rows per
+// index: ((i % 4 + 4) << J) - 4 + c -- arithmetic, no branch)
 __host__ __device__ __forceinline__ uint32_t nib_idx(uint32_t i, uint32_t c) {
-  return i == kFresh ? 60u : (i < 4 ? i : (i < 8 ? 4 + (i - 4) * 2 + c : (i < 12 ? 12 + (i - 8) * 4 + c : 28 + (i - 12) * 8 + c)));
+  return i == kFresh ? 60u : ((((i & 3u) | 4u) << (i >> 2)) - 4u + c);
 }
 // entry: bits (right-aligned, <= 20) | count << 24 | i' << 32 | c' << 40
 void egad_build_nib(uint64_t* T) {
@@ -723,27 +725,26 @@ __global__ __launch_bounds__(256) void k_egad_llen(EgadArgs a) {
 struct EgImgSink {
   uint64_t* img;
   uint32_t idx;
-  uint64_t cur;
+  uint64_t cur, nxt;  // image words idx and idx + 1 so far
   __device__ __forceinline__ void flush() {
-    lds_or64(img, idx, cur);
-    cur = 0;
+    if (cur) lds_or64(img, idx, cur);
+    if (nxt) lds_or64(img, idx + 1, nxt);
+    cur = nxt = 0;
   }
-  // the n (1..64) low bits of v at bit pos
+  // the n (1..32) low bits of v at bit pos; pos never moves back and by at most 32 per call, so the
+  // window only ever slides by one word (selects, one branch per 64 bits)
   __device__ __forceinline__ void put(uint32_t pos, uint64_t v, uint32_t n) {
-    const uint32_t i = pos >> 6, sh = pos & 63;
+    const uint32_t i = pos >> 6, e = (pos & 63) + n;
     if (i != idx) {
-      flush();
+      if (cur) lds_or64(img, idx, cur);
+      cur = i == idx + 1 ? nxt : 0ull;
+      if (i != idx + 1 && nxt) lds_or64(img, idx + 1, nxt);
+      nxt = 0;
       idx = i;
     }
-    if (n < 64) v &= (1ull << n) - 1ull;
-    if (sh + n <= 64) {
-      cur |= v << (64 - sh - n);
-    } else {
-      cur |= v >> (sh + n - 64);
-      flush();
-      idx = i + 1;
-      cur = v << (128 - sh - n);
-    }
+    v &= (1ull << n) - 1ull;
+    cur |= e <= 64 ? v << (64 - e) : v >> (e - 64);
+    nxt |= e > 64 ? v << ((128 - e) & 63) : 0ull;
   }
 };
 
@@ -771,7 +772,7 @@ __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   const uint32_t bits = a.lane_bits[id * 64 + lane_id()];
   uint32_t pos = wave_incl_sum_u32(bits) - bits;  // the lane's first bit in the row
   uint32_t s = a.lane_st[id * 64 + lane_id()];
-  EgImgSink k{img, 0, 0};
+  EgImgSink k{img, 0, 0, 0};
   if (a.lane_lo[id * 64 + lane_id()] != kIdent)
     (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t v, uint32_t n) {
       k.put(pos, v, n);
