@@ -29,7 +29,7 @@
 namespace bic {
 
 #ifdef BIC_STAMPS  // diagnostic build only (make stamps): per-wave phase clocks, never in the product
-__device__ unsigned long long g_stamps[1 << 21];
+__device__ unsigned long long g_stamps[1 << 22];
 // BIC_KNOWN=1 (diagnostic): replay the tile prefixes recorded by the previous normal launch
 // instead of looking them back, to measure what the look-back waits cost
 __device__ unsigned long long g_known[2][1 << 17];
@@ -46,12 +46,12 @@ __device__ unsigned long long g_known[2][1 << 17];
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
     if (threadIdx.x == 0 && (uint64_t)id * 8 + (slot) < (1u << 21)) g_stamps[(uint64_t)id * 8 + (slot)] = t_; \
   } while (0)
-// k_scan_rows' phases per workgroup (slots of g_stamps from 1 << 20: ONES scan, then LEN scan)
+// k_scan_rows' phases per workgroup (slots of g_stamps from 1 << 21: ONES scan, then LEN scan)
 #define SSTAMP(slot)                                                                              \
   do {                                                                                            \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                   \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                               \
-    if (threadIdx.x == 0) g_stamps[(1u << 20) + (ONES ? 0u : 8192u) + blockIdx.x * 8u + (slot)] = t_; \
+    if (threadIdx.x == 0) g_stamps[(1u << 21) + (ONES ? 0u : 8192u) + blockIdx.x * 8u + (slot)] = t_; \
   } while (0)
 #else
 #define STAMP(slot) \
