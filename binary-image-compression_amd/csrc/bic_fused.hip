@@ -2086,6 +2086,9 @@ constexpr int kK0Batch = BIC_K0_BATCH;
 #ifndef BIC_K0_PLACE_AHEAD
 #define BIC_K0_PLACE_AHEAD 0
 #endif
+#ifndef BIC_K0_PIPE
+#define BIC_K0_PIPE 0
+#endif
 // the k = 0 list's entries i0, i0 + nw, ... (one wave; i0 and nw wave-uniform)
 template <int WPL, int BATCH = kK0Batch>
 __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_t nw) {
@@ -2188,6 +2191,36 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
 #pragma unroll
     for (int u = 0; u < BATCH; ++u)
       if (k + u < R) emit(r[u], v[u]);
+  }
+#elif BIC_K0_PIPE
+  // software-pipelined: batch k + 1's loads issued before batch k's stores, so the wait for a batch's
+  // loads never covers the previous batch's stores (vmcnt counts both, in order)
+  Row ra[BATCH], rb[BATCH];
+  uint64_t va[BATCH][WPL + 1], vb[BATCH][WPL + 1];
+#pragma unroll
+  for (int u = 0; u < BATCH; ++u) {
+    ra[u] = place((uint32_t)u < R ? (uint32_t)u : 0u);
+    load(ra[u], va[u]);
+  }
+  for (uint32_t k = 0; k < R; k += 2 * BATCH) {
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const uint32_t kk = k + BATCH + u;
+      rb[u] = place(kk < R ? kk : k);
+      load(rb[u], vb[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u)
+      if (k + u < R) emit(ra[u], va[u]);
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const uint32_t kk = k + 2 * BATCH + u;
+      ra[u] = place(kk < R ? kk : k);
+      load(ra[u], va[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u)
+      if (k + BATCH + u < R) emit(rb[u], vb[u]);
   }
 #else
   for (uint32_t k = 0; k < R; k += BATCH) {

@@ -535,6 +535,13 @@ __device__ __forceinline__ void gray_to_planes(const uint4 (&v)[4], uint64_t (&p
 #ifndef BIC_DIAG_GS
 #define BIC_DIAG_GS 0
 #endif
+#ifndef BIC_GS_NT
+#define BIC_GS_NT 0  // the count pass's EG words: 1 = non-temporal stores
+#endif
+__device__ __forceinline__ void eg_store(uint64_t* p, uint64_t v) {
+  if constexpr (BIC_GS_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 #ifndef BIC_GRAY_PREFETCH
 #define BIC_GRAY_PREFETCH 1
 #endif
@@ -737,13 +744,13 @@ __device__ __forceinline__ void gray_strip_rows(const uint8_t* __restrict__ gray
         eb = out_e + (uint64_t)b * 128 + lane;
 #endif
         if (esh == 0) {
-          eb[0] = bswap64(E);
+          eg_store(eb, bswap64(E));
           if (lastS && lane == 63) eb[1] = bswap64(N);  // the word the '1' opens (the next row's first)
         } else {
           uint64_t En = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(E >> 32), 0x130, 0xf, 0xf, true) << 32) |
                         (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)E, 0x130, 0xf, 0xf, true);
           if (lane == 63) En = N;
-          eb[1] = bswap64(funnel64(E, En, esh));
+          eg_store(eb + 1, bswap64(funnel64(E, En, esh)));
           if (row == 0 && s == 0 && lane == 0) eb[0] = bswap64(BIC_MSB | (E >> 1));  // stream bit 0, row 0
         }
       }
