@@ -2077,7 +2077,7 @@ __device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) { ret
 // Output word t of the row (at bit Gb) holds row bits [64 t - g, 64 t - g + 64), g = Gb % 64: the
 // stream bits from Bsrc + 64 t - g (Bsrc: the row in the EG slot), one funnel shift per word.
 #ifndef BIC_K0_BATCH
-#define BIC_K0_BATCH 4
+#define BIC_K0_BATCH 3  // (pipelined batches of 3: C3 emission 162-165 -> 157-158 us; of 2: 159-162; of 4: 170-173)
 #endif
 constexpr int kK0Batch = BIC_K0_BATCH;
 #ifndef BIC_DIAG_K0
@@ -2087,7 +2087,7 @@ constexpr int kK0Batch = BIC_K0_BATCH;
 #define BIC_K0_PLACE_AHEAD 0
 #endif
 #ifndef BIC_K0_PIPE
-#define BIC_K0_PIPE 0
+#define BIC_K0_PIPE 1
 #endif
 // the k = 0 list's entries i0, i0 + nw, ... (one wave; i0 and nw wave-uniform)
 template <int WPL, int BATCH = kK0Batch>
