@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
   if (a.ctot)
     for (uint32_t i = threadIdx.x; i < 4 * kDecRowWords; i += blockDim.x) (&csum[0][0])[i] = 0;
   __syncthreads();
-  uint64_t* cs = csum[threadIdx.x >> 6];
+  uint64_t* cs = csum[wave_id()];
   const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const bool inrow = id < (uint64_t)a.rows * a.nplanes;
   const uint32_t plane = inrow ? (uint32_t)(id / a.rows) : 0, row = inrow ? (uint32_t)(id % a.rows) : 0;
@@ -806,7 +806,7 @@ __global__ __launch_bounds__(256) void k_dec_golomb_nib(DecArgs a) {
 // EG: the row holding each plane's first residual 1 = the first row whose cols + 1 bits at the
 // unshifted offset row * (cols + 1) are not all '1' (rows before it are ~0 and their '1').
 __global__ __launch_bounds__(256) void k_dec_eg_first(DecArgs a) {
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + wave_id();
   if (gw >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(gw / a.rows), row = (uint32_t)(gw % a.rows);
   const uint64_t* st = plane_stream(a, plane);
@@ -835,7 +835,7 @@ __global__ __launch_bounds__(256) void k_dec_eg_first(DecArgs a) {
 
 __global__ __launch_bounds__(256) void k_dec_eg_rows(DecArgs a) {
   const int lane = lane_id();
-  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t id = (uint64_t)blockIdx.x * 4 + wave_id();
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const uint64_t* st = plane_stream(a, plane);
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(256) void k_col_scan_par(uint64_t* __restrict__ cto
   const uint32_t nch = (rows + kColChunk - 1) / kColChunk;
   const uint32_t w = blockIdx.x % wpr, plane = blockIdx.x / wpr;
   uint64_t* p = ctot + (uint64_t)plane * nch * wpr + w;
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const int lane = lane_id(), wv = (int)wave_id();
   uint64_t carry = 0;
   for (uint32_t c0 = 0; c0 < nch; c0 += 256) {
     const uint32_t c = c0 + threadIdx.x;

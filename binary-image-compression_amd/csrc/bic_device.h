@@ -22,6 +22,10 @@ __device__ __forceinline__ uint32_t uni_u32(uint32_t v) { return (uint32_t)__bui
 __device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
   return ((uint64_t)uni_u32((uint32_t)(v >> 32)) << 32) | uni_u32((uint32_t)v);
 }
+// the wave's index in its workgroup as a wave-uniform value: the compiler takes threadIdx.x >> 6 for
+// divergent, and every row / plane / offset derived from it (and every branch on those) would then be
+// vector work under exec masks (C3 count pass: 2,530 -> 2,323 VALU instructions, 56 -> 50 VGPRs)
+__device__ __forceinline__ uint32_t wave_id() { return uni_u32(threadIdx.x >> 6); }
 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   const uint32_t lo = __shfl((unsigned)(v & 0xffffffffu), src);
@@ -183,7 +187,7 @@ __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) {
 // Exclusive block scan for blockDim.x <= 1024 (<= 16 waves). tmp: >= 17 entries of LDS.
 template <typename T>
 __device__ __forceinline__ T block_excl_scan(T x, T* tmp, T& total) {
-  const int l = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int l = lane_id(), w = (int)wave_id(), nw = blockDim.x >> 6;
   T inc;
   if constexpr (sizeof(T) == 8) inc = wave_incl_sum_u64(x);
   else inc = wave_incl_sum_u32(x);
@@ -484,7 +488,7 @@ struct ChunkId {
 __device__ __forceinline__ ChunkId chunk_id(const Geom& g) {
   ChunkId ci;
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-  ci.id = (uint64_t)b * kWaves + (threadIdx.x >> 6);
+  ci.id = (uint64_t)b * kWaves + wave_id();
   ci.ok = ci.id < g.nchunks;
   const uint64_t id = ci.ok ? ci.id : 0;
   ci.plane = (uint32_t)(id / g.chunks_per_plane);

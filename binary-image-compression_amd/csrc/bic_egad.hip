@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256) void k_egad_lmap(EgadArgs a) {
   __shared__ uint64_t sT[kNibTable];
   nib_stage(a, sT);
   const uint32_t nl = __hip_atomic_load(a.map_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t li = blockIdx.x * 4 + (threadIdx.x >> 6); li < nl; li += gridDim.x * 4)
+  for (uint32_t li = blockIdx.x * 4 + wave_id(); li < nl; li += gridDim.x * 4)
     egad_lmap_row<WPL>(a, a.map_ids[li], sT);
 }
 
@@ -695,7 +695,7 @@ template <int WPL>
 __global__ __launch_bounds__(256) void k_egad_llen(EgadArgs a) {
   __shared__ uint64_t sT[kNibTable];
   nib_stage(a, sT);
-  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t id = (uint64_t)blockIdx.x * 4 + wave_id();
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint32_t plane = (uint32_t)(id / a.rows), row = (uint32_t)(id % a.rows);
   const EgLane<WPL> L = eg_lane_load<WPL>(a, plane, row);
@@ -753,7 +753,7 @@ __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t imgs[4][kEgImg];
   __shared__ uint64_t sT[kNibTable];
   nib_stage(a, sT);
-  const uint64_t id = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t id = (uint64_t)blockIdx.x * 4 + wave_id();
   if (id >= (uint64_t)a.rows * a.nplanes) return;
   const uint64_t Ltot = a.len[id];
   if (Ltot == 0) return;  // past the slot (BIC_ENOSPC)
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
     if (lane_id() == 0) a.slow_ids[atomicAdd(a.slow_n, 1u)] = (uint32_t)id;
     return;
   }
-  uint64_t* img = imgs[threadIdx.x >> 6];
+  uint64_t* img = imgs[wave_id()];
   for (uint32_t i = lane_id(); i < kEgImg; i += 64) img[i] = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -926,7 +926,7 @@ __global__ __launch_bounds__(256) void k_rows_global(FusedArgs a) {
   const int lane = lane_id();
   if (!a.out_g) eg_fix_bit(a.esrc ? a.efix : nullptr, a.out_e, a.slot_e, a.g.nplanes);
   const uint32_t nslow = *a.slow_n;
-  for (uint32_t li = blockIdx.x * 4 + (threadIdx.x >> 6); li < nslow; li += gridDim.x * 4)
+  for (uint32_t li = blockIdx.x * 4 + wave_id(); li < nslow; li += gridDim.x * 4)
     row_global<PREDICT>(a, a.slow_ids[li], lane);
 }
 
@@ -943,6 +943,8 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_encode_rows(FusedArgs a) 
   __shared__ uint32_t sh_tile;
   __shared__ uint32_t s_lut[512];  // k = 1, 2 byte tables
   const Geom& g = a.g;
+  // (the wave index left divergent here: as a scalar the compiler re-schedules this kernel's row loop
+  // and C2 measured 0.032 -> 0.033-0.035 ms)
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* gimg = lds + wave * (kGImg + kEImg);
   uint32_t* eimg = gimg + kGImg;
@@ -1181,7 +1183,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_len_rows(FusedArgs a) {
   __shared__ uint32_t sh_tile;
   __shared__ uint32_t s_lut[512];
   const Geom& g = a.g;
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const int lane = lane_id(), wave = (int)wave_id();
   const uint32_t tpp = (g.rows + kTileRows - 1) / kTileRows;
   if (threadIdx.x == 0) sh_tile = atomicAdd(a.counter, 1u);
   if (DO_G && threadIdx.x < 512) s_lut[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lut + 256)[threadIdx.x];
@@ -1328,7 +1330,7 @@ __global__ __launch_bounds__(64 * kTileRows, 8) void k_emit_rows(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kTileRows * kWin];
   __shared__ uint32_t s_lut[512];
   const Geom& g = a.g;
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const int lane = lane_id(), wave = (int)wave_id();
   uint32_t* win = lds + wave * kWin;
   if (DO_G && threadIdx.x < 512) s_lut[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lut + 256)[threadIdx.x];
   __syncthreads();  // the only workgroup barrier
@@ -1708,7 +1710,7 @@ struct WideRow {
   uint32_t ones;
 };
 __device__ __forceinline__ WideRow wide_prefix(uint64_t x, uint32_t w, uint32_t nbase, uint32_t* sh) {
-  const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = lane_id(), v = (int)wave_id(), nw = blockDim.x >> 6;
   const uint32_t pc = (uint32_t)__popcll(x), inc = wave_incl_sum_u32(pc);
   const int mx = wave_incl_max(x ? (int)(w * 64 + 63 - __builtin_ctzll(x)) : -1);
   if (lane == 63) {
@@ -1761,7 +1763,7 @@ template <bool PREDICT>
 __global__ __launch_bounds__(512) void k_row_walk(FusedArgs a) {
   __shared__ uint32_t sh[16], sl[8], sk[8];
   const Geom& g = a.g;
-  const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = lane_id(), v = (int)wave_id(), nw = blockDim.x >> 6;
   const uint32_t w = (64 * v + lane) / kWalkSplit, h = kWalkSplit == 1 ? 1u : (uint32_t)lane & 1u;
   const uint64_t hmask = kWalkSplit == 1 ? ~0ull : (h ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull);
   const uint32_t nlist = __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1865,7 +1867,7 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
   STAMP(1);
 #ifdef BIC_STAMPS
   if (lane == 0) g_stamps[id * 8 + 3] = (k0 ? 1u : 0u) | (gk1 ? 2u : 0u) | ((uint64_t)blockIdx.x << 8) |
-                                        ((uint64_t)(threadIdx.x >> 6) << 40);
+                                        ((uint64_t)wave_id() << 40);
 #endif
   if constexpr (DO_G) {
     if (k0 && L) {
@@ -1972,7 +1974,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
   __shared__ uint32_t s_lut[512];
   const Geom& g = a.g;
   [[maybe_unused]] const int lane = lane_id();
-  const int wave = threadIdx.x >> 6;
+  const int wave = (int)wave_id();
   uint32_t* gimg = lds + wave * kGImg;
   if (DO_G)
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kKnownTable + i];
@@ -2499,13 +2501,13 @@ __global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
   __shared__ uint32_t s_lut[512];
   const int lane = lane_id();
-  uint32_t* gimg = lds + (threadIdx.x >> 6) * kGImg;
+  uint32_t* gimg = lds + wave_id() * kGImg;
   // every wave writes the whole table itself (the same values as the others): its own reads then
   // follow its own writes, and the kernel needs no workgroup barrier
   for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
   const uint32_t nw = gridDim.x * 4;
   // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
-  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
   k0_rows<WPL>(a, i0, nw);
   k1_rows<WPL>(a, i0, nw, gimg, s_lut);
 }
@@ -2522,7 +2524,7 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
   __shared__ uint32_t sh[16];  // (wide_prefix: up to 8 waves)
   __shared__ int sf[4];
   const Geom& g = a.g;
-  const int lane = lane_id(), v = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = lane_id(), v = (int)wave_id(), nw = blockDim.x >> 6;
   const uint32_t w = 64 * v + lane;
   if (DO_G)
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];

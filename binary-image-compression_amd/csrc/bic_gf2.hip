@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void k_gf2_transpose(const uint64_t* __restric
                                                        uint32_t d_words) {
   const int lane = lane_id();
   const uint32_t wb = blockIdx.x;                            // source word column
-  const uint32_t rb = blockIdx.y * 4 + (threadIdx.x >> 6);   // source row block = destination word
+  const uint32_t rb = blockIdx.y * 4 + wave_id();   // source row block = destination word
   if (rb >= d_words) return;                                    // wave-uniform
   const uint32_t r = rb * 64 + lane;
   const uint64_t x = (r < s_rows && wb < s_words) ? src[(uint64_t)r * s_stride + wb] : 0ull;

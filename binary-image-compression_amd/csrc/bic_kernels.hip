@@ -41,7 +41,7 @@ __global__ __launch_bounds__(kBlock) void k_bitplanes_u8(const uint8_t* __restri
                                                          int plane0, int nplanes, uint64_t* __restrict__ planes,
                                                          uint32_t wpr) {
   const uint32_t groups = (used + 63) / 64;  // 64-word groups per row
-  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave_id();
   if (gw >= (uint64_t)rows * groups) return;
   const uint32_t row = (uint32_t)(gw / groups), w = (uint32_t)(gw % groups) * 64 + lane_id();
   if (w >= used) return;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_med_rows(Geom g, const uint64_t* __r
                                                      uint64_t* __restrict__ resid, uint32_t* __restrict__ part) {
   const int lane = lane_id();
   const uint32_t wpp = (g.rows + RPW - 1) / RPW;  // waves per plane
-  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + wave_id();
   if (gw >= (uint64_t)wpp * g.nplanes) return;
   const uint32_t plane = (uint32_t)(gw / wpp), r0 = (uint32_t)(gw % wpp) * RPW;
   const uint64_t* pl = planes + (uint64_t)plane * g.plane_words;
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void k_med_kstat(Geom g, const uint64_t* __
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   const int lane = lane_id();
   const uint32_t wpp = (g.rows + RPW - 1) / RPW;  // waves per plane
-  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + wave_id();
   if (gw >= (uint64_t)wpp * g.nplanes) return;  // whole wave
   const uint32_t plane = (uint32_t)(gw / wpp), r0 = (uint32_t)(gw % wpp) * RPW;
   const uint64_t* pl = planes + (uint64_t)plane * g.plane_words;
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void k_med_kstat16(Geom g, const uint64_t* 
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
   const int lane = lane_id(), q = lane & 15, grp = lane >> 4;
   const uint32_t wpp = (g.rows + RPW - 1) / RPW;  // waves per plane
-  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + wave_id();
   if (gw >= (uint64_t)wpp * g.nplanes) return;  // whole wave
   const uint32_t plane = (uint32_t)(gw / wpp), r0 = (uint32_t)(gw % wpp) * RPW;
   const uint64_t* pl = planes + (uint64_t)plane * g.plane_words;
@@ -782,8 +782,11 @@ __global__ __launch_bounds__(kBlock, BIC_GRAY_WAVES) void k_gray_strips(const ui
                                                         uint64_t* __restrict__ out_e, uint64_t eg_stride) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[kWaves][1024];  // strip_word_put tables
   if (blockIdx.x == 0 && threadIdx.x < kZeroWords) zero[threadIdx.x] = 0;  // the encoder's counters
-  uint32_t* tw = tab[threadIdx.x >> 6];
-  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+  // the wave's index as a scalar: its strip, rows, stream offsets and branches are then wave-uniform
+  // values in SGPRs (scalar branches, no exec-mask juggling around the EG stores)
+  const uint32_t wv = wave_id();
+  uint32_t* tw = tab[wv];
+  const uint64_t gw = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * kWaves + wv;
   const uint32_t s = (uint32_t)(gw % ns);  // the strips of one row block are neighbouring waves
   const uint32_t r0 = (uint32_t)(gw / ns) * gray_rows_per_wave<PREDICT, STORE_R>();
   if (r0 >= g.rows) return;  // whole wave
@@ -1076,7 +1079,7 @@ __global__ __launch_bounds__(kBlock) void k_golomb_emit(Geom g, const uint64_t* 
   const ChunkId ci = chunk_id(g);
   if (!ci.ok) return;
   const int lane = lane_id();
-  uint32_t* lds = lds_all + (threadIdx.x >> 6) * kLdsWords;
+  uint32_t* lds = lds_all + wave_id() * kLdsWords;
   const uint64_t L = cs.bits[ci.id];
   const uint64_t cb = cs.boff[ci.id];
   const uint64_t slot_end = ((uint64_t)ci.plane + 1) * slot_words * 64;
@@ -1424,7 +1427,7 @@ __global__ __launch_bounds__(kBlock) void k_tiles(const uint64_t* __restrict__ p
   __shared__ uint32_t pc_o[kBlock], pc_O[kBlock];
   __shared__ uint8_t sel[kBlock];
   __shared__ uint64_t red[2][kWaves];
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const int lane = lane_id(), wave = (int)wave_id();
   const uint32_t tpw = 64 / W;
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave;
   const uint32_t tloc = lane / W, r = lane % W;
@@ -1503,7 +1506,7 @@ __global__ __launch_bounds__(kBlock) void k_tiles_aligned(const uint64_t* __rest
                                                           uint64_t* resid, unsigned long long* stats) {
   constexpr int T = 64 / W;
   const int lane = lane_id();
-  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave_id();
   const uint32_t groups = (used + 63) / 64;
   const uint32_t ty = (uint32_t)(gw / groups), w = (uint32_t)(gw % groups) * 64 + lane;
   if (ty >= rows / W) return;  // wave-uniform
@@ -1578,7 +1581,7 @@ __global__ __launch_bounds__(256) void k_tiles_split(const uint64_t* __restrict_
                                                      uint64_t* resid, uint64_t* lpart, uint32_t* zero, uint32_t nzero) {
   constexpr int T = 64 / W, RW = W / 4;
   __shared__ uint32_t part[4][T][2][64];
-  const int lane = lane_id(), v = threadIdx.x >> 6;
+  const int lane = lane_id(), v = (int)wave_id();
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nzero; i += gridDim.x * 256) zero[i] = 0;
   const uint32_t groups = (used + 63) / 64;
   const uint32_t ty = blockIdx.x / groups, w = (blockIdx.x % groups) * 64 + lane;
@@ -1809,7 +1812,7 @@ __global__ __launch_bounds__(kBlock) void k_patch_search(FlatImage img, uint32_t
     const unsigned long long o = shfl_u64(best, lane_id() ^ dd);
     best = o < best ? o : best;
   }
-  if (lane_id() == 0) red[threadIdx.x >> 6] = best;
+  if (lane_id() == 0) red[wave_id()] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int q = 1; q < kWaves; ++q) best = red[q] < best ? red[q] : best;
@@ -1876,7 +1879,7 @@ __global__ __launch_bounds__(kBlock) void k_patch_search_w(FlatImage img, uint32
     const unsigned long long o = shfl_u64(best, lane_id() ^ dd);
     best = o < best ? o : best;
   }
-  if (lane_id() == 0) red[threadIdx.x >> 6] = best;
+  if (lane_id() == 0) red[wave_id()] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int q = 0; q < kWaves; ++q) best = red[q] < best ? red[q] : best;

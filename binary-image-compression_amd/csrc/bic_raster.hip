@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void k_raster_planes(const uint8_t* __restrict
                                                        uint32_t cols, int plane0, int nplanes,
                                                        uint64_t* __restrict__ planes, uint32_t wpr) {
   const uint32_t groups = (cols + 4095) / 4096;  // 64-word groups per row
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + wave_id();
   if (gw >= (uint64_t)rows * groups) return;
   const uint32_t row = (uint32_t)(gw / groups), w = (uint32_t)(gw % groups) * 64 + lane_id();
   const uint32_t used = (cols + 63) / 64;
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void k_planes_gray(const uint64_t* __restrict_
                                                      uint32_t wpr, int plane0, int nplanes, uint8_t* __restrict__ gray,
                                                      uint64_t pitch) {
   const uint32_t groups = (cols + 4095) / 4096;
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + wave_id();
   if (gw >= (uint64_t)rows * groups) return;
   const uint32_t row = (uint32_t)(gw / groups), w = (uint32_t)(gw % groups) * 64 + lane_id();
   const uint32_t used = (cols + 63) / 64;
