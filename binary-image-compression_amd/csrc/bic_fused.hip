@@ -2497,7 +2497,10 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
 // byte-table rows (issue-bound) run side by side instead of one launch after the other. (Odd waves
 // starting on the k = 1 rows measured 196-198 µs against 192-193, round 4.)
 template <int WPL>
-__global__ __launch_bounds__(256) void k_emit_k01(FusedArgs a) {
+#ifndef BIC_K01_OCC
+#define BIC_K01_OCC 0  // (A/B: a minimum of workgroups per CU for k_emit_k01; 0: none)
+#endif
+__global__ __launch_bounds__(256, BIC_K01_OCC ? BIC_K01_OCC : 1) void k_emit_k01(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
   __shared__ uint32_t s_lut[512];
   const int lane = lane_id();
