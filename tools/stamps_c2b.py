@@ -43,5 +43,15 @@ for pi, pl in enumerate(planes):
     top = np.argsort(end)[-6:][::-1]
     for r in top:
         print(f"   row {r:5d} start {S[r, 0] - t0:7d} end {end[r]:7d} phases {list(d[r])} s7 {S[r, 7]}")
+    s7 = S[:, 7]
+    p1 = s7 // 1000000
+    p3 = s7 % 1000
+    lng = (s7 // 1000) % 1000
+    for nm_, sel in (("all copy-path words", ok & (p1 == 64)), ("no copy-path word", ok & (p1 == 0)),
+                     ("mixed paths", ok & (p1 > 0) & (p1 < 64)), ("any per-codeword word", ok & (p3 > 0))):
+        if sel.any():
+            print(f"   {nm_:22s} rows {sel.sum():5d}  emit median {np.median(d[sel][:, 4]):7.0f}  len median {np.median(d[sel][:, 2]):7.0f}"
+                  f"  bits lb median {np.median(d[sel][:, 3]):7.0f}")
+    print(f"   per-codeword words per row: mean {p3[ok].mean():.2f}; long words {lng[ok].sum()}")
     print(f"   rows by end > 20k clk: {(end > 20000).sum()}, start offsets median {np.median(S[ok, 0] - t0):.0f} max {(S[ok, 0] - t0).max()}",
           flush=True)
