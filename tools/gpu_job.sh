@@ -1,5 +1,7 @@
 # tools/gpu_job.sh: one GPU call of this session's A/B and diagnostic steps (edited per call)
 set -o pipefail
 export TMPDIR=/tmp
-timeout -k 10 120 python3 tools/stamps_c2b.py > gpurun_out/stamps_c2b.log 2>&1 || { tail -20 gpurun_out/stamps_c2b.log; exit 1; }
-grep -v "amdgpu.ids\|   row " gpurun_out/stamps_c2b.log
+bash tools/ab.sh "--steps 50 --warmup 5 --workload c2" cur nar s8 nar8 || exit 1
+for v in nar nar8; do
+BIC_LIB_PATH=binary-image-compression_amd/lib/var_$v.so timeout -k 10 180 python3 tools/c2_alt.py 2>&1 | grep -v amdgpu.ids | head -4
+done
