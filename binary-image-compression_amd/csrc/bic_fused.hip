@@ -2169,7 +2169,10 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
       dst = a.sink + lane;
 #endif
       // (unsigned long long: a type apart from the u64 loads, so no load is taken to depend on it)
-      class_store(dst, whole ? bswap64(x) : x);
+      // Only the last word group has lanes past the row (the row's 257-258 words of C3): those store
+      // nothing (exec-masked, the instruction count unchanged) instead of writing the sink (emission
+      // 158-161 -> 155-160 us on one box)
+      if (k < WPL || in) class_store(dst, whole ? bswap64(x) : x);
     }
   };
   // rows in batches of BATCH: every row's loads issued before the first row's stores, so a wave

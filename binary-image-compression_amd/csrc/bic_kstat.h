@@ -115,7 +115,17 @@ __device__ __forceinline__ void strip_word_put(uint32_t* t, int b, uint64_t x, i
   const int lane = lane_id();
   // branch-free: x = 0 gives m = 0 (strip_records then ignores c)
   const uint32_t m = (uint32_t)__popcll(x) | (parity_changes(x) << 8);
-  const uint32_t c = (uint32_t)(c0 + __clzll((long long)x)) | ((uint32_t)(c0 + 64 - __ffsll((long long)x)) << 16);
+  // first / last 1 from the raw find-first-bit instructions (-1 for a zero half, so min() picks the
+  // other half); an all-zero word gives garbage here, which strip_records ignores (m = 0). Four
+  // instructions fewer per plane than clz / ffs with their zero cases
+  uint32_t hh, hl, lh, ll;
+  const uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
+  asm volatile("v_ffbh_u32 %0, %1" : "=v"(hh) : "v"(xh));
+  asm volatile("v_ffbh_u32 %0, %1" : "=v"(hl) : "v"(xl));
+  asm volatile("v_ffbl_b32 %0, %1" : "=v"(lh) : "v"(xh));
+  asm volatile("v_ffbl_b32 %0, %1" : "=v"(ll) : "v"(xl));
+  const uint32_t lz = min(hh, hl + 32u), tz = min(ll, lh + 32u);
+  const uint32_t c = ((uint32_t)c0 + lz) | (((uint32_t)c0 + 63u - tz) << 16);
   // lane l's value is value i = l & 7 of part 8b + (l >> 3): stored at word (i >> 2) * 256 +
   // 4 * part + (i & 3), so that strip_records' 16-byte reads (lane L: words 4L..4L+3 of each
   // quarter) are bank-conflict free

@@ -1,7 +1,7 @@
 # tools/gpu_job.sh: one GPU call of this session's A/B and diagnostic steps (edited per call)
 set -o pipefail
 export TMPDIR=/tmp
-bash tools/ab.sh "--steps 50 --warmup 5 --workload c2" cur nar s8 nar8 || exit 1
-for v in nar nar8; do
-BIC_LIB_PATH=binary-image-compression_amd/lib/var_$v.so timeout -k 10 180 python3 tools/c2_alt.py 2>&1 | grep -v amdgpu.ids | head -4
-done
+BIC_LIB_PATH=binary-image-compression_amd/lib/var_both.so timeout -k 10 300 python -u -m pytest tests/test_gpu_egsrc.py tests/test_gpu_fullsize.py -q -x --timeout 200 --timeout-method thread > gpurun_out/gpu_both.log 2>&1 || { tail -30 gpurun_out/gpu_both.log; exit 1; }
+tail -1 gpurun_out/gpu_both.log
+bash tools/ab.sh "--steps 20 --warmup 3" base nosink ffb both || exit 1
+bash tools/ab.sh "--steps 20 --warmup 3" base nosink ffb both || exit 1
