@@ -36,6 +36,10 @@ struct bic_ctx {
   // clears its counter and look-back records for the next call); ensure_scratch hands the value to
   // its caller (scratch_zero_prev) and resets it, since any other user may dirty the arena
   size_t scratch_zero = 0, scratch_zero_prev = 0;
+  // a call was enqueued under stream capture: graph replays then run work this bookkeeping never sees
+  // (a captured call leaves nothing zeroed when enqueued, and a replay may dirty the arena between two
+  // eager calls), so from then on every single / two-pass call clears the records itself
+  bool captured = false;
   uint64_t* lut = nullptr;        // device [3][256] byte table of the fused encoder
   uint32_t* flags = nullptr;      // device [4]: overflow, domain, look-back timeout, internal length check
   uint64_t* lentab = nullptr;     // device copy of the tile length table
@@ -341,7 +345,7 @@ int bic_memset(bic_ctx* ctx, void* dst, int value, size_t bytes) {
   if (rc) return rc;
   if (bytes == 0) return BIC_OK;
   if (!dst) return BIC_EINVAL;
-  BIC_HIP(hipMemsetAsync(dst, value, bytes, ctx->cur));
+  BIC_HIP((bic::launch_fill(ctx->cur, dst, value, bytes), hipGetLastError()));
   return BIC_OK;
 }
 
@@ -401,7 +405,7 @@ int bic_med_residual(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t r
   int rc = bind(ctx);
   if (rc) return rc;
   if (nplanes < 1 || !geom_ok(rows, cols, wpr) || (rows && !planes)) return BIC_EINVAL;
-  if (weight_out) BIC_HIP(hipMemsetAsync(weight_out, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+  if (weight_out) BIC_HIP((bic::launch_fill(ctx->cur, weight_out, 0, sizeof(uint64_t) * nplanes), hipGetLastError()));
   if (rows == 0) return BIC_OK;
   const bic::Geom g = bic::make_geom(rows, cols, wpr, nplanes);
   if ((rc = ensure_scratch(ctx, bic::chunk_scratch_bytes(g)))) return rc;
@@ -460,10 +464,10 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
   if (out_eg && (!bits_eg || slot_eg == 0)) return BIC_EINVAL;
   if (rows && !planes) return BIC_EINVAL;
   if (rows == 0) {
-    if (out_golomb) BIC_HIP(hipMemsetAsync(bits_golomb, 0, sizeof(uint64_t) * nplanes, ctx->cur));
-    if (out_eg) BIC_HIP(hipMemsetAsync(bits_eg, 0, sizeof(uint64_t) * nplanes, ctx->cur));
-    if (off_golomb) BIC_HIP(hipMemsetAsync(off_golomb, 0, sizeof(uint64_t) * (nplanes + 1), ctx->cur));
-    if (off_eg) BIC_HIP(hipMemsetAsync(off_eg, 0, sizeof(uint64_t) * (nplanes + 1), ctx->cur));
+    if (out_golomb) BIC_HIP((bic::launch_fill(ctx->cur, bits_golomb, 0, sizeof(uint64_t) * nplanes), hipGetLastError()));
+    if (out_eg) BIC_HIP((bic::launch_fill(ctx->cur, bits_eg, 0, sizeof(uint64_t) * nplanes), hipGetLastError()));
+    if (off_golomb) BIC_HIP((bic::launch_fill(ctx->cur, off_golomb, 0, sizeof(uint64_t) * (nplanes + 1)), hipGetLastError()));
+    if (off_eg) BIC_HIP((bic::launch_fill(ctx->cur, off_eg, 0, sizeof(uint64_t) * (nplanes + 1)), hipGetLastError()));
     return BIC_OK;
   }
   const int pr = predict ? 1 : 0;
@@ -495,7 +499,9 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     // (no memset when the previous call's k_fixup left the counters and records zero: C2 0.036 ->
     // 0.032 ms. A call on another stream without synchronisation would share the arena anyway: calls
     // on one context are ordered by the caller)
-    fs.zero_ready = mode != bic::kEncStaged && ctx->scratch_zero_prev >= fs.zero_bytes;
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(ctx->cur, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone) ctx->captured = true;
+    fs.zero_ready = mode != bic::kEncStaged && !ctx->captured && ctx->scratch_zero_prev >= fs.zero_bytes;
     auto stage = [&](int st) {
       bic::launch_fused(ctx->cur, g, planes, ctx->lut, pr, fs, out_golomb, slot_golomb, bits_golomb, out_eg, slot_eg,
                         bits_eg, ctx->flags, mode, st);
@@ -508,7 +514,7 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
           [&] { stage(bic::kFusedRows); });
     timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
     BIC_HIP(hipGetLastError());
-    if (mode != bic::kEncStaged) ctx->scratch_zero = fs.zero_bytes;  // (k_fixup cleared them)
+    if (mode != bic::kEncStaged && !ctx->captured) ctx->scratch_zero = fs.zero_bytes;  // (k_fixup cleared them)
     return BIC_OK;
   }
   // rows wider than 16384 columns: multi-pass chunk kernels (bic_kernels.hip)
@@ -726,7 +732,7 @@ int bic_encode_planes(bic_ctx* ctx, const uint64_t* planes, int nplanes, size_t 
     if (nplanes < 1 || !geom_ok(rows, cols, wpr) || (rows && (!planes || !out || !plane_bits)) || slot_words == 0)
       return BIC_EINVAL;
     if (rows == 0) {
-      BIC_HIP(hipMemsetAsync(plane_bits, 0, sizeof(uint64_t) * nplanes, ctx->cur));
+      BIC_HIP((bic::launch_fill(ctx->cur, plane_bits, 0, sizeof(uint64_t) * nplanes), hipGetLastError()));
       return BIC_OK;
     }
     if ((rc = ensure_scratch(ctx, bic::egad_scratch_bytes((uint64_t)rows * nplanes)))) return rc;
@@ -836,7 +842,7 @@ int bic_patch_encode(bic_ctx* ctx, const uint64_t* plane, size_t rows, size_t co
     BIC_HIP(hipGetLastError());
     return BIC_OK;
   }
-  BIC_HIP(hipMemsetAsync(stats, 0, 3 * sizeof(uint64_t), ctx->cur));
+  BIC_HIP((bic::launch_fill(ctx->cur, stats, 0, 3 * sizeof(uint64_t)), hipGetLastError()));
   timed(ctx, "tiles", [&] {
     bic::launch_tiles(ctx->cur, plane, (uint32_t)rows, (uint32_t)cols, (uint32_t)wpr, W, ctx->lentab, wts,
                       w_nonpred, w_pred, modes, resid, stats);
@@ -908,7 +914,7 @@ static int match_encode_impl(bic_ctx* ctx, const uint64_t* plane, size_t rows, s
     ctx->enuml_host.assign(enuml, enuml + M + 1);
   }
   if (ntiles == 0) {
-    BIC_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(uint64_t), ctx->cur));
+    BIC_HIP((bic::launch_fill(ctx->cur, stats, 0, 4 * sizeof(uint64_t)), hipGetLastError()));
     return BIC_OK;
   }
   const bic::MatchSched sched = bic::match_schedule(W, R, (uint32_t)cols, ctx->match_parts, (uint32_t)var,

@@ -999,7 +999,7 @@ void launch_decode(hipStream_t s, int coder, const uint64_t* streams, uint64_t s
   } else if (coder == 2) {
     k_dec_egad<<<(uint32_t)((nrows + 255) / 256), 256, 0, s>>>(a);
   } else {
-    (void)hipMemsetAsync(a.first_row, 0xff, (size_t)nplanes * 4, s);
+    (void)launch_fill(s, a.first_row, 0xff, (size_t)nplanes * 4);
     k_dec_eg_first<<<grid, 256, 0, s>>>(a);
     k_dec_eg_rows<<<grid, 256, 0, s>>>(a);
   }

@@ -367,6 +367,49 @@ __device__ __forceinline__ uint32_t word_len(uint64_t x, uint32_t w, uint32_t n,
   return len;
 }
 
+// word_len, also returning which codewords have k = 1: kt gets the bit of every 1 of x whose codeword
+// has k = 1, keol (eol) the end-of-row codeword's k == 1 (the masks of bic_k1pi.h kmix_*)
+__device__ __forceinline__ uint32_t word_len_kt(uint64_t x, uint32_t w, uint32_t n, int jp, uint32_t arow, bool eol,
+                                                uint32_t cols, uint32_t& kor, uint64_t& kt, uint32_t& keol) {
+  kt = 0;
+  keol = 0;
+  if (!x && !eol) return 0;
+  uint32_t len = 0;
+  if (x && n) {
+    const uint32_t k0 = kor;
+    kor = 0;
+    if (word_len_fast(x, w, n, jp, arow, eol, cols, kor, len)) {
+      kt = kor == 2u ? x : 0ull;  // (one k for the word's codewords, the end-of-row one included)
+      keol = eol && kor == 2u ? 1u : 0u;
+      kor |= k0;
+      return len;
+    }
+    kor = k0;
+  }
+  uint32_t A = arow + (uint32_t)(jp + 1) - n;
+  len = 0;
+  while (x) {
+    const int cz = __builtin_clzll(x);
+    x ^= BIC_MSB >> cz;
+    const int j = (int)(w * 64) + cz;
+    const uint32_t s = (uint32_t)(j - jp - 1);
+    const uint32_t k = golomb_k_state(n, A);
+    kor |= 1u << min(k, 31u);
+    kt |= k == 1 ? BIC_MSB >> cz : 0ull;
+    len += k + 1 + (s >> k);
+    A += s;
+    ++n;
+    jp = j;
+  }
+  if (eol) {
+    const uint32_t k = golomb_k_state(n, A);
+    kor |= 1u << min(k, 31u);
+    keol = k == 1 ? 1u : 0u;
+    len += k + 1 + ((cols - 1 - (uint32_t)jp) >> k);
+  }
+  return len;
+}
+
 // ------------------------------------------------------------------------------------
 // residual word of a chunk step (med in word form), shared by every chunk kernel
 // ------------------------------------------------------------------------------------

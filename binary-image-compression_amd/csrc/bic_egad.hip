@@ -855,7 +855,7 @@ void launch_egad(hipStream_t s, const uint64_t* planes, uint32_t rows, uint32_t 
     if (out) k_egad_emit<<<grid, 256, 0, s>>>(a);
   } else {  // wave per row (4 rows per workgroup)
     const uint32_t wgrid = (uint32_t)((n + 3) / 4);
-    (void)hipMemsetAsync(a.slow_n, 0, 8, s);
+    (void)launch_fill(s, a.slow_n, 0, 8);
     // row maps from windows (thread per row), the rows they cannot settle by their lanes (a wave each)
     const uint32_t lgrid = (uint32_t)std::min<uint64_t>(wgrid, 2048);
 #define BIC_EGAD(W)                                   \

@@ -53,7 +53,19 @@ __device__ unsigned long long g_known[2][1 << 17];
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                               \
     if (threadIdx.x == 0) g_stamps[(1u << 21) + (ONES ? 0u : 8192u) + blockIdx.x * 8u + (slot)] = t_; \
   } while (0)
+// the class launch's phases (tools/k01_stamps.py), 4 slots per index: per kmix row (index 1 << 18 + its
+// row id; slots 0-2: entry, loads done, stored), per wave of k_emit_k01 (index 1 << 19 + 8192 + its wave;
+// slots 0-3: entry, k = 0 rows done (rest role: kmix rows done), -, exit)
+#define XSTAMP(idx, slot)                                                                          \
+  do {                                                                                             \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
+    if (lane_id() == 0 && (uint64_t)(idx) * 4 + (slot) < (1u << 22)) g_stamps[(uint64_t)(idx) * 4 + (slot)] = t_; \
+  } while (0)
 #else
+#define XSTAMP(idx, slot) \
+  do {                    \
+  } while (0)
 #define STAMP(slot) \
   do {              \
   } while (0)
@@ -90,6 +102,30 @@ constexpr uint32_t kKnownTable = BIC_KNOWN_PI ? 512u : 0u;
 #define BIC_SLOW_REST 1  // class kernels' path: the slow rows by k_emit_rest (listed by the LEN scan), no k_rows_global
 #endif
 constexpr bool kSlowRest = BIC_SLOW_REST != 0;
+#ifndef BIC_K01_REST
+#define BIC_K01_REST 0
+#endif
+// the class kernels' path (EG source): the mixed-k and slow rows by k_emit_k01's own leading workgroups
+// (rest_role: one CU slot each, beside the persistent class waves) instead of k_emit_rest on the second
+// stream -- the emission is one launch, without the fork / join events
+constexpr bool kK01Rest = BIC_K01_REST != 0;
+#ifndef BIC_KMIX
+#define BIC_KMIX 0
+#endif
+// the class kernels' path: rows mixing k = 0 and k = 1 by kmix_rows inside k_emit_k01 (the walk's k = 1
+// masks, bic_k1pi.h kmix_*) instead of k_emit_rest's per-codeword encoder
+constexpr bool kKMixRows = BIC_KMIX != 0;
+#ifndef BIC_K01_RG
+#define BIC_K01_RG 0  // (A/B: the rest role's workgroups; 0: one per CU, the persistent ones one fewer per CU)
+#endif
+constexpr uint32_t kK01Rg = BIC_K01_RG;
+#ifndef BIC_K01_PRIO
+#define BIC_K01_PRIO 0
+#endif
+#ifndef BIC_K01_RLAST
+#define BIC_K01_RLAST 0
+#endif
+constexpr bool kK01Prio = BIC_K01_PRIO != 0, kK01RLast = BIC_K01_RLAST != 0;
 
 // One lane's codewords for one residual word.
 struct LaneEnc {
@@ -657,7 +693,9 @@ __device__ __forceinline__ void write_row(const uint32_t* img, uint64_t L, uint6
 // consumer masks them off, so the two emission launches never write glen)
 constexpr uint64_t kK0Row = 1ull << 63;  // every codeword of the row has k = 0
 constexpr uint64_t kK1Row = 1ull << 62;  // every codeword of the row has k = 1
-constexpr uint64_t kLenMask = kK1Row - 1;
+constexpr uint64_t kKMix = 1ull << 61;   // k = 0 and k = 1 mixed, masks stored (kmix_rows)
+constexpr uint64_t kKEol1 = 1ull << 60;  // (kKMix) the end-of-row codeword has k = 1
+constexpr uint64_t kLenMask = kKEol1 - 1;
 
 struct FusedArgs {
   Geom g;
@@ -701,6 +739,12 @@ struct FusedArgs {
                   // keeps these loads on the scalar cache: no wait on the vector memory counter)
   uint64_t* sink;     // FusedScratch::sink
   uint32_t* walk_o;   // FusedScratch::walk_o (the walked rows' row_o)
+  uint32_t rgrid;     // k_emit_k01: its leading workgroups in the rest role (0: k_emit_rest writes those rows)
+  // class kernels' path: per walked row (walk list index < kcap) the k = 1 masks of its words (kmix_rows),
+  // and per kKMix row its walk list index
+  uint64_t* kmask;
+  uint32_t* row_wi;
+  uint32_t kcap;
 #ifdef BIC_STAMPS
   int known;
 #endif
@@ -1659,6 +1703,30 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
         a.gslow[base + r] = a.row_o[base + r] + r + 1;
         a.slow_ids[atomicAdd(a.slow_n, 1u)] = base + r;
       }
+      // the mixed rows that fit an LDS image: those with the walk's k = 1 masks (kKMix) listed for kmix_rows
+      // (the class entries' third list, counter[8]), the others (a codeword with k >= 2) for k_emit_k01's
+      // rest role (rest_ids, counter[6]). ~1 % of the rows: most waves append nothing.
+      const bool cx = kK01Rest && ok && (f & kKMix) && !big;
+      const bool cm = kK01Rest && ok && !(f & (kK0Row | kK1Row | kKMix)) && !big;
+      const uint64_t mx = __ballot(cx), mm = __ballot(cm);
+      if (mx) {
+        const int leader = __builtin_ctzll(mx);
+        uint32_t wb = 0;
+        if (lane_id() == leader) wb = atomicAdd(a.counter + 8, (uint32_t)__popcll(mx));
+        wb = (uint32_t)__shfl((int)wb, leader);
+        if (cx) {
+          const uint64_t e = 2 * (uint64_t)g.rows * g.nplanes + wb + (uint32_t)__popcll(mx & ((1ull << lane_id()) - 1ull));
+          a.cls[2 * e] = (base + r) | ((v[0] & kLenMask) << 32);
+          a.cls[2 * e + 1] = (uint64_t)plane * cap + pre;
+        }
+      }
+      if (mm) {
+        const int leader = __builtin_ctzll(mm);
+        uint32_t wb = 0;
+        if (lane_id() == leader) wb = atomicAdd(a.counter + 6, (uint32_t)__popcll(mm));
+        wb = (uint32_t)__shfl((int)wb, leader);
+        if (cm) a.rest_ids[wb + (uint32_t)__popcll(mm & ((1ull << lane_id()) - 1ull))] = (uint32_t)(base + r);
+      }
       uint32_t t0, t1;
       const uint32_t x0 = block_excl_scan<uint32_t>(c0, reinterpret_cast<uint32_t*>(tmp), t0);
       const uint32_t x1 = block_excl_scan<uint32_t>(c1, reinterpret_cast<uint32_t*>(tmp), t1);
@@ -1783,14 +1851,22 @@ __global__ __launch_bounds__(512) void k_row_walk(FusedArgs a) {
                                              : resid_word_at<PREDICT>(a.planes, g, plane, row, w)) & hmask;
     WSTAMP(5);
     const WideRow p = wide_prefix(x, w, O + row, sh);
-    uint32_t kor = 0;
-    uint32_t ll = word_len(x, w, p.n, p.jp, row * (g.cols + 1), w == g.used - 1 && h == 1, g.cols, kor);
+    uint32_t kor = 0, keol = 0;
+    uint64_t kt = 0;
+    const bool eol = w == g.used - 1 && h == 1;
+    uint32_t ll = kKMixRows && a.kmask ? word_len_kt(x, w, p.n, p.jp, row * (g.cols + 1), eol, g.cols, kor, kt, keol)
+                                       : word_len(x, w, p.n, p.jp, row * (g.cols + 1), eol, g.cols, kor);
     ll = wave_sum_u32(ll);
     WSTAMP(6);
     const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);  // some k != 0 / some k != 1
+    const uint64_t kbig = __ballot(kor & ~3u), ke = __ballot(keol);     // some k >= 2 / the end-of-row k = 1
+    if (kKMixRows && a.kmask && i < a.kcap) {  // the word's k = 1 mask (its two halves' lanes combined) for kmix_row
+      const uint64_t kw = kWalkSplit == 2 ? kt | shfl_u64(kt, lane ^ 1) : kt;
+      if ((kWalkSplit == 1 || h == 0) && w < g.used) a.kmask[(uint64_t)i * g.used + w] = kw;
+    }
     if (lane == 0) {
       sl[v] = ll;
-      sk[v] = (ks ? 1u : 0u) | (k1s ? 2u : 0u);
+      sk[v] = (ks ? 1u : 0u) | (k1s ? 2u : 0u) | (kbig ? 4u : 0u) | (ke ? 8u : 0u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1801,8 +1877,12 @@ __global__ __launch_bounds__(512) void k_row_walk(FusedArgs a) {
       }
       // (mixed-k rows and the plane's first-1 row are k_emit_rest's: it finds them in this list by
       // glen's flags and row_o, so no row is appended here -- thousands of same-address atomics
-      // would serialise this kernel)
-      a.glen[id] = L | (!(kk & 1u) ? kK0Row : (!(kk & 2u) ? kK1Row : 0));
+      // would serialise this kernel; on the class kernels' path the mixed rows whose codewords all have
+      // k <= 1 and whose masks were stored are kmix_rows', flagged kKMix)
+      const bool kmix = a.kmask && i < a.kcap && (kk & 3u) == 3u && !(kk & 4u);
+      a.glen[id] = L | (!(kk & 1u) ? kK0Row : (!(kk & 2u) ? kK1Row : 0)) | (kmix ? kKMix : 0) |
+                   (kmix && (kk & 8u) ? kKEol1 : 0);
+      if (kmix) a.row_wi[id] = i;
     }
     WSTAMP(7);
     __syncthreads();
@@ -2078,8 +2158,15 @@ __device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) { ret
 // sample's zeros and its '1'), i.e. the EG row ~R '1' (eg.cpp:20-37) with its first cols bits inverted.
 // Output word t of the row (at bit Gb) holds row bits [64 t - g, 64 t - g + 64), g = Gb % 64: the
 // stream bits from Bsrc + 64 t - g (Bsrc: the row in the EG slot), one funnel shift per word.
+#ifndef BIC_K0_W16
+#define BIC_K0_W16 0
+#endif
 #ifndef BIC_K0_BATCH
-#define BIC_K0_BATCH 3  // (pipelined batches of 3: C3 emission 162-165 -> 157-158 us; of 2: 159-162; of 4: 170-173)
+// (8-byte lanes, pipelined batches of 3: C3 emission 162-165 -> 157-158 us; of 2: 159-162; of 4: 170-173.
+// Batches of 2 keep k_emit_k01 at <= 128 VGPRs (113; batches of 3: 129), which its rest role needs
+// (BIC_K01_REST: a fourth workgroup slot per CU beside three persistent ones). 16-byte lanes: 115 VGPRs
+// at batches of 2)
+#define BIC_K0_BATCH (BIC_K01_REST ? 2 : 3)
 #endif
 constexpr int kK0Batch = BIC_K0_BATCH;
 #ifndef BIC_DIAG_K0
@@ -2121,6 +2208,7 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
     r.d = (uint32_t)(s0 & 63);
     return r;
   };
+#if !BIC_K0_W16
   // the row's source words (those holding its bits through its end-of-row '1'; the slot may end
   // there): every lane loads, at a clamped index, the words outside masked where used
   auto load = [&](const Row& r, uint64_t (&v)[WPL + 1]) {
@@ -2175,6 +2263,76 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
       if (k < WPL || in) class_store(dst, whole ? bswap64(x) : x);
     }
   };
+#else
+  // 16 bytes per lane: lane q holds output words t0 = 128 k + 2 q - e and t0 + 1 (e = w0 & 1, so the
+  // pair's store is 16-byte aligned) and loads the source words si + t0, si + t0 + 1 with one 16-byte
+  // load (8-byte aligned: dword alignment is all global dwordx4 needs); si + t0 + 2 is lane q + 1's
+  // first word (DPP), lane 63's from the next group's lane 0. Half the memory instructions of the
+  // 8-byte form per row.
+  constexpr int NG = (64 * WPL + 3 + 127) / 128;
+  using V2 = HIP_vector_type<unsigned long long, 2>;
+  auto load = [&](const Row& r, V2 (&v)[NG]) {
+    const int64_t jend = r.si + (int64_t)((r.d + (r.G & 63) + g.cols) >> 6);
+    const int64_t e = (int64_t)((r.G >> 6) & 1);
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int64_t j = r.si - e + 128 * k + 2 * lane;
+      int64_t jc = j > jend - 1 ? jend - 1 : j;
+      jc = jc < 0 ? 0 : jc;
+      v[k] = *reinterpret_cast<const V2*>(S + jc);
+      // words outside [0, jend] read as 0, the clamped pairs realigned (j = jend: its first word is the
+      // clamped pair's second; j = -1: its second word is the clamped pair's first)
+      const unsigned long long lo = v[k].x, hi = v[k].y;
+      v[k].x = (j >= 0 && j < jend) ? lo : (j == jend ? hi : 0ull);
+      v[k].y = (j >= 0 && j + 1 <= jend) ? (j < jend ? hi : 0ull) : (j == -1 ? lo : 0ull);
+    }
+  };
+  auto emit = [&](const Row& cur, V2 (&v)[NG]) {
+    const uint32_t gs = (uint32_t)(cur.G & 63);
+    const uint64_t w0 = cur.G >> 6;
+    const int64_t nwo = (int64_t)(((cur.G + L - 1) >> 6) - w0 + 1);
+    const int64_t eolw = (int64_t)((g.cols + gs) >> 6);
+    const uint64_t eolb = BIC_MSB >> ((g.cols + gs) & 63);
+    const int64_t e = (int64_t)(w0 & 1);
+    const bool tail_whole = ((cur.G + L) & 63) == 0;
+    auto fix = [&](uint64_t x, int64_t t) {
+      if (t == 0) x &= ~0ull >> gs;
+      if (t >= eolw) x = t == eolw ? (x & ~((eolb << 1) - 1)) | eolb : 0ull;
+      return x;
+    };
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int64_t t0 = 128 * k + 2 * lane - e, t1 = t0 + 1;
+      uint64_t n0 = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v[k].x >> 32), 0x130, 0xf, 0xf, true) << 32) |
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v[k].x, 0x130, 0xf, 0xf, true);
+      if (k + 1 < NG) {
+        const uint64_t nn = rl64(v[k + 1 < NG ? k + 1 : k].x, 0);
+        if (lane == 63) n0 = nn;
+      }
+      const uint64_t h0 = bswap64(v[k].x), h1 = bswap64(v[k].y), h2 = bswap64(n0);
+      const uint64_t x0 = fix(~(cur.d ? funnel64(h0, h1, 64 - cur.d) : h0), t0);
+      const uint64_t x1 = fix(~(cur.d ? funnel64(h1, h2, 64 - cur.d) : h1), t1);
+      const bool in0 = t0 >= 0 && t0 < nwo, in1 = t1 >= 0 && t1 < nwo;
+      const bool wh0 = in0 && (t0 != 0 || gs == 0) && (t0 != nwo - 1 || tail_whole);
+      const bool wh1 = in1 && (t1 != 0 || gs == 0) && (t1 != nwo - 1 || tail_whole);
+      if (wh0 && wh1) {
+        V2 o;
+        o.x = bswap64(x0);
+        o.y = bswap64(x1);
+        *reinterpret_cast<V2*>(a.out_g + w0 + t0) = o;
+      } else {
+        if (in0) class_store(wh0 ? a.out_g + w0 + t0 : a.gfrag + 2 * (uint64_t)cur.id + (t0 == 0 ? 0 : 1), wh0 ? bswap64(x0) : x0);
+        if (in1) class_store(wh1 ? a.out_g + w0 + t1 : a.gfrag + 2 * (uint64_t)cur.id + (t1 == 0 ? 0 : 1), wh1 ? bswap64(x1) : x1);
+      }
+    }
+  };
+#define BIC_K0_VT V2
+#define BIC_K0_VN NG
+#endif
+#if !BIC_K0_W16
+#define BIC_K0_VT uint64_t
+#define BIC_K0_VN WPL + 1
+#endif
   // rows in batches of BATCH: every row's loads issued before the first row's stores, so a wave
   // waits for its previous stores once per batch
 #if BIC_K0_PLACE_AHEAD
@@ -2185,7 +2343,7 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
   for (int u = 0; u < BATCH; ++u) rn[u] = place((uint32_t)u < R ? (uint32_t)u : 0u);
   for (uint32_t k = 0; k < R; k += BATCH) {
     Row r[BATCH];
-    uint64_t v[BATCH][WPL + 1];
+    BIC_K0_VT v[BATCH][BIC_K0_VN];
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
       r[u] = rn[u];
@@ -2201,7 +2359,7 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
   // software-pipelined: batch k + 1's loads issued before batch k's stores, so the wait for a batch's
   // loads never covers the previous batch's stores (vmcnt counts both, in order)
   Row ra[BATCH], rb[BATCH];
-  uint64_t va[BATCH][WPL + 1], vb[BATCH][WPL + 1];
+  BIC_K0_VT va[BATCH][BIC_K0_VN], vb[BATCH][BIC_K0_VN];
 #pragma unroll
   for (int u = 0; u < BATCH; ++u) {
     ra[u] = place((uint32_t)u < R ? (uint32_t)u : 0u);
@@ -2230,7 +2388,7 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
 #else
   for (uint32_t k = 0; k < R; k += BATCH) {
     Row r[BATCH];
-    uint64_t v[BATCH][WPL + 1];
+    BIC_K0_VT v[BATCH][BIC_K0_VN];
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
       r[u] = place(k + u < R ? k + u : k);
@@ -2242,6 +2400,8 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
   }
 #endif
 }
+#undef BIC_K0_VT
+#undef BIC_K0_VN
 
 // write_row64 with a fixed number of store instructions (MAXT per lane, the idle lanes' to a.sink)
 // and its stores typed unsigned long long (k_emit_k0)
@@ -2495,61 +2655,30 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
   }
 }
 
-// Both classes in one launch: persistent waves take their share of each list, the k = 0 rows first.
-// The waves reach the byte-table rows at different times, so the copies (memory-bound) and the
-// byte-table rows (issue-bound) run side by side instead of one launch after the other. (Odd waves
-// starting on the k = 1 rows measured 196-198 µs against 192-193, round 4.)
-template <int WPL>
-#ifndef BIC_K01_OCC
-#define BIC_K01_OCC 0  // (A/B: a minimum of workgroups per CU for k_emit_k01; 0: none)
-#endif
-__global__ __launch_bounds__(256, BIC_K01_OCC ? BIC_K01_OCC : 1) void k_emit_k01(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
-  __shared__ uint32_t s_lut[512];
-  const int lane = lane_id();
-  uint32_t* gimg = lds + wave_id() * kGImg;
-  // every wave writes the whole table itself (the same values as the others): its own reads then
-  // follow its own writes, and the kernel needs no workgroup barrier
-  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
-  const uint32_t nw = gridDim.x * 4;
-  // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform)
-  const uint32_t i0 = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
-  k0_rows<WPL>(a, i0, nw);
-  k1_rows<WPL>(a, i0, nw, gimg, s_lut);
-}
-
 // The rows the prefix kernels leave to this launch: Golomb rows with mixed k (per-codeword k,
 // encode_word; among the walked rows, counter[2]) and the EG row holding the plane's first 1 (with
 // its inserted '0'; walked, or listed by k_scan_rows in counter[3]). One workgroup per row, one word
 // per lane (wide_prefix), one LDS image per workgroup.
+// One row of k_emit_rest (a whole workgroup, one word per lane; `walked`: an entry of the walk list,
+// skipped unless mixed-k or its plane's first-1 row -- uniform over the workgroup). Ends with a
+// workgroup barrier whenever it touched the images or sh (they are reused by the next row).
 template <bool PREDICT, bool DO_G, bool DO_E>
-__global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t gimg[kGImg];
-  __shared__ __attribute__((aligned(16))) uint32_t eimg[kEImg];
-  __shared__ uint32_t s_lut[512];
-  __shared__ uint32_t sh[16];  // (wide_prefix: up to 8 waves)
-  __shared__ int sf[4];
+__device__ __forceinline__ void rest_row(const FusedArgs& a, uint64_t id, bool walked, uint32_t* gimg, uint32_t* eimg,
+                                         const uint32_t* s_lut, uint32_t* sh, int* sf) {
   const Geom& g = a.g;
   const int lane = lane_id(), v = (int)wave_id(), nw = blockDim.x >> 6;
   const uint32_t w = 64 * v + lane;
-  if (DO_G)
-    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
-  __syncthreads();
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
-  // the scan's list (first-1 rows it did not walk), then the walked rows that are mixed-k or hold
-  // their plane's first 1
-  const uint32_t nrest = __hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nwalk = DO_G ? __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  for (uint32_t i = blockIdx.x; i < nrest + nwalk; i += gridDim.x) {
-    const uint64_t id = i < nrest ? a.rest_ids[i] : a.walk_ids[i - nrest];
+  {
     const uint32_t plane = (uint32_t)(id / g.rows), row = (uint32_t)(id % g.rows);
     const uint32_t O = a.row_o[id];
     const uint64_t Lf = DO_G ? a.glen[id] : 0;
     const uint64_t L = Lf & kLenMask;
     const bool k0 = (Lf & kK0Row) != 0, k1 = (Lf & kK1Row) != 0;
-    if (i >= nrest) {  // a walked row: skip it unless mixed or the first-1 row (uniform over the workgroup)
+    if (walked) {  // a walked row: skip it unless mixed or the first-1 row (uniform over the workgroup)
       const uint64_t onext = row + 1 < g.rows ? a.row_o[id + 1] : a.pones[plane];
-      if (!(L && !k0 && !k1) && !(DO_E && O == 0 && onext > 0)) continue;
+      if (!(L && !k0 && !k1) && !(DO_E && O == 0 && onext > 0)) return;
+      if (!DO_E && a.kmask && (Lf & kKMix) && L <= kCapBits) return;  // (k_emit_k01's kmix_rows writes it)
     }
     const bool gmix = DO_G && L && !k0 && !k1 && L <= kCapBits;
     uint64_t rr[1];
@@ -2613,12 +2742,221 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
     }
     __syncthreads();  // the images and sh are reused by the next row
   }
+}
+
+template <bool PREDICT, bool DO_G, bool DO_E>
+__global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t gimg[kGImg];
+  __shared__ __attribute__((aligned(16))) uint32_t eimg[kEImg];
+  __shared__ uint32_t s_lut[512];
+  __shared__ uint32_t sh[16];  // (wide_prefix: up to 8 waves)
+  __shared__ int sf[4];
+  const int lane = lane_id(), v = (int)wave_id(), nw = blockDim.x >> 6;
+  if (DO_G)
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
+  __syncthreads();
+  // the scan's list (first-1 rows it did not walk), then the walked rows that are mixed-k or hold
+  // their plane's first 1
+  const uint32_t nrest = __hip_atomic_load(a.counter + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nwalk = DO_G ? __hip_atomic_load(a.counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  for (uint32_t i = blockIdx.x; i < nrest + nwalk; i += gridDim.x)
+    rest_row<PREDICT, DO_G, DO_E>(a, i < nrest ? a.rest_ids[i] : a.walk_ids[i - nrest], i >= nrest, gimg, eimg, s_lut,
+                                  sh, sf);
   // the class kernels' path (a.cls): the LEN scan listed every row too long for an LDS image, so the
   // slow rows are written here, one wave per row, overlapping the class kernels (no k_rows_global)
   if (DO_G && !PREDICT && kSlowRest && a.cls) {
     const uint32_t nslow = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint32_t li = blockIdx.x * nw + v; li < nslow; li += gridDim.x * nw) row_global<false>(a, a.slow_ids[li], lane);
   }
+}
+
+// Rows mixing k = 0 and k = 1 (the class entries' third list; the walk stored each word's k = 1 mask):
+// the backward-parity rows of k1_rows with every column's k from the masks (bic_k1pi.h kmix_kk /
+// kmix_word_*: a byte whose columns share one k through the k = 1 table or verbatim, a byte where k
+// changes column by column). GolombCoder.cpp:13-34 per codeword. Lane l holds words t * 64 + l (one
+// word group at a time: few registers, as these rows are ~1 % of a C3 step's).
+template <int WPL>
+__device__ __forceinline__ void kmix_row(const FusedArgs& a, uint32_t i, uint32_t* gimg, const uint32_t* s_lut) {
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+  const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
+  const uint32_t tail = g.cols & 63u;  // columns of the row's last word (0: a full word)
+  {
+    const uint64_t e = 2 * nrows + i;
+    const uint64_t e0 = cls_ld(a, 2 * e);
+    const uint32_t id = (uint32_t)e0;
+    const uint64_t L = e0 >> 32;
+    const uint32_t plane = id / g.rows, row = id % g.rows;
+    const uint64_t Gs = cls_ld(a, 2 * e + 1);
+    const uint64_t G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
+    XSTAMP((1u << 18) + id, 0);
+    const uint64_t* km = a.kmask + (uint64_t)a.row_wi[id] * g.used;
+    const uint32_t keol = (a.glen[id] & kKEol1) ? 1u : 0u;
+    uint64_t rr[WPL], ktw[WPL];
+    eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      const uint32_t w = (uint32_t)t * 64 + lane;
+      ktw[t] = km[w < g.used ? w : g.used - 1];
+    }
+    XSTAMP((1u << 18) + id, 1);
+    if (L > kCapBits) {  // (the LEN scan lists such rows as slow, never here: a length disagreement)
+      if (lane == 0) atomicOr(&a.flags[3], 1u);
+      return;
+    }
+    unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
+    for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
+    uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
+    auto ws = [&](int t, uint64_t& xt, uint64_t& Z, uint64_t& kt) {
+      const uint32_t w = (uint32_t)t * 64 + lane;
+      const uint64_t valid = w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
+      const uint64_t eb = (w == g.used - 1 && tail) ? (BIC_MSB >> tail) : 0ull;  // the end-of-row 1
+      xt = rr[t] | eb;
+      Z = ~xt & valid;
+      kt = (ktw[t] & rr[t]) | (keol ? eb : 0ull);
+    };
+    // zeta (pi right of the word) and nk (the k of the first codeword ending after the word): from the
+    // nearest lane to the right in the word's group holding a 1, else from the first such word of a
+    // later group (carried), else the end of the row
+    uint32_t zb = 0, kb = 0, zc = 0, kc = keol;
+#pragma unroll
+    for (int t = WPL - 1; t >= 0; --t) {
+      uint64_t xt, Z, kt;
+      ws(t, xt, Z, kt);
+      const uint32_t cz = xt ? (uint32_t)__builtin_clzll(xt) : 0u;
+      const uint32_t lead = cz & 1u, leadk = (uint32_t)(kt >> (63 - cz)) & 1u;
+      const uint64_t m1 = __ballot(xt != 0);
+      const uint64_t nm = m1 & ~((2ull << lane) - 1ull);
+      const int src = nm ? (int)__builtin_ctzll(nm) : lane;
+      const uint32_t ln = (uint32_t)__shfl((int)lead, src), lnk = (uint32_t)__shfl((int)leadk, src);
+      zb |= (nm ? ln : zc) << t;
+      kb |= (nm ? lnk : kc) << t;
+      if (m1) {
+        const int f = (int)__builtin_ctzll(m1);
+        zc = (uint32_t)__builtin_amdgcn_readlane((int)lead, f);
+        kc = (uint32_t)__builtin_amdgcn_readlane((int)leadk, f);
+      }
+    }
+    const uint32_t kk0 = kc, lf = zc;  // the row's first codeword's k (its remainder bit leads), pi(-1)
+    const uint32_t* T = s_lut;
+    uint32_t loc = kk0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      if (t * 64 >= (int)g.used) break;
+      const uint32_t w = (uint32_t)t * 64 + lane;
+      uint64_t xt, Z, kt;
+      ws(t, xt, Z, kt);
+      const uint32_t zt = (zb >> t) & 1u, nt = (kb >> t) & 1u;
+      const uint64_t Pi = k1_pi(xt, Z, zt), KK = kmix_kk(xt, Z, kt, nt);
+      uint64_t hi = 0, lo = 0, A, B;
+      uint32_t Lw = 0;
+      if (w < g.used) {
+        if (w == g.used - 1 && tail) Lw = kmix_word_last(rr[t], Pi, KK, nt, tail, hi, lo);
+        else Lw = kmix_word_full(rr[t], Pi, KK, nt, T, hi, lo);
+      }
+      left128(hi, lo, Lw ? Lw : 128u, A, B);
+      const uint32_t inc = wave_incl_sum_u32(Lw);
+      place128_64(img, loc + inc - Lw, A, B, Lw);
+      loc += lane63_u32(inc);
+    }
+    const uint32_t tot = loc + (tail ? 0u : 1u);
+    if (lane == 0) {
+      if (kk0 && lf) lds_or64(img, 0, BIC_MSB);
+      if (!tail) lds_or64(img, (tot - 1) >> 6, BIC_MSB >> ((tot - 1) & 63));  // the end-of-row '1'
+      if (tot != L) atomicOr(&a.flags[3], 1u);  // the walk's length disagrees with the emission
+    }
+    write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, L, G, a.out_g, a.gfrag + 2 * (uint64_t)id, a.sink);
+    XSTAMP((1u << 18) + id, 2);
+  }
+}
+
+// The class launch's rest role (the FusedArgs::rgrid leading workgroups of k_emit_k01, dispatched first,
+// one CU slot each beside the persistent class waves): the rows whose latency would otherwise be the
+// persistent waves' tail. First the rows mixing k = 0 and k = 1 (kmix_row, one wave each, claimed by
+// ticket: counter[9]); then, per workgroup, the mixed rows with a codeword of k >= 2 (rest_ids,
+// counter[6]; k_emit_rest's rows, ticket counter[7]); then the slow rows, one wave each. This is
+// k_emit_rest on a second stream without the stream: no fork / join events around the emission.
+template <int WPL>
+__device__ __forceinline__ void rest_role(const FusedArgs& a, uint32_t* lds, uint32_t* s_lut, uint32_t* s_lut2) {
+  __shared__ uint32_t sh[16];
+  __shared__ int sf[4];
+  __shared__ uint32_t tk[2];
+  for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) {
+    s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];  // (kmix_row: the k = 1 table)
+    s_lut2[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];            // (rest_row: encode_word's)
+  }
+  __syncthreads();
+  if (a.kmask) {
+    const uint32_t nx = __hip_atomic_load(a.counter + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t* gimg = lds + wave_id() * kGImg;
+    for (;;) {
+      uint32_t t = 0;
+      if (lane_id() == 0) t = atomicAdd(a.counter + 9, 1u);
+      t = uni_u32((uint32_t)__shfl((int)t, 0));
+      if (t >= nx) break;
+      kmix_row<WPL>(a, t, gimg, s_lut);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
+      __builtin_amdgcn_wave_barrier();
+    }
+    XSTAMP((1u << 19) + 8192u + blockIdx.x * 4u + wave_id(), 1);
+    __syncthreads();  // (the images are the workgroup's again)
+  }
+  const uint32_t n = __hip_atomic_load(a.counter + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t it = 0;; ++it) {
+    // (two ticket slots: a thread still reading the last one is never overwritten)
+    if (threadIdx.x == 0) tk[it & 1] = n ? atomicAdd(a.counter + 7, 1u) : 0u;
+    __syncthreads();
+    const uint32_t i = tk[it & 1];
+    if (i >= n) break;
+    rest_row<false, true, false>(a, a.rest_ids[i], false, lds, nullptr, s_lut2, sh, sf);
+  }
+  if (kSlowRest) {
+    const uint32_t nslow = __hip_atomic_load(a.slow_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t li = blockIdx.x * 4 + wave_id(); li < nslow; li += a.rgrid * 4) row_global<false>(a, a.slow_ids[li], lane_id());
+  }
+}
+
+// Both classes in one launch: persistent waves take their share of each list, the k = 0 rows first.
+// The waves reach the byte-table rows at different times, so the copies (memory-bound) and the
+// byte-table rows (issue-bound) run side by side instead of one launch after the other. (Odd waves
+// starting on the k = 1 rows measured 196-198 µs against 192-193, round 4.)
+template <int WPL>
+#ifndef BIC_K01_OCC
+#define BIC_K01_OCC 0  // (A/B: a minimum of workgroups per CU for k_emit_k01; 0: none)
+#endif
+__global__ __launch_bounds__(256, BIC_K01_OCC ? BIC_K01_OCC : 1) void k_emit_k01(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];
+  __shared__ uint32_t s_lut[512];
+  const int lane = lane_id();
+  [[maybe_unused]] const uint32_t gwv = (1u << 19) + 8192u + blockIdx.x * 4u + wave_id();  // (XSTAMP index)
+  XSTAMP(gwv, 0);
+  // the rest role: the grid's first rgrid workgroups, or (BIC_K01_RLAST) its last ones -- dispatched after
+  // the persistent ones, so its waves are the younger ones in the SIMDs' VALU arbitration
+  const uint32_t pb = kK01RLast ? gridDim.x - a.rgrid : 0u;  // the rest role's first workgroup
+  if constexpr (kK01Rest) {
+    if (blockIdx.x >= pb && blockIdx.x < pb + a.rgrid) {  // the rest role (k_emit_rest's rows in this launch)
+      __shared__ uint32_t s_lut2[512];
+      rest_role<WPL>(a, lds, s_lut, s_lut2);
+      XSTAMP(gwv, 3);
+      return;
+    }
+  }
+  // (BIC_K01_PRIO: the persistent waves' VALU ahead of the rest role's, whose per-codeword rows would
+  // otherwise take issue slots from the copies)
+  if constexpr (kK01Prio) __builtin_amdgcn_s_setprio(2);
+  uint32_t* gimg = lds + wave_id() * kGImg;
+  // every wave writes the whole table itself (the same values as the others): its own reads then
+  // follow its own writes, and the kernel needs no workgroup barrier
+  for (uint32_t i = lane; i < 512; i += 64) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
+  const uint32_t nb = gridDim.x - a.rgrid, nw = nb * 4;
+  // (the wave index through readfirstlane: the compiler then knows i0, and every branch on it, is uniform;
+  // rgrid is a multiple of 8, so block b - rgrid keeps block b's XCD)
+  const uint32_t i0 = xcd_remap(blockIdx.x - (kK01RLast ? 0u : a.rgrid), nb) * 4 + wave_id();
+  k0_rows<WPL>(a, i0, nw);
+  XSTAMP(gwv, 1);
+  k1_rows<WPL>(a, i0, nw, gimg, s_lut);
+  XSTAMP(gwv, 3);
 }
 
 __global__ __launch_bounds__(1024) void k_plane_bases(FusedArgs a) {
@@ -2691,10 +3029,18 @@ void launch_fixup_rows(hipStream_t s, const uint64_t* boff, const uint64_t* len,
 }
 
 // ------------------------------------------------------------------------------------
+// walked rows whose k = 1 masks the walk stores (kmix_rows; the others stay the rest role's): 4 Mi mask
+// words, 32 MiB (C3: 16,384 rows, against ~1,400 walked)
+static uint32_t kmask_rows(const Geom& g) {
+  const uint64_t n = (uint64_t)g.rows * g.nplanes;
+  return (uint32_t)std::min<uint64_t>(n, std::max<uint64_t>(64, (4ull << 20) / g.used));
+}
+
 size_t fused_scratch_bytes(const Geom& g) {
   const size_t n = (size_t)g.rows * g.nplanes;
   return 256 + n * 8 * 2 + n * 8 * 10 + n * kMaxStrips * (16 + 4 + 4) + n * 4 * 4 + 1024 + (size_t)g.nplanes * 8 * 4 + 64 +
-         n * 16 * 2 + 64 + 512;  // (cls, sink)
+         n * 16 * 3 + 64 + 512 +  // (cls: three lists, sink)
+         n * 4 + (size_t)kmask_rows(g) * g.used * 8 + 64;  // (row_wi, kmask)
 }
 
 FusedScratch carve_fused_scratch(void* base, const Geom& g) {
@@ -2729,7 +3075,10 @@ FusedScratch carve_fused_scratch(void* base, const Geom& g) {
     fs.ebase = fs.gbase + g.nplanes;
     fs.efix = fs.ebase + g.nplanes;
     fs.cls = fs.efix + g.nplanes;
-    fs.sink = fs.cls + 4 * n;
+    fs.sink = fs.cls + 6 * n;
+    fs.kmask = fs.sink + 64;
+    fs.kcap = kmask_rows(g);
+    fs.row_wi = reinterpret_cast<uint32_t*>(fs.kmask + (size_t)fs.kcap * g.used);
   }
   fs.ns = 1;
   fs.counted = false;
@@ -2753,7 +3102,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     // the staged encoder's count pass zeroes its counters itself (kZeroWords, launch_row_ones /
     // launch_gray_rows)
     // (single / two-pass: not when the previous call's k_fixup left them zero)
-    if (mode != kEncStaged && !fs.zero_ready) (void)hipMemsetAsync(fs.counter, 0, fs.zero_bytes, s);
+    if (mode != kEncStaged && !fs.zero_ready) (void)launch_fill(s, fs.counter, 0, fs.zero_bytes);
     return;
   }
   const bool single_pass = mode == kEncSingle;
@@ -2774,6 +3123,10 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   a.efix = es ? fs.efix : nullptr;
   a.cls = es && out_g && !fs.eg_src_one ? fs.cls : nullptr;
   a.sink = fs.sink;
+  // the walk stores the k = 1 masks of mixed rows for kmix_rows (class kernels' path only)
+  a.kmask = a.cls && kKMixRows && kK01Rest ? fs.kmask : nullptr;  // (k_emit_k01's rest role writes kKMix rows)
+  a.row_wi = fs.row_wi;
+  a.kcap = fs.kcap;
 #ifdef BIC_STAMPS
   a.known = getenv("BIC_KNOWN") && getenv("BIC_KNOWN")[0] == '1';
 #endif
@@ -2842,8 +3195,10 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     // is one, so that it can overlap the main launch, which skips the listed rows' parts
     const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
     const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 32 / nwv);  // 32 waves per CU (16: C4 +6 us; 4: C3 +30 us -- the listed rows are latency-bound)
+    // (the class kernels' path with the rest role inside k_emit_k01: one launch, no second stream)
+    const bool one_launch = es && a.cls && kK01Rest;
     hipStream_t rs = s;
-    if (kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
+    if (!one_launch && kRestAux && fs.aux && fs.ev_fork && fs.ev_join && hipEventRecord(fs.ev_fork, s) == hipSuccess &&
         hipStreamWaitEvent(fs.aux, fs.ev_fork, 0) == hipSuccess)
       rs = fs.aux;
 #define BIC_EMIT1(W, P, DG, DE, ES)                                                                    \
@@ -2862,9 +3217,16 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     } else if (es) {  // Golomb alone, the residual rows from the EG stream: one kernel per row class
 #define BIC_EMITC(W)                                                                                      \
   {                                                                                                    \
-    k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                    \
     static const int o_ = occ_of(reinterpret_cast<const void*>(&k_emit_k01<W>));                      \
-    k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                     \
+    if (one_launch) {                                                                                  \
+      a.rgrid = kK01Rg ? kK01Rg : std::max(8u, (uint32_t)cus / 8 * 8);                                 \
+      const uint32_t pg = (uint32_t)std::min<uint64_t>((nrows + 3) / 4, kK01Rg ? (uint64_t)cus * o_ - a.rgrid   \
+                                                                                 : (uint64_t)cus * std::max(1, o_ - 1)); \
+      k_emit_k01<W><<<a.rgrid + pg, 256, 0, s>>>(a);                                                   \
+    } else {                                                                                           \
+      k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
+      k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                   \
+    }                                                                                                  \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }
 #undef BIC_EMITC

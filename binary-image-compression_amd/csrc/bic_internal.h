@@ -157,10 +157,14 @@ struct FusedScratch {
   // EG source: the LEN scan lists the rows whose codewords all have k = 0 (entries [0 .. counter[4]))
   // and all k = 1 (entries [n ..], counter[5]) for the two class emission kernels (n = rows * planes),
   // each entry two u64 words: the row id | its Golomb length << 32, then its slot-relative Golomb bit
-  // offset (gboff's value);
-  // the mixed rows stay k_emit_rest's
+  // offset (gboff's value); a third list (entries [2n ..], counter[8]) holds the rows mixing k = 0 and
+  // k = 1 whose per-codeword k the walk stored (kmask / row_wi, kcap walked rows): kmix_rows. The other
+  // mixed rows (a codeword with k >= 2) stay the rest role's / k_emit_rest's
   uint64_t* cls = nullptr;
   uint64_t* sink = nullptr;   // 64 words the class kernels' idle lanes store to (a fixed store count)
+  uint64_t* kmask = nullptr;  // per walked row (walk list index < kcap): its words' k = 1 masks
+  uint32_t* row_wi = nullptr; // per kKMix row: its walk list index
+  uint32_t kcap = 0;
   bool eg_src_one = false;  // (A/B: the one emission kernel k_emit_known for every class instead)
 };
 size_t fused_scratch_bytes(const Geom& g);
@@ -250,6 +254,10 @@ void launch_gf2_transpose(hipStream_t s, const uint64_t* src, uint32_t s_rows, u
 void launch_gf2_ab(hipStream_t s, const uint64_t* A, uint32_t M, uint32_t a_stride, uint32_t kbits, const uint64_t* B,
                    uint32_t b_stride, uint32_t nw, uint64_t* C, uint32_t c_stride, uint32_t nset);
 
+// Byte fill by a kernel (every device-side memset of the library): hipMemsetAsync enqueued under stream
+// capture replays wrongly on this ROCm (the first captured memset of a process zeroed 800 of 1,280 bytes,
+// tools/capture_memset_probe.py), and the encoders' calls are meant to be capturable
+void launch_fill(hipStream_t s, void* dst, int value, size_t bytes);
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,
                  const uint64_t* plane_bits, uint64_t* dst, uint64_t* word_off);
 

@@ -11,8 +11,10 @@
 #endif
 #if defined(__HIPCC__) || defined(__clang__)
 #define BIC_UNROLL _Pragma("unroll")
+#define BIC_NOUNROLL _Pragma("unroll 1")
 #else
 #define BIC_UNROLL _Pragma("GCC unroll 8")
+#define BIC_NOUNROLL _Pragma("GCC unroll 1")
 #endif
 
 namespace bic {
@@ -86,6 +88,104 @@ BIC_HDI uint32_t k1_word_last(uint64_t x, uint64_t Pi, uint32_t nvalid, uint64_t
   put(1u, 1);
   return L;
 }
+// ---- rows whose codewords mix k = 0 and k = 1 (the walked rows, k_row_walk's masks) ---------------
+// With kk(c) the k of the codeword column c belongs to (a zero: the codeword its run ends in; a 1: its
+// own; kk(cols) the end-of-row codeword's), the forward output is: pi(-1) first when kk(0) = 1; a 1
+// at c emits '1', then pi(c) when kk(c + 1) = 1 (the next codeword's remainder); a zero emits '0'
+// when kk(c) = 0, or when kk(c) = 1 and pi(c) = 1; then the end-of-row '1'. kk = 1 everywhere is the
+// k = 1 transducer above, kk = 0 everywhere the residual row itself (k = 0: each run's zeros and its 1).
+//
+// KK, the kk of every column of a word (MSB = its first column): xt its 1s (the end-of-row 1 included
+// when inside the word), Z its zeros, kt the 1s of xt whose codeword has k = 1, nk the k of the first
+// codeword ending after the word. Zeros take the k of the 1 ending their run: the runs before the
+// k = 1 1s are Z & ~(Z + (kt << 1)) (as in k1_pi), the run leaving the word takes nk.
+BIC_HDI uint64_t kmix_kk(uint64_t xt, uint64_t Z, uint64_t kt, uint32_t nk) {
+  const uint64_t F = Z & ~(Z + (kt << 1));
+  const uint64_t T = Z & ((xt & (0ull - xt)) - 1ull);  // the zeros after the word's last 1
+  return kt | F | (nk ? T : 0ull);
+}
+// one column's output appended to (bits, len) (len + 2 <= 64)
+BIC_HDI void kmix_col(uint32_t xb, uint32_t pb, uint32_t kb, uint32_t kn, uint64_t& bits, uint32_t& len) {
+  if (xb) {
+    bits = (bits << 1) | 1u;
+    ++len;
+    if (kn) {
+      bits = (bits << 1) | pb;
+      ++len;
+    }
+  } else if (!kb || pb) {
+    bits <<= 1;
+    ++len;
+  }
+}
+// a full word (64 valid columns, no end-of-row 1 inside): byte by byte, a byte whose columns and the
+// column after it all have kk = 1 through the k = 1 table T, all kk = 0 verbatim, the others column by
+// column; joined into a right-aligned 128-bit (hi, lo); kkn = kk of the column after the word
+BIC_HDI uint32_t kmix_word_full(uint64_t x, uint64_t Pi, uint64_t KK, uint32_t kkn, const uint32_t* T, uint64_t& hi,
+                                uint64_t& lo) {
+  hi = lo = 0;
+  uint32_t L = 0;
+  // KK shifted one column left, the word's kkn after its last column: bit c of KN = kk(c + 1)
+  const uint64_t KN = (KK << 1) | (uint64_t)kkn;
+  // (a loop, not unrolled: these rows are rare, and eight unrolled three-way bytes cost the kernel
+  // ~25 registers)
+BIC_NOUNROLL
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t sh = 56 - 8 * j;
+    const uint32_t xb = (uint32_t)(x >> sh) & 0xffu, kb = (uint32_t)(KK >> sh) & 0xffu, kn = (uint32_t)(KN >> sh) & 0xffu;
+    uint64_t b;
+    uint32_t l;
+    if (kb == 0xffu && kn == 0xffu) {
+      const uint32_t e = T[(((uint32_t)(Pi >> sh) & 1u) << 8) | xb];
+      b = e & 0xffffu;
+      l = e >> 16;
+    } else if (kb == 0 && kn == 0) {
+      b = xb;
+      l = 8;
+    } else {
+      b = 0;
+      l = 0;
+      const uint32_t pv = (uint32_t)(Pi >> sh) & 0xffu;
+BIC_NOUNROLL
+      for (int c = 7; c >= 0; --c)
+        kmix_col((xb >> c) & 1u, (pv >> c) & 1u, (kb >> c) & 1u, (kn >> c) & 1u, b, l);
+    }
+    hi = l ? (hi << l) | (lo >> (64 - l)) : hi;
+    lo = (lo << l) | b;
+    L += l;
+  }
+  return L;
+}
+// the word holding the row's end (nvalid < 64 columns, or the end-of-row 1 right after it), column by
+// column; includes the end-of-row '1' (KK's bit at column nvalid: the end-of-row codeword's k)
+BIC_HDI uint32_t kmix_word_last(uint64_t x, uint64_t Pi, uint64_t KK, uint32_t kkn, uint32_t nvalid, uint64_t& hi,
+                                uint64_t& lo) {
+  hi = lo = 0;
+  uint32_t L = 0;
+  const uint64_t KN = (KK << 1) | (uint64_t)kkn;
+  for (uint32_t c = 0; c < nvalid; ++c) {
+    uint64_t b = 0;
+    uint32_t l = 0;
+    kmix_col((uint32_t)(x >> (63 - c)) & 1u, (uint32_t)(Pi >> (63 - c)) & 1u, (uint32_t)(KK >> (63 - c)) & 1u,
+             (uint32_t)(KN >> (63 - c)) & 1u, b, l);
+    hi = l ? (hi << l) | (lo >> (64 - l)) : hi;
+    lo = (lo << l) | b;
+    L += l;
+  }
+  hi = (hi << 1) | (lo >> 63);
+  lo = (lo << 1) | 1u;
+  return L + 1;
+}
+
+// the length kmix_word_full / kmix_word_last return, by popcounts (Z: the word's valid zeros; the
+// end-of-row 1, when inside the word, neither in x nor in Z): 1s, the remainders after them, zeros
+// with k = 0, zeros with k = 1 and pi = 1 (+ 1 for the end-of-row '1': eol)
+BIC_HDI uint32_t kmix_word_len(uint64_t x, uint64_t Z, uint64_t Pi, uint64_t KK, uint32_t kkn, bool eol) {
+  const uint64_t KN = (KK << 1) | (uint64_t)kkn;
+  return (uint32_t)(__builtin_popcountll(x) + __builtin_popcountll(x & KN) + __builtin_popcountll(Z & ~KK) +
+                    __builtin_popcountll(Z & KK & Pi)) + (eol ? 1u : 0u);
+}
+
 // left-align a right-aligned 128-bit string of L bits (place128_64's operands)
 BIC_HDI void left128(uint64_t hi, uint64_t lo, uint32_t L, uint64_t& A, uint64_t& B) {
   const uint32_t sh = 128 - L;

@@ -1405,11 +1405,11 @@ void launch_golomb_samples(hipStream_t s, const uint32_t* samples, size_t n, uin
                            const uint64_t* lpart, uint32_t nlpart, uint64_t* lout) {
   const uint32_t nblk = (uint32_t)((n + kSampPerBlk - 1) / kSampPerBlk);
   if (nblk == 0) {
-    (void)hipMemsetAsync(bits_out, 0, 2 * sizeof(uint64_t), s);
-    if (lpart) (void)hipMemsetAsync(lout, 0, sizeof(uint64_t), s);
+    (void)launch_fill(s, bits_out, 0, 2 * sizeof(uint64_t));
+    if (lpart) (void)launch_fill(s, lout, 0, sizeof(uint64_t));
     return;
   }
-  if (!prezeroed) (void)hipMemsetAsync(ss.counter, 0, ss.zero_bytes, s);
+  if (!prezeroed) (void)launch_fill(s, ss.counter, 0, ss.zero_bytes);
   k_samp_scan<<<nblk, kBlock, 0, s>>>(samples, n, n0, a0, bit0, ss, out, cap_words, bits_out, flags, nblk);
   if (out) k_samp_emit<<<nblk, kBlock, 0, s>>>(samples, n, n0, ss, out, bits_out, bit0, cap_words, lpart, nlpart, lout);
 }
@@ -1666,7 +1666,7 @@ void launch_tiles_split(hipStream_t s, const uint64_t* plane, uint32_t rows, uin
                         uint8_t* modes, uint64_t* resid, uint64_t* lpart, uint32_t* zero, uint32_t nzero) {
   const uint32_t nx = cols / W, used = (cols + 63) / 64;
   const uint32_t grid = tiles_split_blocks(rows, cols, W);
-  if (resid && wpr > used) (void)hipMemsetAsync(resid, 0, (size_t)rows * wpr * sizeof(uint64_t), s);
+  if (resid && wpr > used) (void)launch_fill(s, resid, 0, (size_t)rows * wpr * sizeof(uint64_t));
 #define BIC_TS(WW) k_tiles_split<WW><<<grid, 256, 0, s>>>(plane, rows, cols, wpr, used, nx, lentab_dev, weights, \
                                                        w_nonpred, w_pred, modes, resid, lpart, zero, nzero)
   if (W == 8) BIC_TS(8);
@@ -1685,7 +1685,7 @@ void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t 
   unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
   if (W == 8 || W == 16 || W == 32 || W == 64) {
     // words past `used` in a row (wpr > used) are the only ones the kernel does not write
-    if (resid && wpr > used) (void)hipMemsetAsync(resid, 0, (size_t)rows * wpr * sizeof(uint64_t), s);
+    if (resid && wpr > used) (void)launch_fill(s, resid, 0, (size_t)rows * wpr * sizeof(uint64_t));
     const uint64_t waves = (uint64_t)ny * ((used + 63) / 64);
     const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
 #define BIC_TILES(WW) \
@@ -1698,7 +1698,7 @@ void launch_tiles(hipStream_t s, const uint64_t* plane, uint32_t rows, uint32_t 
 #undef BIC_TILES
     return;
   }
-  if (resid) (void)hipMemsetAsync(resid, 0, (size_t)rows * wpr * sizeof(uint64_t), s);
+  if (resid) (void)launch_fill(s, resid, 0, (size_t)rows * wpr * sizeof(uint64_t));
   const uint32_t tpw = 64 / W;
   const uint64_t waves = (ntiles + tpw - 1) / tpw;
   const uint32_t grid = (uint32_t)((waves + kWaves - 1) / kWaves);
@@ -1733,6 +1733,30 @@ __global__ __launch_bounds__(kBlock) void k_pack(const uint64_t* __restrict__ sl
   const uint64_t* src = slots + (uint64_t)p * slot_words;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * kBlock)
     dst[off + i] = src[i];
+}
+
+// launch_fill: 16-byte stores over the aligned middle, single bytes at the unaligned ends
+__global__ __launch_bounds__(kBlock) void k_fill(uint8_t* __restrict__ dst, uint32_t v4, size_t head, size_t n16,
+                                                 size_t bytes) {
+  const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x, stride = (size_t)gridDim.x * kBlock;
+  uint4* m = reinterpret_cast<uint4*>(dst + head);
+  for (size_t j = i; j < n16; j += stride) m[j] = make_uint4(v4, v4, v4, v4);
+  const size_t tail0 = head + n16 * 16;
+  for (size_t j = i; j < head + (bytes - tail0); j += stride) {
+    const size_t b = j < head ? j : tail0 + (j - head);
+    dst[b] = (uint8_t)v4;
+  }
+}
+void launch_fill(hipStream_t s, void* dst, int value, size_t bytes) {
+  if (!bytes) return;
+  uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+  const size_t mis = reinterpret_cast<uintptr_t>(d) & 15;
+  const size_t head = mis ? std::min<size_t>(16 - mis, bytes) : 0;
+  const size_t n16 = (bytes - head) / 16;
+  const uint32_t v4 = 0x01010101u * (uint32_t)(uint8_t)value;
+  const size_t work = std::max<size_t>(n16, bytes - n16 * 16);
+  const uint32_t grid = (uint32_t)std::min<size_t>((work + kBlock - 1) / kBlock, 4096);
+  k_fill<<<grid ? grid : 1, kBlock, 0, s>>>(d, v4, head, n16, bytes);
 }
 
 void launch_pack(hipStream_t s, const uint64_t* slots, int nplanes, size_t slot_words,

@@ -1080,14 +1080,14 @@ void launch_match_tiles(hipStream_t s, MatchArgs& a, const MatchSched& m, void* 
   a.G = m.G;
   a.H = m.H;
   a.K = m.K;
-  (void)hipMemsetAsync(a.counter, 0, 4, s);
-  (void)hipMemsetAsync(a.key, 0xff, (size_t)ntiles * 8, s);
-  if (a.var == 5) (void)hipMemsetAsync(a.key2, 0xff, (size_t)ntiles * 8, s);
-  (void)hipMemsetAsync(a.done, 0, (size_t)ntiles * 8, s);  // done + arrive (row schedules: progress)
+  (void)launch_fill(s, a.counter, 0, 4);
+  (void)launch_fill(s, a.key, 0xff, (size_t)ntiles * 8);
+  if (a.var == 5) (void)launch_fill(s, a.key2, 0xff, (size_t)ntiles * 8);
+  (void)launch_fill(s, a.done, 0, (size_t)ntiles * 8);  // done + arrive (row schedules: progress)
   uint32_t* progress = a.done;
   switch (m.kind) {
     case kSchedTeam:
-      if (m.H) (void)hipMemsetAsync(slots, 0, (size_t)ntiles * m.H * 8, s);
+      if (m.H) (void)launch_fill(s, slots, 0, (size_t)ntiles * m.H * 8);
       if (a.W == 8) k_match_team<8><<<a.ny * (m.H + 1), kRB, 0, s>>>(a, progress, slots);
       else if (a.W == 16) k_match_team<16><<<a.ny * (m.H + 1), kRB, 0, s>>>(a, progress, slots);
       else k_match_team<32><<<a.ny * (m.H + 1), kRB, 0, s>>>(a, progress, slots);

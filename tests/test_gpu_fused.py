@@ -456,3 +456,56 @@ def test_look_back_records_left_zero(ctx, oracle):
             check(ctx, oracle, P, cols, i & 1)
     finally:
         ctx.set_encoder("auto")
+
+
+@pytest.mark.parametrize("encoder_name", ["single-kernel", "two-pass"])
+def test_capture_replay_between_other_work(ctx, oracle, encoder_name):
+    """the single and two-pass encoders skip their record / counter memset when the previous
+    call's k_fixup left them zero (host bookkeeping, bic_capi.cpp scratch_zero). A call captured into a
+    graph, and replays of it between other calls of the context, are work that bookkeeping never sees: a
+    graph captured while the arena was clean must still clear it on every replay. Capture an encode, then
+    replay it right after a staged encode (which leaves its counters dirty) and between eager calls;
+    every stream must equal the oracle's."""
+    torch = ctx.torch
+    rows, cols = 64, 2000
+    P1 = oracle.gen_plane(41, 0.3, rows, cols)[None]
+    P2 = oracle.gen_plane(42, 0.45, 3 * rows, cols)[None]
+    d1, d2 = ctx.to_dev(P1), ctx.to_dev(P2)
+    slot = ctx.slot_words(rows, cols, CODER_GOLOMB)
+    og, bg = ctx.empty_i64(1, slot), ctx.empty_i64(1)
+    ctx.reserve(1, 3 * rows, cols)
+
+    def same(out, bits, P):
+        eb, est, _ = oracle.encode_plane(P[0], cols, 1, 0)
+        nb = int(as_u64(bits)[0])
+        return nb == eb and stream_bytes(out[0], nb) == est.tobytes()
+
+    ctx.set_encoder(encoder_name)
+    try:
+        ctx.encode_planes(d1, cols, True, CODER_GOLOMB, out=og, plane_bits=bg)  # eager: leaves the records zero
+        ctx.sync()
+        torch.cuda.synchronize()
+        assert same(og, bg, P1)
+        side = torch.cuda.Stream(ctx.dev)
+        side.wait_stream(torch.cuda.current_stream(ctx.dev))
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(gr, stream=side):
+                ctx.encode_planes(d1, cols, True, CODER_GOLOMB, out=og, plane_bits=bg)
+        torch.cuda.current_stream(ctx.dev).wait_stream(side)
+        torch.cuda.synchronize()
+        for rep in range(3):
+            ctx.set_encoder("staged")  # counters left dirty for the replay that follows
+            o2, b2 = ctx.encode_planes(d2, cols, True, CODER_GOLOMB)
+            ctx.set_encoder(encoder_name)
+            og.zero_()
+            gr.replay()
+            torch.cuda.synchronize()
+            assert same(og, bg, P1), rep
+            assert same(o2, b2, P2), rep
+            o3, b3 = ctx.encode_planes(d2, cols, True, CODER_GOLOMB)  # eager, after a replay
+            ctx.sync()
+            torch.cuda.synchronize()
+            assert same(o3, b3, P2), rep
+    finally:
+        ctx.set_encoder("auto")

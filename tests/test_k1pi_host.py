@@ -61,3 +61,50 @@ def test_k1_rows_match_oracle(prog, cols, layout):
         exp = "".join(map(str, bits[offs[r]:offs[r + 1]]))
         assert got[i] == exp, (r, len(got[i]), len(exp),
                                next((j for j, (a, b) in enumerate(zip(got[i], exp)) if a != b), None))
+
+
+@pytest.mark.parametrize("layout", ["lanes", "strided"])
+@pytest.mark.parametrize("cols", [4096, 16384, 8192, 4000, 1000, 130, 70, 64, 16383])
+def test_kmix_rows_match_oracle(prog, cols, layout):
+    """rows whose codewords mix k = 0 and k = 1 (bic_k1pi.h kmix_*; "strided" composes them as
+    bic_fused.hip kmix_rows does, and checks kmix_word_len against every word's string): given each codeword's k as the walk's masks (a bit at the 1 ending every k = 1 codeword, and
+    the end-of-row codeword's k), the row's bits must equal the oracle's Golomb row"""
+    o = Oracle()
+    rng = np.random.default_rng(cols + 7)
+    rows = 480 if cols <= 8192 else 192
+    P = np.concatenate([_plane(rng, rows // 3, cols, 0.5), _plane(rng, rows // 3, cols, 0.45),
+                        _plane(rng, rows - 2 * (rows // 3), cols, 0.55)])
+    R = o.med(P, cols)
+    nb, st, _ = o.encode_plane(P, cols, 1, 0)
+    bits = np.unpackbits(np.frombuffer(st.tobytes(), np.uint8))[:nb]
+    offs = list(o.row_index(P, cols, 1)[0::2]) + [nb]
+    s, eo = o.plane_runs(R, cols)
+    _, _, kk, _ = o.golomb_samples(s, want_stream=False)
+    kk = kk.astype(np.int64)
+    rowid = np.concatenate([[0], np.cumsum(eo)[:-1]]).astype(np.int64)  # (eo flags each row's last sample)
+    start = np.searchsorted(rowid, np.arange(rows + 1))
+    sel = []
+    wpr = R.shape[1]
+    lines = []
+    for r in range(rows):
+        ks = kk[start[r]:start[r + 1]]
+        if ks.max() > 1 or ks.min() == ks.max():
+            continue
+        sel.append(r)
+        # the row's 1s in column order, each ending the next sample; the last sample is the end of row
+        rb = np.unpackbits(R[r].astype(">u8").view(np.uint8))[:cols]
+        cols1 = np.flatnonzero(rb)
+        assert len(cols1) + 1 == len(ks)
+        kt = np.zeros(wpr * 64, np.uint8)
+        kt[cols1[ks[:-1] == 1]] = 1
+        ktw = np.packbits(kt).view(">u8").astype(np.uint64)
+        lines.append(" ".join(f"{int(w):x}" for w in R[r]) + "\n" + " ".join(f"{int(w):x}" for w in ktw) +
+                     f"\n{int(ks[-1])}")
+    assert sel, "the input has no mixed row"
+    inp = f"{cols} {len(sel)}\n" + "\n".join(lines) + "\n"
+    p = subprocess.run([prog, "m" if layout == "lanes" else "n"], input=inp, capture_output=True, text=True, check=True)
+    got = p.stdout.split("\n")
+    for i, r in enumerate(sel):
+        exp = "".join(map(str, bits[offs[r]:offs[r + 1]]))
+        assert got[i] == exp, (r, len(got[i]), len(exp),
+                               next((j for j, (a, b) in enumerate(zip(got[i], exp)) if a != b), None))

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rows", type=int, default=16384)
     ap.add_argument("--cols", type=int, default=16384)
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--no-planes", action="store_true", help="planes NULL: the bench's default C3 call (EG source)")
     a = ap.parse_args()
     import torch
     import pybic
@@ -29,7 +30,7 @@ def main():
     g.manual_seed(0x5EED0000)
     gray = [t.randint(0, 256, (R, Cc), dtype=t.uint8, device=dev, generator=g) for _ in range(2)]
     wpr = (Cc + 63) // 64
-    planes = ctx.empty_i64(NP, R, wpr)
+    planes = None if a.no_planes else ctx.empty_i64(NP, R, wpr)
     sg = ctx.slot_words(R, Cc, pybic.CODER_GOLOMB)
     se = ctx.slot_words(R, Cc, pybic.CODER_EG)
     outs = (ctx.empty_i64(NP, sg), ctx.empty_i64(NP, se))
@@ -37,7 +38,8 @@ def main():
     ctx.reserve(NP, R, Cc)
 
     def step(k):
-        ctx.encode_gray(gray[k & 1], nplanes=NP, planes=planes, slots=(sg, se), outs=outs, bits=bits)
+        ctx.encode_gray(gray[k & 1], nplanes=NP, planes=planes, slots=(sg, se), outs=outs, bits=bits,
+                        store_planes=not a.no_planes)
 
     for k in range(6):
         step(k)
@@ -76,7 +78,7 @@ def main():
     torch.cuda.synchronize()
     ctx.sync()
     same = all(bool(t.equal(x, y)) for x, y in zip(ref, list(outs + bits)))
-    print({"rows": R, "cols": Cc, "eager_ms_per_step": round(eager_ms, 4), "graph_ms_per_step": round(graph_ms, 4),
+    print({"planes": not a.no_planes, "rows": R, "cols": Cc, "eager_ms_per_step": round(eager_ms, 4), "graph_ms_per_step": round(graph_ms, 4),
            "streams_identical": same}, flush=True)
 
 
