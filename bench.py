@@ -1072,6 +1072,13 @@ def main():
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tnote, "kernel": dom,
                 "algorithmic_bytes_per_launch": kb[dom], "avg_launch_us": round(avg_s * 1e6, 2)}
+        st = per_kernel.get(dom + "_stage")
+        if st:  # the staged encoder's emission: the main kernel timed alone, the whole stage beside it
+            roof["stage_avg_us"] = round(st["avg_us"], 2)
+            roof["note"] = ("avg_launch_us: HIP events on the launch stream right around the main emission kernel "
+                            "(k_emit_k01 / k_emit_known; k_emit_rest's ~1 % of the rows run beside it on a second "
+                            "stream and their bytes are counted too); stage_avg_us: the whole stage, that second "
+                            "stream's fork and join included (untimed profiled steps)")
     pred_pass = wl.predictor_pass(max(args.steps, 5)) if hasattr(wl, "predictor_pass") and type(wl) is C3 else None
     if pred_pass is not None and "bitplanes_count" in per_kernel:
         # the pass that runs inside the step: bic_encode_gray's count pass (k_gray_strips: gray -> planes,

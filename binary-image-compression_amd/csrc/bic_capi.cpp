@@ -64,7 +64,7 @@ struct bic_ctx {
   bool one_stream = false;     // BIC_OPT_ONE_STREAM: no second stream for the staged encoder's emission
   bool eg_src_off = false;     // BIC_OPT_EG_SOURCE = 0: bic_encode_gray* stores R instead of writing EG
   bool eg_src_one = false;     // BIC_OPT_EG_SOURCE = 2: one emission kernel for every row class
-  struct Rec { const char* name; hipEvent_t a, b; };
+  struct Rec { std::string name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
 };
@@ -91,6 +91,42 @@ hipEvent_t take_event(bic_ctx* ctx) {
   // the launches it brackets
   if (hipEventCreateWithFlags(&e, kProfEventFlags) != hipSuccess) (void)hipEventCreate(&e);
   return e;
+}
+
+bool prof_wants(bic_ctx* ctx, const char* name) {
+  return ctx->prof_on && (ctx->prof_only.empty() || ctx->prof_only == name);
+}
+
+// The staged encoder's emission stage: `name` times its main kernel alone (events the launch records
+// on its own stream right around that kernel, FusedScratch::ev_main*: the roofline kernel's launch
+// duration), "<name>_stage" the whole stage, the second stream's fork and join included.
+template <typename F>
+void timed_rows(bic_ctx* ctx, bic::FusedScratch& fs, const char* name, F&& launch) {
+  const std::string stage_name = std::string(name) + "_stage";
+  const bool k = prof_wants(ctx, name), st = prof_wants(ctx, stage_name.c_str());
+  hipEvent_t a = nullptr, b = nullptr, sa = nullptr, sb = nullptr;
+  if (k) {
+    a = take_event(ctx);
+    b = take_event(ctx);
+    // (recorded here too: a path without a separate main kernel then times the whole stage)
+    (void)hipEventRecord(a, ctx->cur);
+    fs.ev_main0 = a;
+    fs.ev_main1 = b;
+  }
+  if (st) {
+    sa = take_event(ctx);
+    sb = take_event(ctx);
+    (void)hipEventRecord(sa, ctx->cur);
+  }
+  launch();
+  if (st) {
+    (void)hipEventRecord(sb, ctx->cur);
+    ctx->recs.push_back({stage_name, sa, sb});
+  }
+  if (k) {
+    fs.ev_main0 = fs.ev_main1 = nullptr;
+    ctx->recs.push_back({name, a, b});
+  }
 }
 
 // Runs one launch, bracketed by events when profiling is on.
@@ -510,8 +546,8 @@ static int encode_planes_impl(bic_ctx* ctx, const uint64_t* planes, int nplanes,
     // staged encoder: per-row counts, scans and Golomb lengths (every row's offsets known up front)
     if (mode == bic::kEncStaged) timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
     // the row kernel alone is timed under the encoder's name (bench.py's roofline kernel)
-    timed(ctx, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
-          [&] { stage(bic::kFusedRows); });
+    timed_rows(ctx, fs, out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
+               [&] { stage(bic::kFusedRows); });
     timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
     BIC_HIP(hipGetLastError());
     if (mode != bic::kEncStaged && !ctx->captured) ctx->scratch_zero = fs.zero_bytes;  // (k_fixup cleared them)
@@ -628,9 +664,9 @@ static int encode_gray_impl(bic_ctx* ctx, const uint8_t* gray, size_t pitch, siz
   });
   timed(ctx, "encode_prefix", [&] { stage(bic::kFusedPrefix); });
   // (EG source: the emission is Golomb's alone, reading the residual rows from the EG stream)
-  timed(ctx, eg_src ? "encode_rows_golomb_egsrc"
-                    : out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
-        [&] { stage(bic::kFusedRows); });
+  timed_rows(ctx, fs, eg_src ? "encode_rows_golomb_egsrc"
+                             : out_golomb ? (out_eg ? "encode_rows_golomb_eg" : "encode_rows_golomb") : "encode_rows_eg",
+             [&] { stage(bic::kFusedRows); });
   timed(ctx, "encode_finish", [&] { stage(bic::kFusedFinish); });
   BIC_HIP(hipGetLastError());
   if (row_index && !out_golomb) return bic_row_index(ctx, planes, nplanes, rows, cols, wpr, pr, row_index);

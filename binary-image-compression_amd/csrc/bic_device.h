@@ -616,11 +616,15 @@ __device__ __forceinline__ uint64_t funnel64(uint64_t hi, uint64_t lo, uint32_t 
 }
 
 // Zero a wave's 32-bit LDS row image (n16 16-byte units) before codewords are OR'd into it with 4-byte
-// LDS atomics: the 16-byte zero stores are drained (s_waitcnt lgkmcnt(0)) before the first atomic issues.
-// Round 4's k_emit_k1 zeroed its image with 16-byte stores and OR'd 8-byte atomics into it with no such
-// wait; on the first encode of a process, with k_emit_rest's workgroups sharing the CUs, its k = 1 rows
-// lost about a quarter of their 1 bits. The 64-bit images now zero with 8-byte stores of
-// the atomics' own type (k1_rows, emit_known_row), the form that measured clean.
+// LDS atomics: the 16-byte zero stores are drained (s_waitcnt lgkmcnt(0)) before the first atomic issues,
+// and the asm's "memory" clobber also keeps the compiler from moving any LDS access across it.
+// Round 4's k_emit_k1 zeroed its 64-bit image with 16-byte stores and OR'd 8-byte atomics into it with
+// neither; on the first encode of a process, with k_emit_rest's workgroups sharing the CUs, its k = 1 rows
+// lost about a quarter of their 1 bits. Its ISA (profiles/r06/isa_67ba6e6_k_emit_k1.txt)
+// has every ds_write_b128 of the zeroing before every ds_or_b64 of the row, over exactly the wave's own
+// 684 words: neither a compiler reordering nor the extent. What measured clean is the same-width form:
+// the 64-bit images zero with 8-byte stores of the atomics' own width and type (k1_rows, emit_known_row);
+// this drain guards the mixed-width 32-bit images against the same hazard.
 __device__ __forceinline__ void lds_image_zero32(uint32_t* img, uint32_t n16) {
   uint4* z = reinterpret_cast<uint4*>(img);
   for (uint32_t i = lane_id(); i < n16; i += 64) z[i] = make_uint4(0, 0, 0, 0);

@@ -62,8 +62,17 @@ __device__ unsigned long long g_known[2][1 << 17];
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
     if (lane_id() == 0 && (uint64_t)(idx) * 4 + (slot) < (1u << 22)) g_stamps[(uint64_t)(idx) * 4 + (slot)] = t_; \
   } while (0)
+// (the same without draining the memory counters first: the instruction's issue time)
+#define YSTAMP(idx, slot)                                                                          \
+  do {                                                                                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
+    if (lane_id() == 0 && (uint64_t)(idx) * 4 + (slot) < (1u << 22)) g_stamps[(uint64_t)(idx) * 4 + (slot)] = t_; \
+  } while (0)
 #else
 #define XSTAMP(idx, slot) \
+  do {                    \
+  } while (0)
+#define YSTAMP(idx, slot) \
   do {                    \
   } while (0)
 #define STAMP(slot) \
@@ -1739,7 +1748,7 @@ __global__ __launch_bounds__(1024) void k_scan_rows(FusedArgs a) {
       const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
       const uint64_t G = (uint64_t)plane * cap + pre;  // (gboff's value, written below)
       if (c0) {
-        a.cls[2 * (lb[0] + x0)] = (base + r) | (v[0] << 32);  // id, Golomb length
+        a.cls[2 * (lb[0] + x0)] = (base + r) | ((uint64_t)plane << 32);  // id, plane (the length is cols + 1)
         a.cls[2 * (lb[0] + x0) + 1] = G;
       }
       if (c1) {
@@ -2178,6 +2187,9 @@ constexpr int kK0Batch = BIC_K0_BATCH;
 #ifndef BIC_K0_PIPE
 #define BIC_K0_PIPE 1
 #endif
+#ifndef BIC_K0_FAST
+#define BIC_K0_FAST 1
+#endif
 // the k = 0 list's entries i0, i0 + nw, ... (one wave; i0 and nw wave-uniform)
 template <int WPL, int BATCH = kK0Batch>
 __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_t nw) {
@@ -2198,8 +2210,11 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
   auto place = [&](uint32_t k) {
     const uint64_t e = i0 + (uint64_t)k * nw;
     Row r;
-    r.id = (uint32_t)cls_ld(a, 2 * e);
-    const uint32_t plane = r.id / g.rows, row = r.id % g.rows;
+    const uint64_t e0 = cls_ld(a, 2 * e);
+    r.id = (uint32_t)e0;
+    // (the k = 0 entries carry the plane where the k = 1 ones carry the length, which is cols + 1 here:
+    // no division by rows on the scalar unit)
+    const uint32_t plane = (uint32_t)(e0 >> 32), row = r.id - plane * g.rows;
     const uint64_t Gs = cls_ld(a, 2 * e + 1);
     r.G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
     // stream bit of output word t's first bit: Bsrc - G % 64 + 64 t (>= -63: floor below)
@@ -2208,7 +2223,62 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
     r.d = (uint32_t)(s0 & 63);
     return r;
   };
-#if !BIC_K0_W16
+#if !BIC_K0_W16 && BIC_K0_FAST
+  // Word groups 64 k .. 64 k + 63 of the output row. A group wholly inside the row (k >= 1 and before
+  // the row's last word: C3's groups 1-3 of 5) needs no masks, clamps or fragment selects -- a uniform
+  // branch on the row's scalar offsets -- and loads / stores through a scalar base plus the lane's
+  // 32-bit offset: ~16 VALU per group instead of ~55 (the copies share each SIMD's VALU issue with the
+  // k = 1 rows and k_emit_rest, and the younger waves wait for it: tools/k01_stamps.py)
+  auto load = [&](const Row& r, uint64_t (&v)[WPL + 1]) {
+    const int64_t jend = r.si + (int64_t)((r.d + (r.G & 63) + g.cols) >> 6);
+    const uint64_t* sb = S + r.si;  // (r.si >= -1: only group 0 may start before the stream)
+#pragma unroll
+    for (int k = 0; k <= WPL; ++k) {
+      if (k >= 1 && r.si + 64 * k + 63 <= jend) {
+        v[k] = sb[64 * k + lane];
+      } else {
+        const int64_t j = r.si + 64 * k + lane;
+        const int64_t jc = j > jend ? jend : j;
+        v[k] = S[jc < 0 ? 0 : jc];
+      }
+    }
+  };
+  auto emit = [&](const Row& cur, uint64_t (&v)[WPL + 1]) {
+    const uint32_t gs = (uint32_t)(cur.G & 63);
+    const uint64_t w0 = cur.G >> 6, nwo = ((cur.G + L - 1) >> 6) - w0 + 1;  // output words (<= used + 2)
+    const uint64_t eolw = (uint64_t)(g.cols + gs) >> 6, eolb = BIC_MSB >> ((g.cols + gs) & 63);
+    const int64_t jend = cur.si + (int64_t)((cur.d + gs + g.cols) >> 6);
+    unsigned long long* ob = reinterpret_cast<unsigned long long*>(a.out_g + w0);
+#pragma unroll
+    for (int k = 0; k <= WPL; ++k) {
+      uint64_t nx = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v[k] >> 32), 0x130, 0xf, 0xf, true) << 32) |
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v[k], 0x130, 0xf, 0xf, true);
+      if (k < WPL) {
+        const uint64_t n0 = rl64(v[k + 1 <= WPL ? k + 1 : k], 0);
+        if (lane == 63) nx = n0;
+      }
+      if (k >= 1 && (uint64_t)(64 * k + 63) < nwo - 1) {  // interior group: a shifted, inverted copy
+        const uint64_t x = ~(cur.d ? funnel64(bswap64(v[k]), bswap64(nx), 64 - cur.d) : bswap64(v[k]));
+        class_store(reinterpret_cast<uint64_t*>(ob + 64 * k + lane), bswap64(x));
+        continue;
+      }
+      const uint32_t t = 64 * k + lane;
+      const int64_t j = cur.si + 64 * k + lane;
+      const uint64_t vk = (j >= 0 && j <= jend) ? v[k] : 0ull;
+      // (lane 63's next word: the next group's first, in range when that group is)
+      const uint64_t hi = bswap64(vk);
+      uint64_t x = ~(cur.d ? funnel64(hi, bswap64(nx), 64 - cur.d) : hi);
+      // row bits outside [0, cols) are not the row's: before it (word 0's first gs bits) and from the
+      // end-of-row '1' on
+      if (t == 0) x &= ~0ull >> gs;
+      if (t >= eolw) x = t == eolw ? (x & ~((eolb << 1) - 1)) | eolb : 0ull;
+      const bool in = t < nwo;
+      const bool whole = in && (t != 0 || gs == 0) && (t != nwo - 1 || ((cur.G + L) & 63) == 0);
+      uint64_t* dst = whole ? a.out_g + w0 + t : (in ? a.gfrag + 2 * (uint64_t)cur.id + (t == 0 ? 0 : 1) : a.sink + lane);
+      if (k < WPL || in) class_store(dst, whole ? bswap64(x) : x);
+    }
+  };
+#elif !BIC_K0_W16
   // the row's source words (those holding its bits through its end-of-row '1'; the slot may end
   // there): every lane loads, at a clamped index, the words outside masked where used
   auto load = [&](const Row& r, uint64_t (&v)[WPL + 1]) {
@@ -2433,6 +2503,11 @@ __device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t 
 #define BIC_K1_BATCH 3
 #endif
 constexpr int kK1Batch = BIC_K1_BATCH;
+#ifndef BIC_K1_DYN
+#define BIC_K1_DYN 0  // (one ticket counter for every chunk of the ~32k k = 1 rows of C3: emission 157 -> 540 us;
+                      // device-scope atomics on one word stall every wave and the memory channel holding it)
+#endif
+constexpr bool kK1Dyn = BIC_K1_DYN != 0;  // k1_rows: chunks claimed by ticket instead of a static share
 // the k = 1 list's entries i0, i0 + nw, ... (one wave, with its LDS row image and the byte table)
 template <int WPL>
 __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_t nw, uint32_t* gimg,
@@ -2448,8 +2523,9 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     uint32_t id, plane, row;
     uint64_t G, L;
   };
-  auto place = [&](uint32_t k) {
-    const uint64_t e = nrows + i0 + (uint64_t)k * nw;
+  // (list entry e of the k = 1 list)
+  auto place_e = [&](uint64_t e_rel) {
+    const uint64_t e = nrows + e_rel;
     Row r;
     const uint64_t e0 = cls_ld(a, 2 * e);
     r.id = (uint32_t)e0;
@@ -2460,6 +2536,7 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
     r.G = a.off_g ? Gs - (uint64_t)r.plane * a.slot_g * 64 + a.gbase[r.plane] * 64 : Gs;
     return r;
   };
+  auto place = [&](uint32_t k) { return place_e(i0 + (uint64_t)k * nw); };  // the wave's k-th row
 #if BIC_K1_LC
   constexpr int kV = WPL + 1;
   auto emit = [&](const Row& cur, const uint64_t (&v)[kV], uint64_t) {
@@ -2474,10 +2551,12 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
       }
       return;
     }
+    YSTAMP((1u << 18) + cur.id, 0);
     unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
     for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
     uint64_t rr[WPL];
     eg_src_assemble_lc<WPL>(g, cur.row, v, rr);
+    YSTAMP((1u << 18) + cur.id, 1);
     uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
 #if BIC_K1_PI
     // the backward parity form (k1_pi): pi of each word's last column's right context (zeta) from the
@@ -2541,8 +2620,10 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
       if (!tail) lds_or64(img, (tot - 1) >> 6, BIC_MSB >> ((tot - 1) & 63));  // the end-of-row '1'
       if (tot != cur.L) atomicOr(&a.flags[3], 1u);  // the closed-form length disagrees with the emission
     }
+    YSTAMP((1u << 18) + cur.id, 2);
     write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, cur.L, cur.G, a.out_g, a.gfrag + 2 * (uint64_t)cur.id,
                                                      a.sink);
+    YSTAMP((1u << 18) + cur.id, 3);
 #else
     // the lane's words l WPL + t: their last 1s, the wave's exclusive max of the lanes' last 1
     int lastc[WPL], mxl = -1;
@@ -2630,8 +2711,9 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
       }
     }
     if (lane == 0 && loc != cur.L) atomicOr(&a.flags[3], 1u);  // word_len disagrees with the emission
-    // (no fence: one wave's LDS operations run in order, and the image's zeroing, atomics and reads
-    // share one type, so the compiler keeps their order)
+    // (no fence: the image's zeroing, atomics and reads are one wave's 8-byte LDS operations of one type --
+    // the same width, which measured in order where a 16-byte zeroing did not (lds_image_zero32) -- and the
+    // compiler keeps same-typed accesses in their order)
     // (rows up to kCapBits: at most (kCapBits + 63) / 64 + 1 output words)
     write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, cur.L, cur.G, a.out_g, a.gfrag + 2 * (uint64_t)cur.id,
                                                      a.sink);
@@ -2641,6 +2723,31 @@ __device__ __forceinline__ void k1_rows(const FusedArgs& a, uint32_t i0, uint32_
   };
   constexpr int kV = WPL;
 #endif
+  if constexpr (kK1Dyn) {
+    // Chunks of kK1Batch consecutive list entries claimed by ticket (counter[10]; each wave comes here
+    // when its k = 0 share is done, so the waves that finish it early -- the older ones, which win the
+    // memory and issue arbitration -- take more of these rows). The next chunk is claimed after this
+    // chunk's loads and before its stores: the wait for the ticket never covers this chunk's stores.
+    (void)R;
+    uint32_t tv = 0;
+    if (lane == 0) tv = atomicAdd(a.counter + 10, 1u);
+    for (;;) {
+      const uint32_t c = uni_u32(tv) * (uint32_t)kK1Batch;
+      if (c >= n) break;
+      Row r[kK1Batch];
+      uint64_t v[kK1Batch][kV], l[kK1Batch];
+#pragma unroll
+      for (int u = 0; u < kK1Batch; ++u) {
+        r[u] = place_e(c + u < n ? c + u : c);
+        load(r[u], v[u], l[u]);
+      }
+      if (lane == 0) tv = atomicAdd(a.counter + 10, 1u);
+#pragma unroll
+      for (int u = 0; u < kK1Batch; ++u)
+        if (c + u < n) emit(r[u], v[u], l[u]);
+    }
+    return;
+  }
   for (uint32_t k = 0; k < R; k += kK1Batch) {  // (batches as k_emit_k0)
     Row r[kK1Batch];
     uint64_t v[kK1Batch][kV], l[kK1Batch];
@@ -3195,6 +3302,11 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     // is one, so that it can overlap the main launch, which skips the listed rows' parts
     const uint32_t nwv = (g.used + 63) / 64;  // waves per row in k_emit_rest
     const uint32_t rgrid = (uint32_t)std::min<uint64_t>(nrows, (uint64_t)cus * 32 / nwv);  // 32 waves per CU (16: C4 +6 us; 4: C3 +30 us -- the listed rows are latency-bound)
+    // (bic_prof_*: events around the main emission kernel alone, on its stream s -- the roofline kernel's
+    // launch, without the fork / join of the second stream; null: not timed)
+    auto main_ev = [&](hipEvent_t e) {
+      if (e) (void)hipEventRecord(e, s);
+    };
     // (the class kernels' path with the rest role inside k_emit_k01: one launch, no second stream)
     const bool one_launch = es && a.cls && kK01Rest;
     hipStream_t rs = s;
@@ -3205,7 +3317,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   {                                                                                                  \
     k_emit_rest<P, DG, DE><<<rgrid, 64 * nwv, 0, rs>>>(a);                                           \
     static const int occ_ = occ_of(reinterpret_cast<const void*>(&k_emit_known<W, P, DG, DE, ES>));  \
+    main_ev(fs.ev_main0);                                                                            \
     k_emit_known<W, P, DG, DE, ES><<<egrid_of(occ_), 64 * kEmitWaves, 0, s>>>(a);                    \
+    main_ev(fs.ev_main1);                                                                            \
   }
 #define BIC_EMIT(W, P)                                                                                \
   if (dg && de) BIC_EMIT1(W, P, true, true, false) else if (dg) BIC_EMIT1(W, P, true, false, false) else BIC_EMIT1(W, P, false, true, false)
@@ -3220,12 +3334,16 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     static const int o_ = occ_of(reinterpret_cast<const void*>(&k_emit_k01<W>));                      \
     if (one_launch) {                                                                                  \
       a.rgrid = kK01Rg ? kK01Rg : std::max(8u, (uint32_t)cus / 8 * 8);                                 \
+      main_ev(fs.ev_main0);                                                                            \
       const uint32_t pg = (uint32_t)std::min<uint64_t>((nrows + 3) / 4, kK01Rg ? (uint64_t)cus * o_ - a.rgrid   \
                                                                                  : (uint64_t)cus * std::max(1, o_ - 1)); \
       k_emit_k01<W><<<a.rgrid + pg, 256, 0, s>>>(a);                                                   \
+      main_ev(fs.ev_main1);                                                                            \
     } else {                                                                                           \
       k_emit_rest<false, true, false><<<rgrid, 64 * nwv, 0, rs>>>(a);                                  \
+      main_ev(fs.ev_main0);                                                                            \
       k_emit_k01<W><<<egrid_of(o_), 256, 0, s>>>(a);                                                   \
+      main_ev(fs.ev_main1);                                                                            \
     }                                                                                                  \
   }
       if (wpl == 1) { BIC_EMITC(1); } else if (wpl == 2) { BIC_EMITC(2); } else { BIC_EMITC(4); }

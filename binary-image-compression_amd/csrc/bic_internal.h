@@ -136,6 +136,8 @@ struct FusedScratch {
   // the fork / join events; null: one stream
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // (bic_prof_*) recorded on the launch stream around the staged emission's main kernel alone
+  hipEvent_t ev_main0 = nullptr, ev_main1 = nullptr;
   bool counted;      // the count pass already ran (bic_encode_gray's fused bitplane kernel)
   uint32_t* slow_n;
   uint64_t* slow_ids;

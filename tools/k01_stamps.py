@@ -49,3 +49,24 @@ for rep in range(2):
                kmix_rows=int(km.sum()), kmix_start_us=d((Kk[:, 0] - t0) / 100),
                kmix_load_us=d((Kk[:, 1] - Kk[:, 0]) / 100), kmix_code_us=d((Kk[:, 2] - Kk[:, 1]) / 100))
     print(json.dumps(out), flush=True)
+    # where the spread comes from: per XCD (block % 8), per wave of the workgroup, per CU slot (block // 8 % ...)
+    if rep == 1:
+        blk = (idx - 0) // 4
+        pw = idx[idx >= rg]
+        b = pw // 4
+        k0d = (W[pw, 1] - t0) / 100
+        ex = (W[pw, 3] - t0) / 100
+        st = (W[pw, 0] - t0) / 100
+        by = lambda key, v: {int(k): round(float(np.median(v[key == k])), 1) for k in np.unique(key)}  # noqa: E731
+        print(json.dumps(dict(start_us=d(st), k0_done_by_xcd=by(b % 8, k0d), exit_by_xcd=by(b % 8, ex),
+                              k0_done_by_wave=by(pw % 4, k0d), exit_by_wave=by(pw % 4, ex),
+                              k0_done_by_block_third=by(np.minimum(b // (len(b) // 12 + 1), 11), k0d),
+                              k1_phase_us=d(ex - k0d), k0_phase_us=d(k0d - st))), flush=True)
+    # the k = 1 rows' phases (YSTAMP, issue times): entry -> row assembled (its loads waited for) ->
+    # codewords placed in the LDS image -> output stores issued
+    if rep == 1:
+        K1 = K[(K[:, 0] > 0) & (K[:, 3] > 0) & (K[:, 0] != K0[:, 0])]
+        if len(K1):
+            print(json.dumps(dict(k1_rows=int(len(K1)), assemble_us=d((K1[:, 1] - K1[:, 0]) / 100),
+                                  encode_us=d((K1[:, 2] - K1[:, 1]) / 100), write_us=d((K1[:, 3] - K1[:, 2]) / 100),
+                                  total_us=d((K1[:, 3] - K1[:, 0]) / 100))), flush=True)
