@@ -124,6 +124,12 @@ constexpr bool kK01Rest = BIC_K01_REST != 0;
 // the class kernels' path: rows mixing k = 0 and k = 1 by kmix_rows inside k_emit_k01 (the walk's k = 1
 // masks, bic_k1pi.h kmix_*) instead of k_emit_rest's per-codeword encoder
 constexpr bool kKMixRows = BIC_KMIX != 0;
+#ifndef BIC_KNOWN_MIX
+#define BIC_KNOWN_MIX 0
+#endif
+// k_emit_known (planes in, Golomb alone: C4's path): the walked rows mixing k = 0 and k = 1 written by the
+// row's own wave from the walk's k = 1 masks (kmix_encode) instead of by k_emit_rest beside it
+constexpr bool kKnownMix = BIC_KNOWN_MIX != 0;
 #ifndef BIC_K01_RG
 #define BIC_K01_RG 0  // (A/B: the rest role's workgroups; 0: one per CU, the persistent ones one fewer per CU)
 #endif
@@ -1863,13 +1869,13 @@ __global__ __launch_bounds__(512) void k_row_walk(FusedArgs a) {
     uint32_t kor = 0, keol = 0;
     uint64_t kt = 0;
     const bool eol = w == g.used - 1 && h == 1;
-    uint32_t ll = kKMixRows && a.kmask ? word_len_kt(x, w, p.n, p.jp, row * (g.cols + 1), eol, g.cols, kor, kt, keol)
+    uint32_t ll = (kKMixRows || kKnownMix) && a.kmask ? word_len_kt(x, w, p.n, p.jp, row * (g.cols + 1), eol, g.cols, kor, kt, keol)
                                        : word_len(x, w, p.n, p.jp, row * (g.cols + 1), eol, g.cols, kor);
     ll = wave_sum_u32(ll);
     WSTAMP(6);
     const uint64_t ks = __ballot(kor & ~1u), k1s = __ballot(kor & ~2u);  // some k != 0 / some k != 1
     const uint64_t kbig = __ballot(kor & ~3u), ke = __ballot(keol);     // some k >= 2 / the end-of-row k = 1
-    if (kKMixRows && a.kmask && i < a.kcap) {  // the word's k = 1 mask (its two halves' lanes combined) for kmix_row
+    if ((kKMixRows || kKnownMix) && a.kmask && i < a.kcap) {  // the word's k = 1 mask (its two halves' lanes combined) for kmix_row
       const uint64_t kw = kWalkSplit == 2 ? kt | shfl_u64(kt, lane ^ 1) : kt;
       if ((kWalkSplit == 1 || h == 0) && w < g.used) a.kmask[(uint64_t)i * g.used + w] = kw;
     }
@@ -1912,12 +1918,134 @@ constexpr int kEmitWaves = 4;
 #define BIC_REST_AUX 1
 #endif
 constexpr bool kRestAux = BIC_REST_AUX != 0;  // k_emit_rest on the context's second stream (beside k_emit_known)
+#ifndef BIC_CLASS_NT
+#define BIC_CLASS_NT 0
+#endif
+// the class kernels' output stores (typed unsigned long long; BIC_CLASS_NT: non-temporal)
+__device__ __forceinline__ void class_store(uint64_t* dst, uint64_t v) {
+  if constexpr (BIC_CLASS_NT) __builtin_nontemporal_store((unsigned long long)v, reinterpret_cast<unsigned long long*>(dst));
+  else *reinterpret_cast<unsigned long long*>(dst) = v;
+}
+// write_row64 with a fixed number of store instructions (MAXT per lane, the idle lanes' to a.sink)
+// and its stores typed unsigned long long (k_emit_k0)
+template <int MAXT>
+__device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t L, uint64_t G, uint64_t* out,
+                                                  uint64_t* frag, uint64_t* sink) {
+  const int lane = lane_id();
+  const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6;
+  const uint32_t nw = (uint32_t)(w1 - w0 + 1), g = (uint32_t)(G & 63);
+  const bool head_whole = g == 0, tail_whole = ((G + L) & 63) == 0;
+#pragma unroll
+  for (int it = 0; it < MAXT; ++it) {
+    const uint32_t t = it * 64 + lane;
+    const bool in = t < nw;
+    const uint32_t tc = in ? t : 0u;
+    // (the image read as unsigned long long, the type its atomics write: ordered after them)
+    const unsigned long long* im = reinterpret_cast<const unsigned long long*>(img);
+    const uint64_t cur = im[tc], prev = tc ? im[tc - 1] : 0ull;
+    const uint64_t v = funnel64(prev, cur, g);
+    const bool whole = in && (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
+    uint64_t* dst = whole ? out + w0 + t : (in ? frag + (t == 0 ? 0 : 1) : sink + lane);
+    class_store(dst, whole ? bswap64(v) : v);
+  }
+}
+
+// Rows mixing k = 0 and k = 1 (the walk stored each word's k = 1 mask): the backward-parity rows of
+// k1_rows with every column's k from the masks (bic_k1pi.h kmix_kk / kmix_word_*: a byte whose columns
+// share one k through the k = 1 table or verbatim, a byte where k changes column by column).
+// GolombCoder.cpp:13-34 per codeword. Lane l holds words t * 64 + l (one word group at a time: few
+// registers). kmix_encode: the row's residual words rr and k = 1 masks ktw into the wave's LDS image
+// gimg, then out (L bits at G; the words shared with neighbouring rows to the fragment table).
+template <int WPL>
+__device__ __forceinline__ void kmix_encode(const FusedArgs& a, const uint64_t (&rr)[WPL], const uint64_t (&ktw)[WPL],
+                                            uint32_t keol, uint64_t id, uint64_t L, uint64_t G, uint32_t* gimg,
+                                            const uint32_t* s_lut) {
+  const Geom& g = a.g;
+  const int lane = lane_id();
+  constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
+  const uint32_t tail = g.cols & 63u;  // columns of the row's last word (0: a full word)
+    unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
+    for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
+    uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
+    auto ws = [&](int t, uint64_t& xt, uint64_t& Z, uint64_t& kt) {
+      const uint32_t w = (uint32_t)t * 64 + lane;
+      const uint64_t valid = w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
+      const uint64_t eb = (w == g.used - 1 && tail) ? (BIC_MSB >> tail) : 0ull;  // the end-of-row 1
+      xt = rr[t] | eb;
+      Z = ~xt & valid;
+      kt = (ktw[t] & rr[t]) | (keol ? eb : 0ull);
+    };
+    // zeta (pi right of the word) and nk (the k of the first codeword ending after the word): from the
+    // nearest lane to the right in the word's group holding a 1, else from the first such word of a
+    // later group (carried), else the end of the row
+    uint32_t zb = 0, kb = 0, zc = 0, kc = keol;
+#pragma unroll
+    for (int t = WPL - 1; t >= 0; --t) {
+      uint64_t xt, Z, kt;
+      ws(t, xt, Z, kt);
+      const uint32_t cz = xt ? (uint32_t)__builtin_clzll(xt) : 0u;
+      const uint32_t lead = cz & 1u, leadk = (uint32_t)(kt >> (63 - cz)) & 1u;
+      const uint64_t m1 = __ballot(xt != 0);
+      const uint64_t nm = m1 & ~((2ull << lane) - 1ull);
+      const int src = nm ? (int)__builtin_ctzll(nm) : lane;
+      const uint32_t ln = (uint32_t)__shfl((int)lead, src), lnk = (uint32_t)__shfl((int)leadk, src);
+      zb |= (nm ? ln : zc) << t;
+      kb |= (nm ? lnk : kc) << t;
+      if (m1) {
+        const int f = (int)__builtin_ctzll(m1);
+        zc = (uint32_t)__builtin_amdgcn_readlane((int)lead, f);
+        kc = (uint32_t)__builtin_amdgcn_readlane((int)leadk, f);
+      }
+    }
+    const uint32_t kk0 = kc, lf = zc;  // the row's first codeword's k (its remainder bit leads), pi(-1)
+    const uint32_t* T = s_lut;
+    uint32_t loc = kk0;
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      if (t * 64 >= (int)g.used) break;
+      const uint32_t w = (uint32_t)t * 64 + lane;
+      uint64_t xt, Z, kt;
+      ws(t, xt, Z, kt);
+      const uint32_t zt = (zb >> t) & 1u, nt = (kb >> t) & 1u;
+      const uint64_t Pi = k1_pi(xt, Z, zt), KK = kmix_kk(xt, Z, kt, nt);
+      uint64_t hi = 0, lo = 0, A, B;
+      uint32_t Lw = 0;
+      if (w < g.used) {
+        if (w == g.used - 1 && tail) Lw = kmix_word_last(rr[t], Pi, KK, nt, tail, hi, lo);
+        else Lw = kmix_word_full2(rr[t], Pi, KK, nt, T, hi, lo);
+      }
+      left128(hi, lo, Lw ? Lw : 128u, A, B);
+      const uint32_t inc = wave_incl_sum_u32(Lw);
+      place128_64(img, loc + inc - Lw, A, B, Lw);
+      loc += lane63_u32(inc);
+    }
+    const uint32_t tot = loc + (tail ? 0u : 1u);
+    if (lane == 0) {
+      if (kk0 && lf) lds_or64(img, 0, BIC_MSB);
+      if (!tail) lds_or64(img, (tot - 1) >> 6, BIC_MSB >> ((tot - 1) & 63));  // the end-of-row '1'
+      if (tot != L) atomicOr(&a.flags[3], 1u);  // the walk's length disagrees with the emission
+    }
+    write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, L, G, a.out_g, a.gfrag + 2 * (uint64_t)id, a.sink);
+}
+
+// kmask / row_wi of a kKMix row: its words' k = 1 masks (word t * 64 + lane)
+template <int WPL>
+__device__ __forceinline__ void kmix_masks(const FusedArgs& a, uint64_t id, uint64_t (&ktw)[WPL]) {
+  const uint64_t* km = a.kmask + (uint64_t)a.row_wi[id] * a.g.used;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) {
+    const uint32_t w = (uint32_t)t * 64 + lane_id();
+    ktw[t] = km[w < a.g.used ? w : a.g.used - 1];
+  }
+}
+
 // One row of k_emit_known (rr: its residual words; O, Lf, Gb: its ones before, Golomb length + flags,
 // absolute Golomb bit offset; Eb: its plane's EG start bit), by one wave with its LDS image gimg.
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E>
 __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, uint32_t plane, uint32_t row,
                                                const uint64_t (&rr)[WPL], uint32_t O, uint64_t Lf, uint64_t Gb,
-                                               uint64_t Eb, uint32_t* gimg, const uint32_t* s_lut) {
+                                               uint64_t Eb, uint32_t* gimg, const uint32_t* s_lut,
+                                               const uint32_t* s_lut2 = nullptr) {
   const Geom& g = a.g;
   const int lane = lane_id();
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
@@ -2041,6 +2169,10 @@ __device__ __forceinline__ void emit_known_row(const FusedArgs& a, uint64_t id, 
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       write_row64(img, L, Gb, a.out_g, a.gfrag + 2 * id);
+    } else if (kKnownMix && !DO_E && a.kmask && (Lf & kKMix) && L && fits) {  // k = 0 and k = 1 mixed
+      uint64_t ktw[WPL];
+      kmix_masks<WPL>(a, id, ktw);
+      kmix_encode<WPL>(a, rr, ktw, (Lf & kKEol1) ? 1u : 0u, id, L, Gb, gimg, s_lut2);
     }
     if (lane == 0) {
       // glen keeps its flags: k_emit_rest (on the other stream) reads them too
@@ -2058,15 +2190,21 @@ template <int WPL>
 constexpr int kKnownBatch = WPL == 1 ? BIC_KNOWN_BATCH : 1;
 // ES: the residual rows from the EG stream the count pass wrote (FusedArgs::esrc; PREDICT false)
 template <int WPL, bool PREDICT, bool DO_G, bool DO_E, bool ES = false>
-__global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) {
+#ifndef BIC_KNOWN_MINW
+#define BIC_KNOWN_MINW 4  // (k_emit_known<1>: minimum waves per SIMD the compiler must fit)
+#endif
+__global__ __launch_bounds__(64 * kEmitWaves, WPL == 1 ? BIC_KNOWN_MINW : 4) void k_emit_known(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kEmitWaves * kGImg];
   __shared__ uint32_t s_lut[512];
+  __shared__ uint32_t s_lut2[kKnownMix && DO_G && !DO_E ? 512 : 1];  // (kmix_encode: the k = 1 parity table)
   const Geom& g = a.g;
   [[maybe_unused]] const int lane = lane_id();
   const int wave = (int)wave_id();
   uint32_t* gimg = lds + wave * kGImg;
   if (DO_G)
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kKnownTable + i];
+  if constexpr (kKnownMix && DO_G && !DO_E)
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut2[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[kK1Table + i];
   __syncthreads();  // the only workgroup barrier
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
   // persistent waves: rows id, id + stride, ...
@@ -2099,7 +2237,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
         uint64_t rr[WPL];
         row_resid<WPL, PREDICT>(g, row, cp_[u], cu_[u], rr);
         const uint64_t Eb = DO_E ? (a.ebase ? a.ebase[plane] : (uint64_t)plane * a.slot_e * 64) : 0;
-        emit_known_row<WPL, PREDICT, DO_G, DO_E>(a, iu, plane, row, rr, O[u], Lf[u], Gb[u], Eb, gimg, s_lut);
+        emit_known_row<WPL, PREDICT, DO_G, DO_E>(a, iu, plane, row, rr, O[u], Lf[u], Gb[u], Eb, gimg, s_lut, s_lut2);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
         __builtin_amdgcn_wave_barrier();
       }
@@ -2126,7 +2264,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
       row_resid<WPL, PREDICT>(g, row, cp_, cu_, rr);
     }
     const uint64_t Eb = DO_E ? (a.ebase ? a.ebase[plane] : (uint64_t)plane * a.slot_e * 64) : 0;
-    emit_known_row<WPL, PREDICT, DO_G, DO_E>(a, id, plane, row, rr, O, Lf, Gb, Eb, gimg, s_lut);
+    emit_known_row<WPL, PREDICT, DO_G, DO_E>(a, id, plane, row, rr, O, Lf, Gb, Eb, gimg, s_lut, s_lut2);
     STAMP(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next row reuses the LDS image
     __builtin_amdgcn_wave_barrier();
@@ -2148,14 +2286,6 @@ __global__ __launch_bounds__(64 * kEmitWaves, 4) void k_emit_known(FusedArgs a) 
 // scalar cache (the kernels' stores are typed unsigned long long, apart from the entries' u64, and
 // they hold no fence or workgroup barrier, so the compiler proves the entries unclobbered), the
 // compiler waits for the loads alone.
-#ifndef BIC_CLASS_NT
-#define BIC_CLASS_NT 0
-#endif
-// the class kernels' output stores (typed unsigned long long; BIC_CLASS_NT: non-temporal)
-__device__ __forceinline__ void class_store(uint64_t* dst, uint64_t v) {
-  if constexpr (BIC_CLASS_NT) __builtin_nontemporal_store((unsigned long long)v, reinterpret_cast<unsigned long long*>(dst));
-  else *reinterpret_cast<unsigned long long*>(dst) = v;
-}
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
@@ -2472,30 +2602,6 @@ __device__ __forceinline__ void k0_rows(const FusedArgs& a, uint32_t i0, uint32_
 }
 #undef BIC_K0_VT
 #undef BIC_K0_VN
-
-// write_row64 with a fixed number of store instructions (MAXT per lane, the idle lanes' to a.sink)
-// and its stores typed unsigned long long (k_emit_k0)
-template <int MAXT>
-__device__ __forceinline__ void write_row64_fixed(const uint64_t* img, uint64_t L, uint64_t G, uint64_t* out,
-                                                  uint64_t* frag, uint64_t* sink) {
-  const int lane = lane_id();
-  const uint64_t w0 = G >> 6, w1 = (G + L - 1) >> 6;
-  const uint32_t nw = (uint32_t)(w1 - w0 + 1), g = (uint32_t)(G & 63);
-  const bool head_whole = g == 0, tail_whole = ((G + L) & 63) == 0;
-#pragma unroll
-  for (int it = 0; it < MAXT; ++it) {
-    const uint32_t t = it * 64 + lane;
-    const bool in = t < nw;
-    const uint32_t tc = in ? t : 0u;
-    // (the image read as unsigned long long, the type its atomics write: ordered after them)
-    const unsigned long long* im = reinterpret_cast<const unsigned long long*>(img);
-    const uint64_t cur = im[tc], prev = tc ? im[tc - 1] : 0ull;
-    const uint64_t v = funnel64(prev, cur, g);
-    const bool whole = in && (t != 0 || head_whole) && (t != nw - 1 || tail_whole);
-    uint64_t* dst = whole ? out + w0 + t : (in ? frag + (t == 0 ? 0 : 1) : sink + lane);
-    class_store(dst, whole ? bswap64(v) : v);
-  }
-}
 
 // k = 1 rows: emit_known_row's byte-table path (encode_word_k1b into a 64-bit LDS row image, then
 // write_row64_fixed); rows whose image exceeds the window are listed for k_rows_global.
@@ -2877,105 +2983,32 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
   }
 }
 
-// Rows mixing k = 0 and k = 1 (the class entries' third list; the walk stored each word's k = 1 mask):
-// the backward-parity rows of k1_rows with every column's k from the masks (bic_k1pi.h kmix_kk /
-// kmix_word_*: a byte whose columns share one k through the k = 1 table or verbatim, a byte where k
-// changes column by column). GolombCoder.cpp:13-34 per codeword. Lane l holds words t * 64 + l (one
-// word group at a time: few registers, as these rows are ~1 % of a C3 step's).
+// the class entries' third list (BIC_KMIX: k_emit_k01's rest role), residual rows from the EG stream
 template <int WPL>
 __device__ __forceinline__ void kmix_row(const FusedArgs& a, uint32_t i, uint32_t* gimg, const uint32_t* s_lut) {
   const Geom& g = a.g;
   const int lane = lane_id();
   constexpr uint32_t kCapBits = (kGImg - kPad) * 32;
   const uint64_t nrows = (uint64_t)g.rows * g.nplanes;
-  const uint32_t tail = g.cols & 63u;  // columns of the row's last word (0: a full word)
-  {
-    const uint64_t e = 2 * nrows + i;
-    const uint64_t e0 = cls_ld(a, 2 * e);
-    const uint32_t id = (uint32_t)e0;
-    const uint64_t L = e0 >> 32;
-    const uint32_t plane = id / g.rows, row = id % g.rows;
-    const uint64_t Gs = cls_ld(a, 2 * e + 1);
-    const uint64_t G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
-    XSTAMP((1u << 18) + id, 0);
-    const uint64_t* km = a.kmask + (uint64_t)a.row_wi[id] * g.used;
-    const uint32_t keol = (a.glen[id] & kKEol1) ? 1u : 0u;
-    uint64_t rr[WPL], ktw[WPL];
-    eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
-#pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      const uint32_t w = (uint32_t)t * 64 + lane;
-      ktw[t] = km[w < g.used ? w : g.used - 1];
-    }
-    XSTAMP((1u << 18) + id, 1);
-    if (L > kCapBits) {  // (the LEN scan lists such rows as slow, never here: a length disagreement)
-      if (lane == 0) atomicOr(&a.flags[3], 1u);
-      return;
-    }
-    unsigned long long* z = reinterpret_cast<unsigned long long*>(gimg);
-    for (int j = lane; j < kGImg / 2; j += 64) z[j] = 0ull;
-    uint64_t* img = reinterpret_cast<uint64_t*>(gimg);
-    auto ws = [&](int t, uint64_t& xt, uint64_t& Z, uint64_t& kt) {
-      const uint32_t w = (uint32_t)t * 64 + lane;
-      const uint64_t valid = w < g.used ? (w == g.used - 1 ? g.trail : ~0ull) : 0ull;
-      const uint64_t eb = (w == g.used - 1 && tail) ? (BIC_MSB >> tail) : 0ull;  // the end-of-row 1
-      xt = rr[t] | eb;
-      Z = ~xt & valid;
-      kt = (ktw[t] & rr[t]) | (keol ? eb : 0ull);
-    };
-    // zeta (pi right of the word) and nk (the k of the first codeword ending after the word): from the
-    // nearest lane to the right in the word's group holding a 1, else from the first such word of a
-    // later group (carried), else the end of the row
-    uint32_t zb = 0, kb = 0, zc = 0, kc = keol;
-#pragma unroll
-    for (int t = WPL - 1; t >= 0; --t) {
-      uint64_t xt, Z, kt;
-      ws(t, xt, Z, kt);
-      const uint32_t cz = xt ? (uint32_t)__builtin_clzll(xt) : 0u;
-      const uint32_t lead = cz & 1u, leadk = (uint32_t)(kt >> (63 - cz)) & 1u;
-      const uint64_t m1 = __ballot(xt != 0);
-      const uint64_t nm = m1 & ~((2ull << lane) - 1ull);
-      const int src = nm ? (int)__builtin_ctzll(nm) : lane;
-      const uint32_t ln = (uint32_t)__shfl((int)lead, src), lnk = (uint32_t)__shfl((int)leadk, src);
-      zb |= (nm ? ln : zc) << t;
-      kb |= (nm ? lnk : kc) << t;
-      if (m1) {
-        const int f = (int)__builtin_ctzll(m1);
-        zc = (uint32_t)__builtin_amdgcn_readlane((int)lead, f);
-        kc = (uint32_t)__builtin_amdgcn_readlane((int)leadk, f);
-      }
-    }
-    const uint32_t kk0 = kc, lf = zc;  // the row's first codeword's k (its remainder bit leads), pi(-1)
-    const uint32_t* T = s_lut;
-    uint32_t loc = kk0;
-#pragma unroll
-    for (int t = 0; t < WPL; ++t) {
-      if (t * 64 >= (int)g.used) break;
-      const uint32_t w = (uint32_t)t * 64 + lane;
-      uint64_t xt, Z, kt;
-      ws(t, xt, Z, kt);
-      const uint32_t zt = (zb >> t) & 1u, nt = (kb >> t) & 1u;
-      const uint64_t Pi = k1_pi(xt, Z, zt), KK = kmix_kk(xt, Z, kt, nt);
-      uint64_t hi = 0, lo = 0, A, B;
-      uint32_t Lw = 0;
-      if (w < g.used) {
-        if (w == g.used - 1 && tail) Lw = kmix_word_last(rr[t], Pi, KK, nt, tail, hi, lo);
-        else Lw = kmix_word_full(rr[t], Pi, KK, nt, T, hi, lo);
-      }
-      left128(hi, lo, Lw ? Lw : 128u, A, B);
-      const uint32_t inc = wave_incl_sum_u32(Lw);
-      place128_64(img, loc + inc - Lw, A, B, Lw);
-      loc += lane63_u32(inc);
-    }
-    const uint32_t tot = loc + (tail ? 0u : 1u);
-    if (lane == 0) {
-      if (kk0 && lf) lds_or64(img, 0, BIC_MSB);
-      if (!tail) lds_or64(img, (tot - 1) >> 6, BIC_MSB >> ((tot - 1) & 63));  // the end-of-row '1'
-      if (tot != L) atomicOr(&a.flags[3], 1u);  // the walk's length disagrees with the emission
-    }
-    write_row64_fixed<(kCapBits / 64 + 1 + 63) / 64>(img, L, G, a.out_g, a.gfrag + 2 * (uint64_t)id, a.sink);
-    XSTAMP((1u << 18) + id, 2);
+  const uint64_t e = 2 * nrows + i;
+  const uint64_t e0 = cls_ld(a, 2 * e);
+  const uint32_t id = (uint32_t)e0;
+  const uint64_t L = e0 >> 32;
+  const uint32_t plane = id / g.rows, row = id % g.rows;
+  const uint64_t Gs = cls_ld(a, 2 * e + 1);
+  const uint64_t G = a.off_g ? Gs - (uint64_t)plane * a.slot_g * 64 + a.gbase[plane] * 64 : Gs;
+  XSTAMP((1u << 18) + id, 0);
+  const uint32_t keol = (a.glen[id] & kKEol1) ? 1u : 0u;
+  uint64_t rr[WPL], ktw[WPL];
+  eg_src_row<WPL>(a.esrc + (uint64_t)plane * a.slot_e, g, row, rr);
+  kmix_masks<WPL>(a, id, ktw);
+  XSTAMP((1u << 18) + id, 1);
+  if (L > kCapBits) {  // (the LEN scan lists such rows as slow, never here: a length disagreement)
+    if (lane == 0) atomicOr(&a.flags[3], 1u);
+    return;
   }
+  kmix_encode<WPL>(a, rr, ktw, keol, id, L, G, gimg, s_lut);
+  XSTAMP((1u << 18) + id, 2);
 }
 
 // The class launch's rest role (the FusedArgs::rgrid leading workgroups of k_emit_k01, dispatched first,
@@ -3231,7 +3264,9 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
   a.cls = es && out_g && !fs.eg_src_one ? fs.cls : nullptr;
   a.sink = fs.sink;
   // the walk stores the k = 1 masks of mixed rows for kmix_rows (class kernels' path only)
-  a.kmask = a.cls && kKMixRows && kK01Rest ? fs.kmask : nullptr;  // (k_emit_k01's rest role writes kKMix rows)
+  // (k_emit_k01's rest role writes kKMix rows; or k_emit_known itself, planes in and Golomb alone)
+  a.kmask = (a.cls && kKMixRows && kK01Rest) || (kKnownMix && !es && out_g && !out_e && mode == kEncStaged) ? fs.kmask
+                                                                                                            : nullptr;
   a.row_wi = fs.row_wi;
   a.kcap = fs.kcap;
 #ifdef BIC_STAMPS

@@ -156,6 +156,61 @@ BIC_NOUNROLL
   }
   return L;
 }
+// The same, with the eight table reads issued together (one LDS round trip per word, as k1_word_full):
+// every byte's entry is read, used when the byte and the column after it all have kk = 1; a byte with
+// kk = 0 throughout is verbatim; the bytes where kk changes (a few per mixed row) go column by column.
+BIC_HDI uint32_t kmix_word_full2(uint64_t x, uint64_t Pi, uint64_t KK, uint32_t kkn, const uint32_t* T, uint64_t& hi,
+                                 uint64_t& lo) {
+  const uint64_t KN = (KK << 1) | (uint64_t)kkn;
+  uint32_t b[8], l[8];
+  uint32_t mixed = 0;  // bit j: byte j goes column by column
+BIC_UNROLL
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t sh = 56 - 8 * j;
+    const uint32_t xb = (uint32_t)(x >> sh) & 0xffu, kb = (uint32_t)(KK >> sh) & 0xffu, kn = (uint32_t)(KN >> sh) & 0xffu;
+    const uint32_t e = T[(((uint32_t)(Pi >> sh) & 1u) << 8) | xb];
+    const bool one = kb == 0xffu && kn == 0xffu, zero = kb == 0 && kn == 0;
+    b[j] = one ? (e & 0xffffu) : xb;
+    l[j] = one ? (e >> 16) : 8u;
+    mixed |= (one || zero) ? 0u : (1u << j);
+  }
+  if (mixed) {
+BIC_NOUNROLL
+    for (int j = 0; j < 8; ++j) {
+      if (!((mixed >> j) & 1u)) continue;
+      const uint32_t sh = 56 - 8 * j;
+      const uint32_t xb = (uint32_t)(x >> sh) & 0xffu, kb = (uint32_t)(KK >> sh) & 0xffu, kn = (uint32_t)(KN >> sh) & 0xffu;
+      const uint32_t pv = (uint32_t)(Pi >> sh) & 0xffu;
+      uint64_t bb = 0;
+      uint32_t ll = 0;
+BIC_NOUNROLL
+      for (int c = 7; c >= 0; --c) kmix_col((xb >> c) & 1u, (pv >> c) & 1u, (kb >> c) & 1u, (kn >> c) & 1u, bb, ll);
+      // (constant indices below: select the slot instead of indexing the arrays dynamically)
+BIC_UNROLL
+      for (int q = 0; q < 8; ++q)
+        if (q == j) {
+          b[q] = (uint32_t)bb;
+          l[q] = ll;
+        }
+    }
+  }
+  // joined as k1_word_full: pairs (<= 32 bits), fours (<= 64), the two halves into 128 bits
+  uint64_t q[2];
+  uint32_t lq[2];
+BIC_UNROLL
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t* bh = b + 4 * h;
+    const uint32_t* lh = l + 4 * h;
+    const uint32_t p0 = (bh[0] << lh[1]) | bh[1], p1 = (bh[2] << lh[3]) | bh[3];
+    const uint32_t lp1 = lh[2] + lh[3];
+    q[h] = ((uint64_t)p0 << lp1) | p1;
+    lq[h] = lh[0] + lh[1] + lp1;
+  }
+  const uint32_t lb = lq[1];
+  lo = lb >= 64 ? q[1] : (q[0] << lb) | q[1];
+  hi = lb >= 64 ? q[0] : (lb ? q[0] >> (64 - lb) : 0ull);
+  return lq[0] + lb;
+}
 // the word holding the row's end (nvalid < 64 columns, or the end-of-row 1 right after it), column by
 // column; includes the end-of-row '1' (KK's bit at column nvalid: the end-of-row codeword's k)
 BIC_HDI uint32_t kmix_word_last(uint64_t x, uint64_t Pi, uint64_t KK, uint32_t kkn, uint32_t nvalid, uint64_t& hi,

@@ -284,7 +284,7 @@ static std::vector<int> encode_row_mixed_strided(const std::vector<uint64_t>& ro
       const uint64_t Pi = k1_pi(xt, Z, zt), KK = kmix_kk(xt, Z, kt, nt);
       uint64_t hi = 0, lo = 0, A, B;
       const bool last = w == used - 1 && tail;
-      const uint32_t L = last ? kmix_word_last(x, Pi, KK, nt, tail, hi, lo) : kmix_word_full(x, Pi, KK, nt, T, hi, lo);
+      const uint32_t L = last ? kmix_word_last(x, Pi, KK, nt, tail, hi, lo) : kmix_word_full2(x, Pi, KK, nt, T, hi, lo);
       if (L != kmix_word_len(x, Z, Pi, KK, nt, last)) {
         fprintf(stderr, "kmix_word_len disagrees at word %u\n", w);
         exit(4);
