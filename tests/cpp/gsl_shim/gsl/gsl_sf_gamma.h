@@ -7,9 +7,11 @@
  * reference build is made with it. The expected output is assembled from the reference's own loop
  * objects (oracle/ref_capi.cpp) with the same lnchoose, so both sides see the same enumL values.
  *
- * ln C(n, m) as a left-to-right sum of log((n - m + i) / i), i = 1..m, with m = min(m, n - m) as GSL
- * does (gsl_sf_lnchoose_e); accurate to a few ulps, and reproducible from Python's math.log (libm's
- * log), which tests/test_dropin_compress.py uses for the expected lines. */
+ * ln C(n, m) as a left-to-right sum of log((n - m + i) / i), i = 1..m. Only the symmetry step
+ * m = min(m, n - m) matches GSL's gsl_sf_lnchoose_e; GSL itself takes differences of lnfact, so the two
+ * can differ in the last ulps. The sum is reproducible from Python's math.log (libm's log), which
+ * tests/test_dropin_compress.py uses for the expected lines. Parity of enumL with a GSL-linked build is
+ * therefore unpinned: a last-ulp difference that flips a ceil in enumL would not be caught here. */
 #ifndef BIC_TEST_GSL_SF_GAMMA_H
 #define BIC_TEST_GSL_SF_GAMMA_H
 #include <math.h>
