@@ -71,9 +71,19 @@ struct bic_ctx {
 
 namespace {
 
+// A failing HIP call returns BIC_EDEVICE; with BIC_VERBOSE set in the environment it is also named on
+// stderr (source line, call, HIP's error string)
+void hip_fail(hipError_t e, int line, const char* what) {
+  static const bool verbose = std::getenv("BIC_VERBOSE") != nullptr;
+  if (verbose) std::fprintf(stderr, "bic_capi.cpp:%d: %s: %s\n", line, what, hipGetErrorString(e));
+}
 #define BIC_HIP(x)                                  \
   do {                                              \
-    if ((x) != hipSuccess) return BIC_EDEVICE;      \
+    const hipError_t bic_e_ = (x);                  \
+    if (bic_e_ != hipSuccess) {                     \
+      hip_fail(bic_e_, __LINE__, #x);               \
+      return BIC_EDEVICE;                           \
+    }                                               \
   } while (0)
 #ifndef BIC_PROF_EVENT_FLAGS
 #define BIC_PROF_EVENT_FLAGS hipEventDisableSystemFence
@@ -105,13 +115,16 @@ void timed_rows(bic_ctx* ctx, bic::FusedScratch& fs, const char* name, F&& launc
   const std::string stage_name = std::string(name) + "_stage";
   const bool k = prof_wants(ctx, name), st = prof_wants(ctx, stage_name.c_str());
   hipEvent_t a = nullptr, b = nullptr, sa = nullptr, sb = nullptr;
+  bool main_rec = false;
   if (k) {
     a = take_event(ctx);
     b = take_event(ctx);
-    // (recorded here too: a path without a separate main kernel then times the whole stage)
+    // (recorded here too: a path without a separate main kernel -- the single and two-pass encoders --
+    // then times the whole stage, b recorded below)
     (void)hipEventRecord(a, ctx->cur);
     fs.ev_main0 = a;
     fs.ev_main1 = b;
+    fs.ev_main_rec = &main_rec;
   }
   if (st) {
     sa = take_event(ctx);
@@ -119,12 +132,16 @@ void timed_rows(bic_ctx* ctx, bic::FusedScratch& fs, const char* name, F&& launc
     (void)hipEventRecord(sa, ctx->cur);
   }
   launch();
+  // (an event never recorded would fail hipEventElapsedTime, and that error would stay pending for
+  // the next call's hipGetLastError)
+  if (k && !main_rec) (void)hipEventRecord(b, ctx->cur);
   if (st) {
     (void)hipEventRecord(sb, ctx->cur);
     ctx->recs.push_back({stage_name, sa, sb});
   }
   if (k) {
     fs.ev_main0 = fs.ev_main1 = nullptr;
+    fs.ev_main_rec = nullptr;
     ctx->recs.push_back({name, a, b});
   }
 }
@@ -324,6 +341,7 @@ int bic_sync(bic_ctx* ctx) {
   uint32_t f[4] = {0, 0, 0, 0};
   BIC_HIP(hipMemcpy(f, ctx->flags, sizeof(f), hipMemcpyDeviceToHost));
   if (f[0] || f[1] || f[2] || f[3]) BIC_HIP(hipMemset(ctx->flags, 0, sizeof(f)));
+  if (f[2] || f[3]) hip_fail(hipSuccess, __LINE__, f[2] ? "look-back record flag" : "length disagreement flag");
   if (f[2]) return BIC_EDEVICE;  // a look-back record never arrived (should not happen)
   if (f[3]) return BIC_EDEVICE;  // the row encoder's length pass disagreed with its emission (a bug)
   if (f[1] & 2u) return BIC_EDATA;  // a decoder met a malformed stream
@@ -1282,6 +1300,7 @@ int bic_prof_collect(bic_ctx* ctx, char* buf, size_t cap) {
     ctx->pool.push_back(r.b);
   }
   ctx->recs.clear();
+  (void)hipGetLastError();  // a failed elapsed-time query (-1 above) must not fail the next call
   std::string outs;
   for (auto& kv : agg) {
     char line[160];

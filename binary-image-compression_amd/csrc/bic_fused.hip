@@ -3340,7 +3340,7 @@ void launch_fused(hipStream_t s, const Geom& g, const uint64_t* planes, const ui
     // (bic_prof_*: events around the main emission kernel alone, on its stream s -- the roofline kernel's
     // launch, without the fork / join of the second stream; null: not timed)
     auto main_ev = [&](hipEvent_t e) {
-      if (e) (void)hipEventRecord(e, s);
+      if (e && hipEventRecord(e, s) == hipSuccess && e == fs.ev_main1 && fs.ev_main_rec) *fs.ev_main_rec = true;
     };
     // (the class kernels' path with the rest role inside k_emit_k01: one launch, no second stream)
     const bool one_launch = es && a.cls && kK01Rest;

@@ -138,6 +138,7 @@ struct FusedScratch {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // (bic_prof_*) recorded on the launch stream around the staged emission's main kernel alone
   hipEvent_t ev_main0 = nullptr, ev_main1 = nullptr;
+  bool* ev_main_rec = nullptr;  // set true when ev_main1 was recorded (paths without a main kernel leave it)
   bool counted;      // the count pass already ran (bic_encode_gray's fused bitplane kernel)
   uint32_t* slow_n;
   uint64_t* slow_ids;
