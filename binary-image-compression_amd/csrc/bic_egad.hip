@@ -381,7 +381,16 @@ __host__ __device__ __forceinline__ uint32_t nib_j(uint32_t i) { return i < 16 ?
 __host__ __device__ __forceinline__ uint32_t nib_idx(uint32_t i, uint32_t c) {
   return i == kFresh ? 60u : ((((i & 3u) | 4u) << (i >> 2)) - 4u + c);
 }
-// entry: bits (right-aligned, <= 20) | count << 24 | i' << 32 | c' << 40
+// A coder state as one word (the walks of k_egad_llen / k_egad_lemit): i | c << 8, and either its table
+// row x 16 << 16 (i <= 15 or the fresh coder) or bit 31 (i > 15: no table row, pixel by pixel; c then
+// up to 2^15 - 1, bits 8..22). Equal words are equal states.
+__host__ __device__ __forceinline__ uint32_t nib_st(uint32_t i, uint32_t c) {
+  return (i < 16 || i == kFresh) ? (i | c << 8 | nib_idx(i, c) * 16 << 16) : (i | c << 8 | 0x80000000u);
+}
+__device__ __forceinline__ uint32_t st_i(uint32_t st) { return st & 63u; }
+__device__ __forceinline__ uint32_t st_c(uint32_t st) { return (st >> 8) & ((int32_t)st < 0 ? 0x7FFFu : 0xFFu); }
+// entry: bits (right-aligned, <= 20) | count << 24 | nib_st(i', c') << 32 (c' <= 7: one nibble from a
+// state of block size <= 8)
 void egad_build_nib(uint64_t* T) {
   for (uint32_t i0 = 0; i0 <= kFresh; ++i0) {
     if (i0 >= 16 && i0 != kFresh) continue;
@@ -404,7 +413,7 @@ void egad_build_nib(uint64_t* T) {
             c = 0;
           }
         }
-        T[nib_idx(i0, c0) * 16 + nib] = bits | ((uint64_t)n << 24) | ((uint64_t)i << 32) | ((uint64_t)c << 40);
+        T[nib_idx(i0, c0) * 16 + nib] = bits | ((uint64_t)n << 24) | ((uint64_t)nib_st(i, c) << 32);
       }
   }
 }
@@ -462,7 +471,7 @@ struct NibCoder {
       const uint32_t cnt = (uint32_t)(e >> 24) & 31u;
       if (cnt) out((uint32_t)e & 0xFFFFFFu, cnt);
       i = (uint32_t)(e >> 32) & 63u;
-      c = (uint32_t)(e >> 40);
+      c = (uint32_t)(e >> 40) & 0xFFu;
     } else {
       pixels(nib, n, out);
     }
@@ -568,6 +577,167 @@ __device__ __forceinline__ void eg_lane_nib2(const EgLane<WPL>& L, uint32_t used
   }
 }
 
+// ---- The lane walk as a chain of table steps (k_egad_llen, k_egad_lemit, the lane chain) ------------
+// The same coder over the same columns as eg_lane_nib, with other step boundaries: the zeros before the
+// nibble of the lane's first 1, then EVERY nibble from there to the one before the nibble of its last 1
+// -- whole nibbles, across its words and through zero words, so no per-word partial nibble and zero
+// stretch -- then that last nibble's pixels, then (row's last lane) the zeros to the row end and the
+// end-of-row '1'. A table step is one LDS read whose high half is the next state (nib_st), so a step
+// costs a handful of VALU; states above 15 (sparse rows) take the pixel path for their nibble. The
+// boundaries depend on the lane's pixels alone, so eg_lane_walk2's meeting point is a boundary of every
+// walk of the lane. (bic_egad.hip, round 6: 2.97 ms -> see DESIGN.md §3.)
+#ifndef BIC_EGAD_CHAIN
+#define BIC_EGAD_CHAIN 1
+#endif
+constexpr bool kEgadChain = BIC_EGAD_CHAIN != 0;
+template <int WPL>
+struct LaneSpan {
+  uint32_t f1, l1;  // the lane's first and last 1 (columns); any = a 1 in the lane
+  bool any;
+};
+template <int WPL>
+__device__ __forceinline__ LaneSpan<WPL> lane_span(const EgLane<WPL>& L) {
+  LaneSpan<WPL> sp{0u, 0u, false};
+#pragma unroll
+  for (int t = WPL - 1; t >= 0; --t) {  // (backwards: the first nonzero word's f1 is the last written)
+    const uint64_t x = L.R[t];
+    if (x) {
+      const uint32_t w = L.w0 + t;
+      if (!sp.any) sp.l1 = w * 64 + 63 - (uint32_t)__builtin_ctzll(x);
+      sp.f1 = w * 64 + (uint32_t)__builtin_clzll(x);
+      sp.any = true;
+    }
+  }
+  return sp;
+}
+// the lane's nibble k (0 .. 16 WPL - 1), k uniform or not
+template <int WPL>
+__device__ __forceinline__ uint32_t lane_nib(const EgLane<WPL>& L, uint32_t k) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int t = 0; t < WPL; ++t) x = (k >> 4) == (uint32_t)t ? L.R[t] : x;
+  return (uint32_t)(x >> (60 - 4 * (k & 15))) & 15u;
+}
+// one step of state st over a whole nibble
+template <typename OUT>
+__device__ __forceinline__ uint32_t chain_step(uint32_t st, uint32_t nib, const uint64_t* T, OUT&& out) {
+  if ((int32_t)st < 0) {  // i > 15: pixel by pixel
+    NibCoder q{st_i(st), st_c(st)};
+    q.pixels(nib, 4, out);
+    return nib_st(q.i, q.c);
+  }
+  const uint64_t e = T[(st >> 16) + nib];
+  const uint32_t n = (uint32_t)(e >> 24) & 31u;
+  if (n) out((uint32_t)e & 0xFFFFFFu, n);
+  return (uint32_t)(e >> 32);
+}
+// eg_lane_nib's contract: the state after the lane's columns from start s (returns i); stop: return after
+// the step that ends at that column (one of this walk's boundaries)
+template <int WPL, typename OUT>
+__device__ __forceinline__ uint32_t eg_lane_walk(const EgLane<WPL>& L, uint32_t used, uint32_t cols, uint32_t s,
+                                                 const uint64_t* T, OUT&& out, uint32_t stop = 0xFFFFFFFFu) {
+  const LaneSpan<WPL> sp = lane_span(L);
+  NibCoder k{s, 0};
+  uint32_t col = (uint32_t)(L.jp + 1);
+  if (sp.any) {
+    const uint32_t a0 = sp.f1 & ~3u, base = L.w0 * 64;
+    if (a0 > col) {
+      k.zeros(a0 - col, out);
+      if (a0 >= stop) return k.i;
+    }
+    const uint32_t kf = (a0 - base) >> 2, kl = (sp.l1 - base) >> 2;
+    const bool cut = stop <= base + 4 * kl;  // stops after a whole nibble
+    const uint32_t ke = cut ? (stop - base) >> 2 : kl;
+    uint32_t st = nib_st(k.i, k.c);
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      uint64_t cur = L.R[t];
+#pragma unroll 1
+      for (uint32_t j = 0; j < 16; ++j, cur <<= 4) {
+        const uint32_t kk = 16 * t + j;
+        if (kk >= kf && kk < ke) st = chain_step(st, (uint32_t)(cur >> 60), T, out);
+      }
+    }
+    if (cut) return st_i(st);
+    NibCoder q{st_i(st), st_c(st)};
+    q.pixels(lane_nib(L, kl), (sp.l1 & 3u) + 1, out);
+    k = q;
+    col = sp.l1 + 1;
+    if (col >= stop) return k.i;
+  }
+  if (L.eol) {
+    k.zeros(cols - col, out);
+    if (cols >= stop) return k.i;
+    out(1u, 1);  // end of row (eg.cpp:30-32: no decBlockSize)
+  }
+  return k.i;
+}
+// eg_lane_nib2<WPL, true>'s contract over eg_lane_walk's boundaries: the walks from 0 and 31 together
+// until they hold the same state (X: the boundary where they first do; ~0: never), the walk from 0
+// counted (btot bits in all, bat before X)
+template <int WPL>
+__device__ __forceinline__ void eg_lane_walk2(const EgLane<WPL>& L, uint32_t used, uint32_t cols, const uint64_t* T,
+                                              uint32_t& lo, uint32_t& hi, uint32_t& X, uint32_t& btot, uint32_t& bat) {
+  const LaneSpan<WPL> sp = lane_span(L);
+  NibCoder k0{0, 0}, k1{31, 0};
+  bool met = false;
+  uint32_t nb0 = 0, mX = 0xFFFFFFFFu, mb = 0;
+  auto cnt = [&](uint32_t, uint32_t n) { nb0 += n; };
+  auto none = [](uint32_t, uint32_t) {};
+  auto check = [&](uint32_t pos, bool same) {
+    if (!met && same) {
+      met = true;
+      mX = pos;
+      mb = nb0;
+    }
+  };
+  uint32_t col = (uint32_t)(L.jp + 1);
+  if (sp.any) {
+    const uint32_t a0 = sp.f1 & ~3u, base = L.w0 * 64;
+    if (a0 > col) {
+      k0.zeros(a0 - col, cnt);
+      if (!met) k1.zeros(a0 - col, none);
+      check(a0, k0.i == k1.i && k0.c == k1.c);
+    }
+    const uint32_t kf = (a0 - base) >> 2, kl = (sp.l1 - base) >> 2;
+    uint32_t s0 = nib_st(k0.i, k0.c), s1 = nib_st(k1.i, k1.c);
+#pragma unroll
+    for (int t = 0; t < WPL; ++t) {
+      uint64_t cur = L.R[t];
+#pragma unroll 1
+      for (uint32_t j = 0; j < 16; ++j, cur <<= 4) {
+        const uint32_t kk = 16 * t + j;
+        if (kk >= kf && kk < kl) {
+          const uint32_t nib = (uint32_t)(cur >> 60);
+          s0 = chain_step(s0, nib, T, cnt);
+          if (!met) {
+            s1 = chain_step(s1, nib, T, none);
+            check(base + 4 * (kk + 1), s0 == s1);
+          }
+        }
+      }
+    }
+    const uint32_t nib = lane_nib(L, kl), n = (sp.l1 & 3u) + 1;
+    k0 = NibCoder{st_i(s0), st_c(s0)};
+    k0.pixels(nib, n, cnt);
+    k1 = NibCoder{st_i(s1), st_c(s1)};
+    if (!met) k1.pixels(nib, n, none);
+    col = sp.l1 + 1;
+    check(col, k0.i == k1.i && k0.c == k1.c);
+  }
+  if (L.eol) {
+    k0.zeros(cols - col, cnt);
+    if (!met) k1.zeros(cols - col, none);
+    check(cols, k0.i == k1.i && k0.c == k1.c);
+    cnt(1u, 1);
+  }
+  lo = k0.i;
+  hi = met ? k0.i : k1.i;
+  X = mX;
+  btot = nb0;
+  bat = mb;
+}
+
 // Every lane's start state for the row start s0 (lane 0 starts at s0): constant maps are known at
 // once; a round hands each known end to the next lane. Returns the lane's start; *end = its end.
 template <int WPL>
@@ -583,6 +753,7 @@ __device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t
       if (ident) sout = sin;
       else if (sin == 0 || sin == kFresh) sout = lo;  // (a fresh coder steps like index 0)
       else if (sin == 31) sout = hi;
+      else if constexpr (kEgadChain) sout = eg_lane_walk(L, used, cols, sin, T, [](uint32_t, uint32_t) {});
       else sout = eg_lane_nib(L, used, cols, sin, T, [](uint32_t, uint32_t) {});
       done = true;
     }
@@ -705,13 +876,17 @@ __global__ __launch_bounds__(256) void k_egad_llen(EgadArgs a) {
 #pragma unroll
   for (int t = 0; t < WPL; ++t) any |= L.R[t] != 0;
   uint32_t lo = kIdent, hi = kIdent, X = 0xFFFFFFFFu, btot = 0, bat = 0;
-  if (any) eg_lane_nib2<WPL, true>(L, a.used, a.cols, sT, lo, hi, &X, &btot, &bat);
+  if (any) {
+    if constexpr (kEgadChain) eg_lane_walk2(L, a.used, a.cols, sT, lo, hi, X, btot, bat);
+    else eg_lane_nib2<WPL, true>(L, a.used, a.cols, sT, lo, hi, &X, &btot, &bat);
+  }
   a.lane_lo[id * 64 + lane_id()] = (uint8_t)lo;
   uint32_t end;
   const uint32_t s = eg_lane_chain(L, a.used, a.cols, lo, hi, a.start[id], sT, &end);
   uint32_t bits = 0;
   if (lo != kIdent) {
-    (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t, uint32_t n) { bits += n; }, X);
+    if constexpr (kEgadChain) (void)eg_lane_walk(L, a.used, a.cols, s, sT, [&](uint32_t, uint32_t n) { bits += n; }, X);
+    else (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t, uint32_t n) { bits += n; }, X);
     if (X != 0xFFFFFFFFu) bits += btot - bat;
   }
   a.lane_st[id * 64 + lane_id()] = (uint8_t)s;
@@ -773,11 +948,14 @@ __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   uint32_t pos = wave_incl_sum_u32(bits) - bits;  // the lane's first bit in the row
   uint32_t s = a.lane_st[id * 64 + lane_id()];
   EgImgSink k{img, 0, 0, 0};
-  if (a.lane_lo[id * 64 + lane_id()] != kIdent)
-    (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t v, uint32_t n) {
+  if (a.lane_lo[id * 64 + lane_id()] != kIdent) {
+    auto sink = [&](uint32_t v, uint32_t n) {
       k.put(pos, v, n);
       pos += n;
-    });
+    };
+    if constexpr (kEgadChain) (void)eg_lane_walk(L, a.used, a.cols, s, sT, sink);
+    else (void)eg_lane_nib(L, a.used, a.cols, s, sT, sink);
+  }
   k.flush();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
