@@ -631,9 +631,20 @@ __device__ __forceinline__ uint32_t chain_step(uint32_t st, uint32_t nib, const 
   if (n) out((uint32_t)e & 0xFFFFFFu, n);
   return (uint32_t)(e >> 32);
 }
+// chain_step for a walk that writes nothing (the map walks): a state above 15 whose open block cannot
+// fill within the nibble (c + 4 < 2^J(i), J >= 4) steps in closed form -- each 1 lowers i by one and
+// the zeros after the last 1 open the next block (fewer than 4 < 8, the block size of any i' >= 12) --
+// so the walk from 31 leaves the pixel path after its first run instead of at i = 15
+__device__ __forceinline__ uint32_t chain_step_free(uint32_t st, uint32_t nib, const uint64_t* T) {
+  if ((int32_t)st < 0) {
+    const uint32_t i = st_i(st), c = st_c(st);
+    if (c + 4 < (1u << nib_j(i))) return nib_st(i - (uint32_t)__popc(nib), nib ? (uint32_t)__builtin_ctz(nib) : c + 4);
+  }
+  return chain_step(st, nib, T, [](uint32_t, uint32_t) {});
+}
 // eg_lane_nib's contract: the state after the lane's columns from start s (returns i); stop: return after
-// the step that ends at that column (one of this walk's boundaries)
-template <int WPL, typename OUT>
+// the step that ends at that column (one of this walk's boundaries). FREE: the walk writes nothing
+template <int WPL, bool FREE = false, typename OUT>
 __device__ __forceinline__ uint32_t eg_lane_walk(const EgLane<WPL>& L, uint32_t used, uint32_t cols, uint32_t s,
                                                  const uint64_t* T, OUT&& out, uint32_t stop = 0xFFFFFFFFu) {
   const LaneSpan<WPL> sp = lane_span(L);
@@ -655,7 +666,10 @@ __device__ __forceinline__ uint32_t eg_lane_walk(const EgLane<WPL>& L, uint32_t 
 #pragma unroll 1
       for (uint32_t j = 0; j < 16; ++j, cur <<= 4) {
         const uint32_t kk = 16 * t + j;
-        if (kk >= kf && kk < ke) st = chain_step(st, (uint32_t)(cur >> 60), T, out);
+        if (kk >= kf && kk < ke) {
+          if constexpr (FREE) st = chain_step_free(st, (uint32_t)(cur >> 60), T);
+          else st = chain_step(st, (uint32_t)(cur >> 60), T, out);
+        }
       }
     }
     if (cut) return st_i(st);
@@ -711,7 +725,7 @@ __device__ __forceinline__ void eg_lane_walk2(const EgLane<WPL>& L, uint32_t use
           const uint32_t nib = (uint32_t)(cur >> 60);
           s0 = chain_step(s0, nib, T, cnt);
           if (!met) {
-            s1 = chain_step(s1, nib, T, none);
+            s1 = chain_step_free(s1, nib, T);
             check(base + 4 * (kk + 1), s0 == s1);
           }
         }
@@ -753,7 +767,7 @@ __device__ __forceinline__ uint32_t eg_lane_chain(const EgLane<WPL>& L, uint32_t
       if (ident) sout = sin;
       else if (sin == 0 || sin == kFresh) sout = lo;  // (a fresh coder steps like index 0)
       else if (sin == 31) sout = hi;
-      else if constexpr (kEgadChain) sout = eg_lane_walk(L, used, cols, sin, T, [](uint32_t, uint32_t) {});
+      else if constexpr (kEgadChain) sout = eg_lane_walk<WPL, true>(L, used, cols, sin, T, [](uint32_t, uint32_t) {});
       else sout = eg_lane_nib(L, used, cols, sin, T, [](uint32_t, uint32_t) {});
       done = true;
     }
@@ -949,12 +963,27 @@ __global__ __launch_bounds__(256) void k_egad_lemit(EgadArgs a) {
   uint32_t s = a.lane_st[id * 64 + lane_id()];
   EgImgSink k{img, 0, 0, 0};
   if (a.lane_lo[id * 64 + lane_id()] != kIdent) {
-    auto sink = [&](uint32_t v, uint32_t n) {
-      k.put(pos, v, n);
-      pos += n;
-    };
-    if constexpr (kEgadChain) (void)eg_lane_walk(L, a.used, a.cols, s, sT, sink);
-    else (void)eg_lane_nib(L, a.used, a.cols, s, sT, sink);
+    if constexpr (kEgadChain) {
+      // codewords gathered 32 bits at a time in a register (acc's low nacc bits, nacc < 32 between
+      // calls), the image window touched once per 32 bits instead of once per codeword
+      uint64_t acc = 0;
+      uint32_t nacc = 0;
+      (void)eg_lane_walk(L, a.used, a.cols, s, sT, [&](uint32_t v, uint32_t n) {  // n <= 32
+        acc = (acc << n) | v;
+        nacc += n;
+        if (nacc >= 32) {
+          nacc -= 32;
+          k.put(pos, (uint32_t)(acc >> nacc), 32);
+          pos += 32;
+        }
+      });
+      if (nacc) k.put(pos, (uint32_t)acc, nacc);
+    } else {
+      (void)eg_lane_nib(L, a.used, a.cols, s, sT, [&](uint32_t v, uint32_t n) {
+        k.put(pos, v, n);
+        pos += n;
+      });
+    }
   }
   k.flush();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
