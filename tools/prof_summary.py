@@ -68,7 +68,7 @@ def main():
               "bitplanes_count": ["k_gray_strips"],
               "encode_finish": ["k_rows_global", "k_fixup"],
               "bitplanes_u8": ["k_bitplanes_u8"], "med_count": ["k_med_rows", "k_count", "k_plane_weight"],
-              "tiles": ["k_tiles_aligned", "k_tiles"], "golomb_samples": ["k_samp_scan", "k_samp_emit"],
+              "tiles": ["k_tiles_aligned", "k_tiles", "k_tiles_split"], "golomb_samples": ["k_samp_scan", "k_samp_emit"],
               "pack": ["k_pack"]}
     res["timers"] = {}
     K = res["kernels"]
