@@ -1917,7 +1917,10 @@ constexpr int kEmitWaves = 4;
 #ifndef BIC_REST_AUX
 #define BIC_REST_AUX 1
 #endif
-constexpr bool kRestAux = BIC_REST_AUX != 0;  // k_emit_rest on the context's second stream (beside k_emit_known)
+constexpr bool kRestAux = BIC_REST_AUX != 0;
+#ifndef BIC_REST_PRIO
+#define BIC_REST_PRIO 0  // (A/B: k_emit_rest's waves at s_setprio(N) beside the class kernels)
+#endif  // k_emit_rest on the context's second stream (beside k_emit_known)
 #ifndef BIC_CLASS_NT
 #define BIC_CLASS_NT 0
 #endif
@@ -2304,8 +2307,10 @@ __device__ __forceinline__ uint64_t cls_ld(const FusedArgs& a, uint64_t i) { ret
 // (8-byte lanes, pipelined batches of 3: C3 emission 162-165 -> 157-158 us; of 2: 159-162; of 4: 170-173.
 // Batches of 2 keep k_emit_k01 at <= 128 VGPRs (113; batches of 3: 129), which its rest role needs
 // (BIC_K01_REST: a fourth workgroup slot per CU beside three persistent ones). 16-byte lanes: 115 VGPRs
-// at batches of 2)
-#define BIC_K0_BATCH (BIC_K01_REST ? 2 : 3)
+// at batches of 2). Round 6: batches of 2 with four workgroups per CU (BIC_K01_OCC 4, 113 VGPRs) --
+// k_emit_k01 137 -> 132-137 us against 142-147 at batches of 3 and three per CU, same box
+// (profiles/r06/ab_emission.txt gj25, gj26); the C3 step unchanged (k_emit_rest beside it takes the slack)
+#define BIC_K0_BATCH 2
 #endif
 constexpr int kK0Batch = BIC_K0_BATCH;
 #ifndef BIC_DIAG_K0
@@ -2965,6 +2970,9 @@ __global__ __launch_bounds__(256) void k_emit_rest(FusedArgs a) {
   __shared__ uint32_t sh[16];  // (wide_prefix: up to 8 waves)
   __shared__ int sf[4];
   const int lane = lane_id(), v = (int)wave_id(), nw = blockDim.x >> 6;
+#if BIC_REST_PRIO
+  __builtin_amdgcn_s_setprio(BIC_REST_PRIO);  // (A/B: the listed rows' waves ahead in the issue arbitration)
+#endif
   if (DO_G)
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) s_lut[i] = reinterpret_cast<const uint32_t*>(a.lut + 256)[i];
   __syncthreads();
@@ -3063,7 +3071,8 @@ __device__ __forceinline__ void rest_role(const FusedArgs& a, uint32_t* lds, uin
 // starting on the k = 1 rows measured 196-198 µs against 192-193, round 4.)
 template <int WPL>
 #ifndef BIC_K01_OCC
-#define BIC_K01_OCC 0  // (A/B: a minimum of workgroups per CU for k_emit_k01; 0: none)
+#define BIC_K01_OCC 4  // a minimum of workgroups (one wave per SIMD each) per CU for k_emit_k01 (0: none;
+                       // the compiler then took 133 VGPRs, three per CU)
 #endif
 __global__ __launch_bounds__(256, BIC_K01_OCC ? BIC_K01_OCC : 1) void k_emit_k01(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kGImg];

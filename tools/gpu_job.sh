@@ -1,5 +1,5 @@
 # tools/gpu_job.sh: one GPU call of this session's A/B and diagnostic steps (edited per call)
 set -o pipefail
 export TMPDIR=/tmp
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/egad_prof -o run --output-format csv -- python3 tools/egad_only.py > gpurun_out/egad_prof.log 2>&1 || { tail -5 gpurun_out/egad_prof.log; exit 1; }
-grep '^{' gpurun_out/egad_prof.log | tail -2
+bash tools/ab.sh "--steps 20 --warmup 3" base o4 o4p1 o4p3 || exit 1
+bash tools/ab.sh "--steps 20 --warmup 3 --workload c4" base o4p1 o4p3
